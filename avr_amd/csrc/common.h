@@ -1,0 +1,83 @@
+// Shared device helpers for the AVR HIP library (gfx950).
+//
+// This translation unit family is compiled with -ffp-contract=off: every
+// a*b+c below is two roundings unless written as fmaf(), because the
+// reference's torch-CPU ops round each op separately
+// and the integer delays are sensitive to single-ulp differences.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+#include <string>
+
+#include "avr_hip.h"
+
+namespace avr {
+
+// ---------------------------------------------------------------- errors
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int check_launch(const char* what);
+
+#define AVR_REQUIRE(cond, msg)                          \
+    do {                                                \
+        if (!(cond)) return ::avr::fail(AVR_E_ARG, msg); \
+    } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------- dtypes
+__device__ __forceinline__ float load_f(const float* p, int64_t i) { return p[i]; }
+__device__ __forceinline__ float load_f(const __half* p, int64_t i) { return __half2float(p[i]); }
+__device__ __forceinline__ void store_f(float* p, int64_t i, float v) { p[i] = v; }
+__device__ __forceinline__ void store_f(__half* p, int64_t i, float v) { p[i] = __float2half(v); }
+
+// ---------------------------------------------------------------- geometry
+// torch.linspace(a, b, n)[i] on CPU: step = (b-a)/(n-1) in fp32, lower half
+// a + step*i, upper half b - step*(n-1-i), each a single fused rounding.
+__device__ __forceinline__ float linspace_at(float a, float b, int n, int i) {
+    if (n == 1) return a;
+    const float step = (b - a) / (float)(n - 1);
+    return (i < n / 2) ? fmaf(step, (float)i, a) : fmaf(-step, (float)(n - 1 - i), b);
+}
+
+// normalize_points (renderer.py:127-128): 2*(x-lo)/span - 1, op by op.
+__device__ __forceinline__ float to_unit(float x, float lo, float span) {
+    float y = x - lo;
+    y = 2.0f * y;
+    y = y / span;
+    return y - 1.0f;
+}
+
+// denormalize_points (renderer.py:130-131): (q+1)/2*span + lo, op by op.
+__device__ __forceinline__ float from_unit(float q, float lo, float span) {
+    float y = q + 1.0f;
+    y = y / 2.0f;
+    y = y * span;
+    return y + lo;
+}
+
+// Integer source delay of one ray-sample (renderer.py:55-58, 86-87):
+// world point o + dir*d, normalized; tx normalized; denormalized gap; norm
+// as torch's vector_norm reduces it (fma chain); *fs/speed; round-half-even;
+// clamp to [0, T-1].
+__device__ __forceinline__ int source_delay(const avr_render_params& p, const float o[3],
+                                            const float txn[3], const float dir[3], float d) {
+    float g[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float world = o[c] + dir[c] * d;
+        const float pn = to_unit(world, p.lo, p.span);
+        g[c] = from_unit(txn[c] - pn, p.lo, p.span);
+    }
+    const float n2 = fmaf(g[2], g[2], fmaf(g[1], g[1], g[0] * g[0]));
+    const float idx = (sqrtf(n2) * p.fs) / p.speed;
+    float r = rintf(idx);
+    r = fminf(fmaxf(r, 0.0f), (float)(p.T - 1));
+    return (int)r;
+}
+
+__host__ __device__ inline int n_rays(const avr_render_params& p) { return p.n_azi * p.n_ele + 2; }
+
+}  // namespace avr

@@ -1,0 +1,417 @@
+// Backward of the render hot path (a14): torch autograd through
+// renderer.py:86-121 restated as three kernels.
+//
+//   forward:  out[b,f] = sum_s phase[s,f] * sum_t z[b,s,t] * e^{-2 pi i f t/T}
+//             z[b,s,t] = pl[s,t]*tail[s,t] * sum_r w[b,r,s]*[t>=delay]*x[b,r,s,t]
+//   dft_phase_bwd:  gz[b,s,t] = pl*tail * dL/dz            (fp32 MFMA GEMM over f)
+//   ray_reduce_bwd: dL/dx = w*[t>=delay]*gz ;  dL/dw = sum_t [t>=delay]*gz*x
+//   weights_bwd:    adjoint of w = T_s*alpha_s (suffix affine scan) and of
+//                   alpha = 1-exp(-attn*dist)
+#include "common.h"
+
+using namespace avr;
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+// ----------------------------------------------------- adjoint DFT (MFMA)
+// gz[s,t] = sum_f U[s,f]*cos(2pi f t/T) + V[s,f]*sin(2pi f t/T), with
+//   U = gr*pc + gi*ps,  V = gr*ps - gi*pc   (g = dL/dout[b,f], ph = phase[s,f])
+// v_mfma_f32_16x16x4_f32: lane l feeds A[s=l&15][k=l>>4], B[k=l>>4][t=l&15];
+// the 4 k-slots of one instruction are (f, cos), (f, sin), (f+1, cos),
+// (f+1, sin).  A tile (U, V for 16 samples x 32 bins) is built in LDS; the
+// twiddle is gathered from the T-entry table by (t*f) mod T.
+constexpr int kBwdThreads = 256;
+constexpr int kFc = 32;  // bins per LDS stage
+
+__global__ __launch_bounds__(kBwdThreads) void dft_phase_bwd_kernel(
+    const float2* __restrict__ gout, const float* __restrict__ pl,
+    const int32_t* __restrict__ shift, const float2* __restrict__ phase,
+    const float2* __restrict__ twg, float* __restrict__ gz, int B, int S, int T) {
+    extern __shared__ float2 tw[];         // [T]  (cos, -sin)
+    __shared__ float Au[16][kFc + 1];      // U
+    __shared__ float Av[16][kFc + 1];      // -V  (pairs with the -sin table entry)
+    const int F = T / 2 + 1;
+    const int b = blockIdx.z;
+    const int s0 = blockIdx.y * 16;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int t = blockIdx.x * 64 + wave * 16 + (lane & 15);
+    const int tm = (t < T) ? t : 0;
+    const int kq = lane >> 4;            // 0..3
+    const int fo = kq >> 1, comp = kq & 1;
+    for (int i = threadIdx.x; i < T; i += kBwdThreads) tw[i] = twg[i];
+    floatx4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    const int inc = (int)((2LL * tm) % T);
+    for (int fc = 0; fc < F; fc += kFc) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < 16 * kFc; e += kBwdThreads) {
+            const int row = e / kFc, col = e % kFc;
+            const int s = s0 + row, f = fc + col;
+            float u = 0.0f, nv = 0.0f;
+            if (s < S && f < F) {
+                const float2 g = gout[(int64_t)b * F + f];
+                const float2 ph = phase[(int64_t)s * F + f];
+                u = g.x * ph.x + g.y * ph.y;
+                nv = -(g.x * ph.y - g.y * ph.x);
+            }
+            Au[row][col] = u;
+            Av[row][col] = nv;
+        }
+        __syncthreads();
+        int idx = (int)(((int64_t)(fc + fo) * tm) % T);
+#pragma unroll 4
+        for (int ff = 0; ff < kFc; ff += 2) {
+            const int r = lane & 15;
+            const float a = comp ? Av[r][ff + fo] : Au[r][ff + fo];
+            const float2 c = tw[idx];
+            const float bv = comp ? c.y : c.x;
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc, 0, 0, 0);
+            idx += inc;
+            if (idx >= T) idx -= T;
+        }
+    }
+    // C layout: col t = lane&15, rows s = 4*(lane>>4) + reg
+    if (t < T) {
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+            const int s = s0 + 4 * kq + reg;
+            if (s < S) {
+                const int sh = shift[s];
+                const float v = (t < T - 1 - sh) ? acc[reg] * pl[sh + t] : 0.0f;
+                gz[((int64_t)b * S + s) * T + t] = v;
+            }
+        }
+    }
+}
+
+// -------------------------------------------------- ray reduce backward
+// One row (b,r,s) per wavefront: the wave keeps gz[b,s,:] for its lanes'
+// t-chunks in registers and walks the rays of its split; per row it streams
+// x in, writes grad_x = w*[t>=d]*gz, and reduces grad_w with lane shuffles.
+// Boundary chunks (that straddle a neighbouring row) are stored per element.
+template <typename Tin>
+struct V16;
+template <>
+struct V16<float> {
+    static constexpr int N = 4;
+    using raw = float4;
+    __device__ static void load(const float* p, float* o) {
+        float4 v = *reinterpret_cast<const float4*>(p);
+        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    }
+    __device__ static void store(float* p, const float* o) {
+        *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+};
+template <>
+struct V16<__half> {
+    static constexpr int N = 8;
+    __device__ static void load(const __half* p, float* o) {
+        uint4 v = *reinterpret_cast<const uint4*>(p);
+        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float2 f = __half22float2(*reinterpret_cast<const __half2*>(&u[i]));
+            o[2 * i] = f.x;
+            o[2 * i + 1] = f.y;
+        }
+    }
+    __device__ static void store(__half* p, const float* o) {
+        uint32_t u[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            __half2 h = __floats2half2_rn(o[2 * i], o[2 * i + 1]);
+            u[i] = *reinterpret_cast<uint32_t*>(&h);
+        }
+        *reinterpret_cast<uint4*>(p) = make_uint4(u[0], u[1], u[2], u[3]);
+    }
+};
+
+constexpr int kRbThreads = 256;
+
+template <typename Tin, bool VECTOR, int CPL>
+__global__ __launch_bounds__(kRbThreads) void ray_reduce_bwd_kernel(
+    const Tin* __restrict__ sig, const float* __restrict__ gz, const float* __restrict__ w,
+    const int32_t* __restrict__ delay, Tin* __restrict__ gsig, float* __restrict__ gw, int B,
+    int R, int S, int T, int rays_per_block) {
+    constexpr int VEC = VECTOR ? V16<Tin>::N : 1;
+    const int split = blockIdx.x, s = blockIdx.y, b = blockIdx.z;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r0 = split * rays_per_block;
+    const int r1 = min(R, r0 + rays_per_block);
+    const int64_t row_stride = (int64_t)S * T;
+    const int64_t rowA = (((int64_t)b * R + r0) * S + s) * (int64_t)T;
+    const int phase = (int)(rowA % VEC);
+    const int nchunks = (T + phase + VEC - 1) / VEC;
+    // this lane's gz values
+    float g[CPL][VEC];
+    int t0[CPL];
+    const float* gzr = gz + ((int64_t)b * S + s) * T;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+        t0[c] = (lane + c * 64) * VEC - phase;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const int t = t0[c] + k;
+            g[c][k] = (t >= 0 && t < T) ? gzr[t] : 0.0f;
+        }
+    }
+    for (int r = r0 + wave; r < r1; r += kRbThreads / 64) {
+        const int64_t ridx = ((int64_t)b * R + r) * S + s;
+        const float wr = w[ridx];
+        const int dr = delay[ridx];
+        const int64_t rowbase = rowA + (int64_t)(r - r0) * row_stride - phase;
+        float dot = 0.0f;
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) {
+            const int j = lane + c * 64;
+            if (j >= nchunks) continue;
+            const int64_t e0 = rowbase + (int64_t)j * VEC;
+            const bool interior = VECTOR && t0[c] >= 0 && t0[c] + VEC <= T;
+            float x[VEC], o[VEC];
+            if (interior) {
+                V16<Tin>::load(sig + e0, x);
+            } else {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    const int t = t0[c] + k;
+                    x[k] = (t >= 0 && t < T) ? load_f(sig, e0 + k) : 0.0f;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const bool keep = (t0[c] + k) >= dr;
+                const float gk = keep ? g[c][k] : 0.0f;
+                o[k] = wr * gk;
+                dot = fmaf(gk, x[k], dot);
+            }
+            if (interior) {
+                if constexpr (VECTOR) V16<Tin>::store(gsig + e0, o);
+            } else {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    const int t = t0[c] + k;
+                    if (t >= 0 && t < T) store_f(gsig, e0 + k, o[k]);
+                }
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) dot += __shfl_xor(dot, off, 64);
+        if (lane == 0) gw[ridx] = dot;
+    }
+}
+
+// --------------------------------------------------- weights backward
+// Per ray (one wavefront), with f_k = (1-alpha_k)+1e-6, T_s = prod_{k<s} f_k:
+//   dL/dalpha_s = T_s * (gw_s - U_s),  U_s = sum_{j>s} gw_j alpha_j prod_{s<k<j} f_k
+//   U_{s-1} = gw_s alpha_s + f_s U_s  -> reverse affine scan over lanes
+//   dL/dattn_s = dL/dalpha_s * exp(-attn_s*dist_s) * dist_s
+template <typename Ta>
+__global__ void weights_bwd_kernel(avr_render_params p, int B, const Ta* __restrict__ attn,
+                                   const float* __restrict__ d_vals,
+                                   const float* __restrict__ grad_w, Ta* __restrict__ grad_attn,
+                                   int waves_per_block) {
+    extern __shared__ float lds[];
+    const int R = n_rays(p), S = p.n_samples;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t ray = (int64_t)blockIdx.x * waves_per_block + wave;
+    const bool active = ray < (int64_t)B * R;
+    float* alpha = lds + (int64_t)wave * 4 * S;
+    float* gwl = alpha + S;
+    float* ex = gwl + S;     // exp(-attn*dist)
+    float* dist = ex + S;
+    const int64_t base = ray * S;
+    if (active) {
+        for (int s = lane; s < S; s += 64) {
+            const float a = load_f(attn, base + s);
+            const float d = d_vals[s];
+            const float gap = (s + 1 < S) ? d_vals[s + 1] - d : 1e10f;
+            const float e = expf(-a * gap);
+            alpha[s] = 1.0f - e;
+            ex[s] = e;
+            dist[s] = gap;
+            gwl[s] = grad_w[base + s];
+        }
+    }
+    __syncthreads();
+    if (!active) return;
+    const int per = (S + 63) / 64;
+    const int s0 = min(S, lane * per), s1 = min(S, s0 + per);
+    // forward exclusive transmittance at the chunk start
+    float run = 1.0f;
+    for (int s = s0; s < s1; ++s) run = run * ((1.0f - alpha[s]) + 1e-6f);
+    float incl = run;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const float v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl = incl * v;
+    }
+    float trans0 = __shfl_up(incl, 1, 64);
+    if (lane == 0) trans0 = 1.0f;
+    // chunk composite of u -> a_s + m_s*u over s in [s0, s1), applied from the top
+    float ca = 0.0f, cm = 1.0f;
+    for (int s = s1 - 1; s >= s0; --s) {
+        const float a_s = gwl[s] * alpha[s];
+        const float m_s = (1.0f - alpha[s]) + 1e-6f;
+        ca = a_s + m_s * ca;
+        cm = m_s * cm;
+    }
+    // suffix composition over lanes: cur = mine o next o ... (shfl_down)
+    float qa = ca, qm = cm;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const float na = __shfl_down(qa, off, 64);
+        const float nm = __shfl_down(qm, off, 64);
+        if (lane + off < 64) {
+            qa = qa + qm * na;
+            qm = qm * nm;
+        }
+    }
+    float q = __shfl_down(qa, 1, 64);  // Q at s1 (value of U_{s1-1})
+    if (lane == 63) q = 0.0f;
+    // local transmittance for each s needs a forward walk; store per-s T in ex? keep
+    // a second pass: walk forward computing T_s, walk backward computing U_s.
+    // Use the gwl slot to hold dL/dalpha after the backward walk.
+    for (int s = s1 - 1; s >= s0; --s) {
+        const float u_s = q;  // U_s
+        q = gwl[s] * alpha[s] + ((1.0f - alpha[s]) + 1e-6f) * q;
+        gwl[s] = gwl[s] - u_s;  // (gw_s - U_s)
+    }
+    float tr = trans0;
+    for (int s = s0; s < s1; ++s) {
+        const float galpha = tr * gwl[s];
+        const float gatt = (galpha * ex[s]) * dist[s];
+        store_f(grad_attn, base + s, gatt);
+        tr = tr * ((1.0f - alpha[s]) + 1e-6f);
+    }
+}
+
+}  // namespace
+
+// ======================================================================
+// C-ABI
+// ======================================================================
+extern "C" int avr_dft_phase_bwd(const avr_render_params* p, int32_t B, const float* grad_out,
+                                 const float* pl_table, const int32_t* shift, const float* phase,
+                                 const float* twiddle, float* gz, void* stream) {
+    AVR_REQUIRE(p && B >= 1 && grad_out && pl_table && shift && phase && twiddle && gz,
+                "avr_dft_phase_bwd: bad args");
+    const int S = p->n_samples, T = p->T;
+    AVR_REQUIRE(T >= 2 && T <= 16384, "avr_dft_phase_bwd: T out of range");
+    const dim3 grid((T + 63) / 64, (S + 15) / 16, B);
+    const size_t lds = (size_t)T * sizeof(float2);
+    hipLaunchKernelGGL(dft_phase_bwd_kernel, grid, dim3(kBwdThreads), lds, as_stream(stream),
+                       reinterpret_cast<const float2*>(grad_out), pl_table, shift,
+                       reinterpret_cast<const float2*>(phase),
+                       reinterpret_cast<const float2*>(twiddle), gz, (int)B, S, T);
+    return check_launch("avr_dft_phase_bwd");
+}
+
+namespace {
+template <typename Tin, bool VECTOR>
+int launch_rb(const avr_render_params* p, int B, const void* sig, const float* gz, const float* w,
+              const int32_t* delay, void* gsig, float* gw, hipStream_t st) {
+    constexpr int VEC = VECTOR ? V16<Tin>::N : 1;
+    const int R = n_rays(*p), S = p->n_samples, T = p->T;
+    const int nch = (T + 2 * VEC - 2) / VEC;
+    const int cpl = (nch + 63) / 64;
+    // ~4 rows per wave per block; enough blocks to fill the chip
+    int rpb = 16;
+    const int64_t cols = (int64_t)B * S;
+    while (rpb > 4 && cols * ((R + rpb - 1) / rpb) < 2048) rpb /= 2;
+    const dim3 grid((R + rpb - 1) / rpb, S, B);
+    const Tin* x = (const Tin*)sig;
+    Tin* gx = (Tin*)gsig;
+#define AVR_RB(C)                                                                                \
+    case C:                                                                                      \
+        hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, C>), grid, dim3(kRbThreads), 0, st, \
+                           x, gz, w, delay, gx, gw, B, R, S, T, rpb);                            \
+        break;
+    switch (cpl) {
+        AVR_RB(1) AVR_RB(2) AVR_RB(3) AVR_RB(4) AVR_RB(5) AVR_RB(6) AVR_RB(8) AVR_RB(12) AVR_RB(16)
+        AVR_RB(24) AVR_RB(32) AVR_RB(48) AVR_RB(64)
+        default:
+            if (cpl == 7) {
+                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 8>), grid, dim3(kRbThreads), 0,
+                                   st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
+            } else if (cpl <= 12) {
+                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 12>), grid, dim3(kRbThreads),
+                                   0, st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
+            } else if (cpl <= 16) {
+                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 16>), grid, dim3(kRbThreads),
+                                   0, st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
+            } else if (cpl <= 24) {
+                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 24>), grid, dim3(kRbThreads),
+                                   0, st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
+            } else if (cpl <= 32) {
+                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 32>), grid, dim3(kRbThreads),
+                                   0, st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
+            } else if (cpl <= 48) {
+                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 48>), grid, dim3(kRbThreads),
+                                   0, st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
+            } else if (cpl <= 64) {
+                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 64>), grid, dim3(kRbThreads),
+                                   0, st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
+            } else {
+                return fail(AVR_E_CONFIG, "ray_reduce_bwd: T too long");
+            }
+    }
+#undef AVR_RB
+    return check_launch("avr_ray_reduce_bwd");
+}
+}  // namespace
+
+extern "C" int avr_ray_reduce_bwd(const avr_render_params* p, int32_t B, const void* signal,
+                                  int32_t sig_dtype, const float* gz, const float* w,
+                                  const int32_t* delay, void* grad_signal, float* grad_w,
+                                  void* stream) {
+    AVR_REQUIRE(p && B >= 1 && signal && gz && w && delay && grad_signal && grad_w,
+                "avr_ray_reduce_bwd: bad args");
+    AVR_REQUIRE(p->T >= 2 && p->T <= 16384, "avr_ray_reduce_bwd: T out of range");
+    const int64_t st = (int64_t)p->n_samples * p->T;
+    const bool aligned = (reinterpret_cast<uintptr_t>(signal) % 16) == 0 &&
+                         (reinterpret_cast<uintptr_t>(grad_signal) % 16) == 0;
+    hipStream_t s = as_stream(stream);
+    if (sig_dtype == AVR_DTYPE_F32) {
+        if (aligned && st % 4 == 0)
+            return launch_rb<float, true>(p, B, signal, gz, w, delay, grad_signal, grad_w, s);
+        return launch_rb<float, false>(p, B, signal, gz, w, delay, grad_signal, grad_w, s);
+    }
+    if (sig_dtype == AVR_DTYPE_F16) {
+        if (aligned && st % 8 == 0)
+            return launch_rb<__half, true>(p, B, signal, gz, w, delay, grad_signal, grad_w, s);
+        return launch_rb<__half, false>(p, B, signal, gz, w, delay, grad_signal, grad_w, s);
+    }
+    return fail(AVR_E_ARG, "avr_ray_reduce_bwd: unknown signal dtype");
+}
+
+extern "C" int avr_weights_bwd(const avr_render_params* p, int32_t B, const void* attn,
+                               int32_t attn_dtype, const float* d_vals, const float* grad_w,
+                               void* grad_attn, void* stream) {
+    AVR_REQUIRE(p && B >= 1 && attn && d_vals && grad_w && grad_attn, "avr_weights_bwd: bad args");
+    const int S = p->n_samples;
+    AVR_REQUIRE(S >= 1 && S <= 8192, "avr_weights_bwd: n_samples out of range");
+    const int wpb = (S <= 1024) ? 4 : 1;
+    const int64_t rays = (int64_t)B * n_rays(*p);
+    const dim3 grid((unsigned)((rays + wpb - 1) / wpb));
+    const size_t lds = (size_t)wpb * 4 * S * sizeof(float);
+    if (lds > 65536) {
+        if (attn_dtype == AVR_DTYPE_F32)
+            (void)hipFuncSetAttribute((const void*)weights_bwd_kernel<float>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        else
+            (void)hipFuncSetAttribute((const void*)weights_bwd_kernel<__half>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
+    if (attn_dtype == AVR_DTYPE_F32)
+        hipLaunchKernelGGL(weights_bwd_kernel<float>, grid, dim3(64 * wpb), lds, as_stream(stream),
+                           *p, (int)B, (const float*)attn, d_vals, grad_w, (float*)grad_attn, wpb);
+    else if (attn_dtype == AVR_DTYPE_F16)
+        hipLaunchKernelGGL(weights_bwd_kernel<__half>, grid, dim3(64 * wpb), lds,
+                           as_stream(stream), *p, (int)B, (const __half*)attn, d_vals, grad_w,
+                           (__half*)grad_attn, wpb);
+    else
+        return fail(AVR_E_ARG, "avr_weights_bwd: unknown attn dtype");
+    return check_launch("avr_weights_bwd");
+}

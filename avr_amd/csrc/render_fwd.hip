@@ -1,0 +1,668 @@
+// Forward render hot path for MI355X (gfx950): tables, ray generation,
+// network-input sampling, compositing weights, the HBM ray-reduction stream,
+// the fp32-MFMA DFT with fused phase epilogue, and the irfft to the IR.
+//
+// Reference: renderer.py:31-193 (AVRRender.forward, ray_directions,
+// acoustic_render) and utils/criterion.py:71 (irfft).  See DESIGN.md for the
+// reordering (sum over rays in the time domain before the transform) and the
+// roofline of each kernel.
+#include "common.h"
+
+using namespace avr;
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr double kTwoPi = 6.283185307179586476925286766559;
+
+// ------------------------------------------------------------------ tables
+// d_vals/frac/shift: renderer.py:54, 79-80.  Path loss: renderer.py:95-98
+// (arange/fs*speed + 1e-3, then pathloss * reciprocal, the near-field entries
+// copied from index near_clamp+1).  Phase: renderer.py:108, theta =
+// fp32(fp32(c*f)*frac[s]), exp(i*theta).  Twiddles in double, rounded once.
+__global__ void tables_kernel(avr_render_params p, float* __restrict__ d_vals,
+                              float* __restrict__ frac, int32_t* __restrict__ shift,
+                              float* __restrict__ pl, float2* __restrict__ phase,
+                              float2* __restrict__ tw) {
+    const int S = p.n_samples, T = p.T, F = T / 2 + 1;
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = gid; i < S; i += stride) {
+        const float d = linspace_at(0.0f, 1.0f, S, (int)i) * p.depth_scale + p.depth_offset;
+        const float fr = (p.fs * d) / p.speed;
+        d_vals[i] = d;
+        frac[i] = fr;
+        shift[i] = (int32_t)rintf(fr);
+    }
+    for (int64_t i = gid; i < p.pl_len; i += stride) {
+        const int k = (i < p.near_clamp) ? p.near_clamp + 1 : (int)i;
+        const float dist = ((float)k / p.fs) * p.speed;
+        const float den = dist + 1e-3f;
+        pl[i] = p.pathloss * (1.0f / den);
+    }
+    for (int64_t i = gid; i < (int64_t)S * F; i += stride) {
+        const int s = (int)(i / F), f = (int)(i % F);
+        const float d = linspace_at(0.0f, 1.0f, S, s) * p.depth_scale + p.depth_offset;
+        const float fr = (p.fs * d) / p.speed;
+        const float cf = p.phase_c * (float)f;
+        const float th = cf * fr;
+        phase[i] = make_float2((float)cos((double)th), (float)sin((double)th));
+    }
+    for (int64_t k = gid; k < T; k += stride) {
+        const double a = kTwoPi * (double)k / (double)T;
+        tw[k] = make_float2((float)cos(a), (float)(-sin(a)));
+    }
+}
+
+__global__ void depth_samples_kernel(avr_render_params p, float* __restrict__ d_vals) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < p.n_samples)
+        d_vals[s] = linspace_at(0.0f, 1.0f, p.n_samples, s) * p.depth_scale + p.depth_offset;
+}
+
+__global__ void ir_twiddle_kernel(int n, float2* __restrict__ tw) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const double a = kTwoPi * (double)k / (double)n;
+        tw[k] = make_float2((float)cos(a), (float)sin(a));
+    }
+}
+
+// ------------------------------------------------------------- a2: rays
+// renderer.py:147-165: azimuth linspace + jitter, elevation acos ring,
+// meshgrid(ij) azimuth-major, then the two poles.  Trig in double, rounded
+// once (the reference uses SLEEF u10; components may differ by 1 ulp).
+__global__ void ray_directions_kernel(avr_render_params p, const float* __restrict__ u_azi,
+                                      float* __restrict__ dirs) {
+    const int R = n_rays(p);
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    float x, y, z;
+    const int grid = p.n_azi * p.n_ele;
+    if (r < grid) {
+        const int ia = r / p.n_ele, ie = r % p.n_ele;
+        const float base = linspace_at(0.0f, p.two_pi, p.n_azi + 1, ia);
+        const float jit = p.azi_jitter * u_azi[ia];
+        const float azi = base + jit;
+        const float el_lin = linspace_at(0.0f, 1.0f, p.n_ele + 2, ie + 1);
+        const float el_arg = 2.0f * el_lin - 1.0f;
+        const float ele = (float)acos((double)el_arg);
+        const float se = (float)sin((double)ele);
+        x = (float)cos((double)azi) * se;
+        y = (float)sin((double)azi) * se;
+        z = (float)cos((double)ele);
+    } else {
+        x = 0.0f;
+        y = 0.0f;
+        z = (r == grid) ? 1.0f : -1.0f;
+    }
+    dirs[r * 3 + 0] = x;
+    dirs[r * 3 + 1] = y;
+    dirs[r * 3 + 2] = z;
+}
+
+// ------------------------------------------------- a3/a4: network inputs
+// renderer.py:54-62: pts = norm(o + dir*d), view = -dir, tx = norm(tx),
+// dir_tx broadcast.  One thread per ray-sample, [B][R*S][3] outputs.
+__global__ void sample_points_kernel(avr_render_params p, int B, const float* __restrict__ rays_o,
+                                     const float* __restrict__ pos_tx,
+                                     const float* __restrict__ dir_tx,
+                                     const float* __restrict__ dirs,
+                                     const float* __restrict__ d_vals, float* __restrict__ net_pts,
+                                     float* __restrict__ net_view, float* __restrict__ net_tx,
+                                     float* __restrict__ net_dir_tx) {
+    const int R = n_rays(p), S = p.n_samples;
+    const int64_t n = (int64_t)B * R * S;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int s = (int)(i % S);
+        const int64_t br = i / S;
+        const int r = (int)(br % R);
+        const int b = (int)(br / R);
+        const float d = d_vals[s];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float dc = dirs[r * 3 + c];
+            const float world = rays_o[b * 3 + c] + dc * d;
+            net_pts[i * 3 + c] = to_unit(world, p.lo, p.span);
+            net_view[i * 3 + c] = -dc;
+            net_tx[i * 3 + c] = to_unit(pos_tx[b * 3 + c], p.lo, p.span);
+            if (dir_tx) net_dir_tx[i * 3 + c] = dir_tx[b * 3 + c];
+        }
+    }
+}
+
+// ------------------------------------- a8 + a11: delays and the weights
+// One ray per wavefront; samples strided over the 64 lanes for coalesced
+// attn loads, alpha staged in LDS, then each lane owns a contiguous run of
+// samples for the exclusive transmittance product (renderer.py:185-192):
+//   alpha = 1 - exp(-attn*dist), dist = d[s+1]-d[s] (last 1e10)
+//   T_s = prod_{k<s} ((1-alpha_k) + 1e-6), w = T_s * alpha_s
+// The cross-lane part is a multiplicative shuffle scan (6 steps).
+template <typename Ta>
+__global__ __launch_bounds__(256) void weights_fwd_kernel(
+    avr_render_params p, int B, const Ta* __restrict__ attn, const float* __restrict__ rays_o,
+    const float* __restrict__ pos_tx, const float* __restrict__ dirs,
+    const float* __restrict__ d_vals, float* __restrict__ w_out, int32_t* __restrict__ delay) {
+    extern __shared__ float lds_alpha[];
+    const int R = n_rays(p), S = p.n_samples;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t ray = (int64_t)blockIdx.x * 4 + wave;  // flattened (b, r)
+    const bool active = ray < (int64_t)B * R;
+    float* alpha = lds_alpha + wave * S;
+    if (active) {
+        const int b = (int)(ray / R), r = (int)(ray % R);
+        float o[3], txn[3], dir[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            o[c] = rays_o[b * 3 + c];
+            txn[c] = to_unit(pos_tx[b * 3 + c], p.lo, p.span);
+            dir[c] = dirs[r * 3 + c];
+        }
+        const int64_t base = ray * S;
+        for (int s = lane; s < S; s += 64) {
+            const float a = load_f(attn, base + s);
+            const float d = d_vals[s];
+            const float gap = (s + 1 < S) ? d_vals[s + 1] - d : 1e10f;
+            alpha[s] = 1.0f - expf(-a * gap);
+            delay[base + s] = source_delay(p, o, txn, dir, d);
+        }
+    }
+    __syncthreads();
+    if (!active) return;
+    const int64_t base = ray * S;
+    const int per = (S + 63) / 64;
+    const int s0 = min(S, lane * per), s1 = min(S, s0 + per);
+    float run = 1.0f;
+    for (int s = s0; s < s1; ++s) run = run * ((1.0f - alpha[s]) + 1e-6f);
+    // inclusive multiplicative scan over lanes, then shift to exclusive
+    float incl = run;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const float v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl = incl * v;
+    }
+    float trans = __shfl_up(incl, 1, 64);
+    if (lane == 0) trans = 1.0f;
+    for (int s = s0; s < s1; ++s) {
+        const float al = alpha[s];
+        w_out[base + s] = trans * al;
+        trans = trans * ((1.0f - al) + 1e-6f);
+    }
+}
+
+// --------------------------------------------- the HBM stream: ray reduce
+// part[k][b][s][t] = sum_{r in split k} w[b,r,s] * [t >= delay[b,r,s]] * x[b,r,s,t]
+// One workgroup per (split, s, b); each row (b,r,s) of T contiguous elements
+// is read once with 16-byte loads.  Because S*T is a multiple of VEC, every
+// row of one (b,s) column has the same alignment phase, so a lane's register
+// accumulators always see the same t indices.  The per-ray w/delay of the
+// split are gathered into LDS once.
+template <typename Tin>
+struct Vec16;
+template <>
+struct Vec16<float> {
+    static constexpr int N = 4;
+    using raw = float4;
+    __device__ static void cvt(const raw& v, float* o) {
+        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    }
+};
+template <>
+struct Vec16<__half> {
+    static constexpr int N = 8;
+    using raw = uint4;
+    __device__ static void cvt(const raw& v, float* o) {
+        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            __half2 h = *reinterpret_cast<const __half2*>(&u[i]);
+            float2 f = __half22float2(h);
+            o[2 * i] = f.x;
+            o[2 * i + 1] = f.y;
+        }
+    }
+};
+
+constexpr int kReduceThreads = 256;
+constexpr int kMaxRaysPerSplit = 2048;
+constexpr int kUnroll = 4;
+
+template <typename Tin, bool VECTOR, int CPT>
+__global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
+    const Tin* __restrict__ sig, const float* __restrict__ w, const int32_t* __restrict__ delay,
+    float* __restrict__ part, int B, int R, int S, int T, int rays_per_split, int64_t total) {
+    constexpr int VEC = VECTOR ? Vec16<Tin>::N : 1;
+    __shared__ float w_l[kMaxRaysPerSplit];
+    __shared__ int d_l[kMaxRaysPerSplit];
+    const int split = blockIdx.x, s = blockIdx.y, b = blockIdx.z;
+    const int r0 = split * rays_per_split;
+    const int nr = min(R, r0 + rays_per_split) - r0;
+    for (int i = threadIdx.x; i < nr; i += kReduceThreads) {
+        const int64_t idx = ((int64_t)b * R + r0 + i) * S + s;
+        w_l[i] = w[idx];
+        d_l[i] = delay[idx];
+    }
+    __syncthreads();
+    if (nr <= 0) return;
+    const int64_t row0 = (((int64_t)b * R + r0) * S + s) * (int64_t)T;
+    const int phase = (int)(row0 % VEC);
+    const int nchunks = (T + phase + VEC - 1) / VEC;
+    const int64_t row_stride = (int64_t)S * T;
+
+    float acc[CPT][VEC];
+    int t0[CPT];
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+        t0[c] = (threadIdx.x + c * kReduceThreads) * VEC - phase;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) acc[c][k] = 0.0f;
+    }
+
+    auto load_chunk = [&](int64_t rowbase, int c, float* x) {
+        const int j = threadIdx.x + c * kReduceThreads;
+        if (j >= nchunks) {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) x[k] = 0.0f;
+            return;
+        }
+        const int64_t e0 = rowbase + (int64_t)j * VEC;  // first element of the chunk
+        if constexpr (VECTOR) {
+            if (e0 + VEC <= total) {
+                typename Vec16<Tin>::raw v =
+                    *reinterpret_cast<const typename Vec16<Tin>::raw*>(sig + e0);
+                Vec16<Tin>::cvt(v, x);
+                return;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) x[k] = (e0 + k < total) ? load_f(sig, e0 + k) : 0.0f;
+    };
+
+    int r = 0;
+    for (; r + kUnroll <= nr; r += kUnroll) {
+        float x[kUnroll][CPT][VEC];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const int64_t rowbase = row0 + (int64_t)(r + u) * row_stride - phase;
+#pragma unroll
+            for (int c = 0; c < CPT; ++c) load_chunk(rowbase, c, x[u][c]);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+            const float wr = w_l[r + u];
+            const int dr = d_l[r + u];
+#pragma unroll
+            for (int c = 0; c < CPT; ++c)
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    const float wm = (t0[c] + k >= dr) ? wr : 0.0f;
+                    acc[c][k] = fmaf(wm, x[u][c][k], acc[c][k]);
+                }
+        }
+    }
+    for (; r < nr; ++r) {
+        const int64_t rowbase = row0 + (int64_t)r * row_stride - phase;
+        const float wr = w_l[r];
+        const int dr = d_l[r];
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            float x[VEC];
+            load_chunk(rowbase, c, x);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const float wm = (t0[c] + k >= dr) ? wr : 0.0f;
+                acc[c][k] = fmaf(wm, x[k], acc[c][k]);
+            }
+        }
+    }
+    float* out = part + (((int64_t)split * B + b) * S + s) * (int64_t)T;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const int t = t0[c] + k;
+            if (t >= 0 && t < T) out[t] = acc[c][k];
+        }
+}
+
+// ------------------------------- DFT + phase + sum over samples (MFMA f32)
+// C[s, (f,re|im)] = sum_t z[b,s,t] * tw[(t*f) mod T]  with v_mfma_f32_32x32x2_f32
+// (exact fp32 FMA chain).  A = z tile staged in LDS (32 samples x 64 t),
+// built on the fly from the ray-reduce partials with path loss and the tail
+// mask applied; B = twiddles gathered from a 1-D table of T complex values
+// in LDS by the index (t*f) mod T, advanced incrementally.  Epilogue: rotate
+// by phase[s,f] and reduce the 32 sample rows; partials per (s-tile, k-slice)
+// are summed by avr_spectrum_finalize.
+constexpr int kDftThreads = 256;
+constexpr int kKc = 64;  // t per LDS stage
+
+__global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
+    const float* __restrict__ part, int n_split, const float* __restrict__ pl,
+    const int32_t* __restrict__ shift, const float2* __restrict__ phase,
+    const float2* __restrict__ twg, float2* __restrict__ spart, int B, int S, int T, int KS,
+    int kchunk) {
+    extern __shared__ float2 tw[];           // [T]
+    __shared__ float As[32][kKc + 1];
+    const int F = T / 2 + 1;
+    const int P = ((S + 31) / 32) * KS;
+    const int b = blockIdx.z;
+    const int stile = blockIdx.y / KS, ks = blockIdx.y % KS;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int fbase = blockIdx.x * 128 + wave * 32;
+    const int f = fbase + (lane & 31);
+    const int fm = (f < F) ? f : 0;
+    const int half = lane >> 5;
+    for (int i = threadIdx.x; i < T; i += kDftThreads) tw[i] = twg[i];
+
+    const int k0 = ks * kchunk;
+    const int k1 = min(T, k0 + kchunk);
+    floatx16 acc_re, acc_im;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        acc_re[i] = 0.0f;
+        acc_im[i] = 0.0f;
+    }
+    const int64_t slab = (int64_t)B * S * T;
+    const int inc = (int)((2LL * fm) % T);
+    for (int kc = k0; kc < k1; kc += kKc) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < 32 * kKc; e += kDftThreads) {
+            const int row = e / kKc, col = e % kKc;
+            const int s = stile * 32 + row, t = kc + col;
+            float v = 0.0f;
+            if (s < S && t < k1) {
+                const int sh = shift[s];
+                if (t < T - 1 - sh) {
+                    const float* src = part + ((int64_t)b * S + s) * T + t;
+                    float sum = 0.0f;
+                    for (int k = 0; k < n_split; ++k) sum += src[k * slab];
+                    v = sum * pl[sh + t];
+                }
+            }
+            As[row][col] = v;
+        }
+        __syncthreads();
+        int idx = (int)(((int64_t)(kc + half) * fm) % T);
+#pragma unroll 8
+        for (int kk = 0; kk < kKc; kk += 2) {
+            const float a = As[lane & 31][kk + half];
+            const float2 c = tw[idx];
+            acc_re = __builtin_amdgcn_mfma_f32_32x32x2f32(a, c.x, acc_re, 0, 0, 0);
+            acc_im = __builtin_amdgcn_mfma_f32_32x32x2f32(a, c.y, acc_im, 0, 0, 0);
+            idx += inc;
+            if (idx >= T) idx -= T;
+        }
+    }
+    // epilogue: rows (reg&3) + 8*(reg>>2) + 4*half, column lane&31
+    float re = 0.0f, im = 0.0f;
+    if (f < F) {
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int s = stile * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * half;
+            if (s < S) {
+                const float2 ph = phase[(int64_t)s * F + f];
+                const float zr = acc_re[reg], zi = acc_im[reg];
+                re += zr * ph.x - zi * ph.y;
+                im += zr * ph.y + zi * ph.x;
+            }
+        }
+    }
+    re += __shfl_xor(re, 32, 64);
+    im += __shfl_xor(im, 32, 64);
+    if (half == 0 && f < F) {
+        spart[((int64_t)b * P + stile * KS + ks) * F + f] = make_float2(re, im);
+    }
+}
+
+__global__ void spectrum_finalize_kernel(int B, int P, int F, const float2* __restrict__ spart,
+                                         float2* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)B * F) return;
+    const int b = (int)(i / F), f = (int)(i % F);
+    float re = 0.0f, im = 0.0f;
+    const float2* src = spart + (int64_t)b * P * F + f;
+    for (int q = 0; q < P; ++q) {
+        const float2 v = src[(int64_t)q * F];
+        re += v.x;
+        im += v.y;
+    }
+    out[i] = make_float2(re, im);
+}
+
+// -------------------------------------------------- a13: irfft -> IR
+// torch.fft.irfft semantics (n = 2(F-1), backward norm 1/n, imaginary parts
+// of the DC and Nyquist bins ignored):
+//   ir[t] = (X0 + (-1)^t X_{n/2} + 2 sum_{k=1}^{n/2-1} Re(X_k e^{2 pi i k t/n})) / n
+__global__ __launch_bounds__(256) void irfft_kernel(int F, const float2* __restrict__ spec,
+                                                    const float2* __restrict__ twg,
+                                                    float* __restrict__ ir) {
+    extern __shared__ float2 lds[];
+    const int n = 2 * (F - 1);
+    float2* X = lds;       // [F]
+    float2* tw = lds + F;  // [n]
+    const int b = blockIdx.y;
+    for (int i = threadIdx.x; i < F; i += blockDim.x) X[i] = spec[(int64_t)b * F + i];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) tw[i] = twg[i];
+    __syncthreads();
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    float acc = 0.0f;
+    int idx = t % n;  // k = 1
+    for (int k = 1; k < F - 1; ++k) {
+        const float2 c = tw[idx];
+        const float2 x = X[k];
+        acc += x.x * c.x - x.y * c.y;
+        idx += t;
+        if (idx >= n) idx -= n;
+    }
+    const float nyq = (t & 1) ? -X[F - 1].x : X[F - 1].x;
+    const float v = (X[0].x + nyq) + 2.0f * acc;
+    ir[(int64_t)b * n + t] = v / (float)n;
+}
+
+int pick_blocks(int64_t n, int threads, int cap = 4096) {
+    int64_t g = (n + threads - 1) / threads;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+int validate(const avr_render_params* p) {
+    if (!p) return fail(AVR_E_ARG, "null params");
+    if (p->n_azi < 1 || p->n_ele < 1 || p->n_samples < 1 || p->T < 2)
+        return fail(AVR_E_CONFIG, "n_azi, n_ele, n_samples must be >=1 and T >= 2");
+    if (p->T > 16384) return fail(AVR_E_CONFIG, "T > 16384 not supported");
+    if (p->n_samples > 8192) return fail(AVR_E_CONFIG, "n_samples > 8192 not supported");
+    return 0;
+}
+
+}  // namespace
+
+// ======================================================================
+// C-ABI
+// ======================================================================
+extern "C" int avr_tables(const avr_render_params* p, float* d_vals, float* frac, int32_t* shift,
+                          float* pl_table, float* phase, float* twiddle, void* stream) {
+    if (int e = validate(p)) return e;
+    AVR_REQUIRE(d_vals && frac && shift && pl_table && phase && twiddle, "avr_tables: null pointer");
+    const int64_t work = (int64_t)p->n_samples * (p->T / 2 + 1);
+    hipLaunchKernelGGL(tables_kernel, dim3(pick_blocks(work, 256, 1024)), dim3(256), 0,
+                       as_stream(stream), *p, d_vals, frac, shift, pl_table,
+                       reinterpret_cast<float2*>(phase), reinterpret_cast<float2*>(twiddle));
+    return check_launch("avr_tables");
+}
+
+extern "C" int avr_depth_samples(const avr_render_params* p, float* d_vals, void* stream) {
+    AVR_REQUIRE(p && p->n_samples >= 1 && d_vals, "avr_depth_samples: bad args");
+    hipLaunchKernelGGL(depth_samples_kernel, dim3((p->n_samples + 255) / 256), dim3(256), 0,
+                       as_stream(stream), *p, d_vals);
+    return check_launch("avr_depth_samples");
+}
+
+extern "C" int avr_ir_twiddle(int32_t n, float* tw, void* stream) {
+    AVR_REQUIRE(n >= 2 && tw, "avr_ir_twiddle: bad args");
+    hipLaunchKernelGGL(ir_twiddle_kernel, dim3(pick_blocks(n, 256, 256)), dim3(256), 0,
+                       as_stream(stream), n, reinterpret_cast<float2*>(tw));
+    return check_launch("avr_ir_twiddle");
+}
+
+extern "C" int avr_ray_directions(const avr_render_params* p, const float* u_azi, float* dirs,
+                                  void* stream) {
+    if (int e = validate(p)) return e;
+    AVR_REQUIRE(u_azi && dirs, "avr_ray_directions: null pointer");
+    const int R = n_rays(*p);
+    hipLaunchKernelGGL(ray_directions_kernel, dim3((R + 255) / 256), dim3(256), 0,
+                       as_stream(stream), *p, u_azi, dirs);
+    return check_launch("avr_ray_directions");
+}
+
+extern "C" int avr_sample_points(const avr_render_params* p, int32_t B, const float* rays_o,
+                                 const float* pos_tx, const float* dir_tx, const float* dirs,
+                                 const float* d_vals, float* net_pts, float* net_view,
+                                 float* net_tx, float* net_dir_tx, void* stream) {
+    if (int e = validate(p)) return e;
+    AVR_REQUIRE(B >= 1 && rays_o && pos_tx && dirs && d_vals && net_pts && net_view && net_tx,
+                "avr_sample_points: bad args");
+    AVR_REQUIRE(!dir_tx || net_dir_tx, "avr_sample_points: dir_tx given without net_dir_tx");
+    const int64_t n = (int64_t)B * n_rays(*p) * p->n_samples;
+    hipLaunchKernelGGL(sample_points_kernel, dim3(pick_blocks(n, 256, 8192)), dim3(256), 0,
+                       as_stream(stream), *p, (int)B, rays_o, pos_tx, dir_tx, dirs, d_vals,
+                       net_pts, net_view, net_tx, dir_tx ? net_dir_tx : nullptr);
+    return check_launch("avr_sample_points");
+}
+
+extern "C" int avr_weights_fwd(const avr_render_params* p, int32_t B, const void* attn,
+                               int32_t attn_dtype, const float* rays_o, const float* pos_tx,
+                               const float* dirs, const float* d_vals, float* w, int32_t* delay,
+                               void* stream) {
+    if (int e = validate(p)) return e;
+    AVR_REQUIRE(B >= 1 && attn && rays_o && pos_tx && dirs && d_vals && w && delay,
+                "avr_weights_fwd: bad args");
+    const int64_t rays = (int64_t)B * n_rays(*p);
+    const dim3 grid((unsigned)((rays + 3) / 4));
+    const size_t lds = 4 * (size_t)p->n_samples * sizeof(float);
+    if (lds > 65536) {
+        (void)hipFuncSetAttribute((const void*)weights_fwd_kernel<float>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)weights_fwd_kernel<__half>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
+    if (attn_dtype == AVR_DTYPE_F32)
+        hipLaunchKernelGGL(weights_fwd_kernel<float>, grid, dim3(256), lds, as_stream(stream), *p,
+                           (int)B, (const float*)attn, rays_o, pos_tx, dirs, d_vals, w, delay);
+    else if (attn_dtype == AVR_DTYPE_F16)
+        hipLaunchKernelGGL(weights_fwd_kernel<__half>, grid, dim3(256), lds, as_stream(stream),
+                           *p, (int)B, (const __half*)attn, rays_o, pos_tx, dirs, d_vals, w, delay);
+    else
+        return fail(AVR_E_ARG, "avr_weights_fwd: unknown attn dtype");
+    return check_launch("avr_weights_fwd");
+}
+
+namespace {
+template <typename Tin, bool VECTOR>
+int launch_reduce(const avr_render_params* p, int B, const void* sig, const float* w,
+                  const int32_t* delay, int n_split, float* part, hipStream_t st) {
+    constexpr int VEC = VECTOR ? Vec16<Tin>::N : 1;
+    const int R = n_rays(*p), S = p->n_samples, T = p->T;
+    const int rps = (R + n_split - 1) / n_split;
+    const int nchunks_max = (T + VEC - 1 + VEC - 1) / VEC;
+    const int cpt = (nchunks_max + kReduceThreads - 1) / kReduceThreads;
+    const int64_t total = (int64_t)B * R * S * T;
+    const dim3 grid(n_split, S, B);
+    const Tin* s = (const Tin*)sig;
+#define AVR_RR(C)                                                                            \
+    case C:                                                                                  \
+        hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C>), grid, dim3(kReduceThreads), \
+                           0, st, s, w, delay, part, B, R, S, T, rps, total);                \
+        break;
+    switch (cpt) {
+        AVR_RR(1) AVR_RR(2) AVR_RR(3) AVR_RR(4) AVR_RR(5) AVR_RR(6) AVR_RR(7) AVR_RR(8)
+        AVR_RR(12) AVR_RR(16)
+        default: {
+            if (cpt <= 12) {
+                hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, 12>), grid,
+                                   dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T,
+                                   rps, total);
+            } else if (cpt <= 16) {
+                hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, 16>), grid,
+                                   dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T,
+                                   rps, total);
+            } else {
+                return fail(AVR_E_CONFIG, "ray_reduce: T too long for this build");
+            }
+        }
+    }
+#undef AVR_RR
+    return check_launch("avr_ray_reduce_fwd");
+}
+}  // namespace
+
+extern "C" int avr_ray_reduce_fwd(const avr_render_params* p, int32_t B, const void* signal,
+                                  int32_t sig_dtype, const float* w, const int32_t* delay,
+                                  int32_t n_split, float* part, void* stream) {
+    if (int e = validate(p)) return e;
+    AVR_REQUIRE(B >= 1 && signal && w && delay && part, "avr_ray_reduce_fwd: null pointer");
+    const int R = n_rays(*p);
+    AVR_REQUIRE(n_split >= 1 && n_split <= R, "avr_ray_reduce_fwd: n_split out of range");
+    AVR_REQUIRE((R + n_split - 1) / n_split <= kMaxRaysPerSplit,
+                "avr_ray_reduce_fwd: too many rays per split (raise n_split)");
+    const int64_t st = (int64_t)p->n_samples * p->T;
+    const bool aligned = (reinterpret_cast<uintptr_t>(signal) % 16) == 0;
+    hipStream_t s = as_stream(stream);
+    if (sig_dtype == AVR_DTYPE_F32) {
+        if (aligned && st % 4 == 0) return launch_reduce<float, true>(p, B, signal, w, delay, n_split, part, s);
+        return launch_reduce<float, false>(p, B, signal, w, delay, n_split, part, s);
+    }
+    if (sig_dtype == AVR_DTYPE_F16) {
+        if (aligned && st % 8 == 0) return launch_reduce<__half, true>(p, B, signal, w, delay, n_split, part, s);
+        return launch_reduce<__half, false>(p, B, signal, w, delay, n_split, part, s);
+    }
+    return fail(AVR_E_ARG, "avr_ray_reduce_fwd: unknown signal dtype");
+}
+
+extern "C" int avr_dft_phase_fwd(const avr_render_params* p, int32_t B, const float* part,
+                                 int32_t n_split, const float* pl_table, const int32_t* shift,
+                                 const float* phase, const float* twiddle, int32_t k_split,
+                                 float* spart, void* stream) {
+    if (int e = validate(p)) return e;
+    AVR_REQUIRE(B >= 1 && part && pl_table && shift && phase && twiddle && spart,
+                "avr_dft_phase_fwd: null pointer");
+    const int S = p->n_samples, T = p->T, F = T / 2 + 1;
+    const int nkc = (T + kKc - 1) / kKc;
+    AVR_REQUIRE(k_split >= 1 && k_split <= nkc, "avr_dft_phase_fwd: k_split out of range");
+    const int kchunk = ((nkc + k_split - 1) / k_split) * kKc;
+    const dim3 grid((F + 127) / 128, ((S + 31) / 32) * k_split, B);
+    const size_t lds = (size_t)T * sizeof(float2);
+    if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)dft_phase_fwd_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(dft_phase_fwd_kernel, grid, dim3(kDftThreads), lds, as_stream(stream), part,
+                       (int)n_split, pl_table, shift, reinterpret_cast<const float2*>(phase),
+                       reinterpret_cast<const float2*>(twiddle), reinterpret_cast<float2*>(spart),
+                       (int)B, S, T, (int)k_split, kchunk);
+    return check_launch("avr_dft_phase_fwd");
+}
+
+extern "C" int avr_spectrum_finalize(int32_t B, int32_t P, int32_t F, const float* spart,
+                                     float* out, void* stream) {
+    AVR_REQUIRE(B >= 1 && P >= 1 && F >= 1 && spart && out, "avr_spectrum_finalize: bad args");
+    const int64_t n = (int64_t)B * F;
+    hipLaunchKernelGGL(spectrum_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), (int)B, (int)P, (int)F,
+                       reinterpret_cast<const float2*>(spart), reinterpret_cast<float2*>(out));
+    return check_launch("avr_spectrum_finalize");
+}
+
+extern "C" int avr_irfft(int32_t B, int32_t F, const float* spec, const float* tw, float* ir,
+                         void* stream) {
+    AVR_REQUIRE(B >= 1 && F >= 2 && spec && tw && ir, "avr_irfft: bad args");
+    const int n = 2 * (F - 1);
+    AVR_REQUIRE(n <= 16384, "avr_irfft: n too large");
+    const size_t lds = (size_t)(F + n) * sizeof(float2);
+    hipLaunchKernelGGL(irfft_kernel, dim3((n + 255) / 256, B), dim3(256), lds, as_stream(stream),
+                       (int)F, reinterpret_cast<const float2*>(spec),
+                       reinterpret_cast<const float2*>(tw), ir);
+    return check_launch("avr_irfft");
+}

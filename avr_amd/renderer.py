@@ -1,0 +1,376 @@
+"""Drop-in `AVRRender` for MI355X: the reference's renderer interface, HIP inside.
+
+Mirrors `renderer.py` of the reference (KMASAHIRO/AVR):
+
+* `AVRRender(networks_fn, **render_cfg)` — renderer.py:13-29, reads
+  n_samples, near, far, n_azi, n_ele, speed, fs, pathloss, xyz_min, xyz_max
+  and ignores extra keys (e.g. `sig_length`, avr_raf_furnished.yml:22).
+* `forward(rays_o, position_tx, direction_tx=None, ch_idx=None) -> [B, F, 2]`
+  — renderer.py:31-124.  `ch_idx` is passed to `network_fn` only when it is
+  not None (the reference always passes it, which `AVRModel_complex.forward`
+  (model.py:291) rejects).
+* module functions `ray_directions`, `normalize_points`,
+  `denormalize_points` with the reference's names (renderer.py:127-165).
+
+Everything after the network call runs in hand-written HIP kernels
+(`avr_amd/csrc`) through the C-ABI; autograd flows to the network's `attn`
+and `signal` outputs through `RenderCore`.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import math
+import threading
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+from ._lib import DTYPE_F16, DTYPE_F32, render_params
+
+# Optional instrumentation for bench.py: an object with begin(stream) / end(stream)
+# called around the dominant kernel (the ray-reduction stream).  None in normal use.
+KERNEL_TIMER = None
+
+_RENDER_KEYS = ("n_samples", "near", "far", "n_azi", "n_ele", "speed", "fs", "pathloss",
+                "xyz_min", "xyz_max")
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _dtype_code(t):
+    if t.dtype == torch.float32:
+        return DTYPE_F32
+    if t.dtype == torch.float16:
+        return DTYPE_F16
+    raise TypeError(f"unsupported dtype {t.dtype} (float32 or float16)")
+
+
+# --------------------------------------------------------------------------
+# per-device, per-config resident tables (pose independent)
+# --------------------------------------------------------------------------
+class Tables:
+    """d_vals, frac, shift, path-loss table, phase[S,F], twiddles on one device."""
+
+    def __init__(self, p, device):
+        S, T = p.n_samples, p.T
+        F = T // 2 + 1
+        f32 = dict(dtype=torch.float32, device=device)
+        self.d_vals = torch.empty(S, **f32)
+        self.frac = torch.empty(S, **f32)
+        self.shift = torch.empty(S, dtype=torch.int32, device=device)
+        self.pl = torch.empty(p.pl_len, **f32)
+        self.phase = torch.empty(S, F, 2, **f32)
+        self.twiddle = torch.empty(T, 2, **f32)
+        n = 2 * (F - 1)
+        self.ir_n = n
+        self.ir_twiddle = torch.empty(max(n, 2), 2, **f32)
+        st = _stream(device)
+        with torch.cuda.device(device):
+            _lib.call("avr_tables", ctypes_ref(p), _ptr(self.d_vals), _ptr(self.frac),
+                      _ptr(self.shift), _ptr(self.pl), _ptr(self.phase), _ptr(self.twiddle), st)
+            if n >= 2:
+                _lib.call("avr_ir_twiddle", n, _ptr(self.ir_twiddle), st)
+        # shift values are needed on the host for the reference's range check
+        shifts = self.shift.cpu()
+        self.max_shift = int(shifts.max().item()) if S > 0 else 0
+
+
+def ctypes_ref(p):
+    import ctypes
+
+    return ctypes.byref(p)
+
+
+_TABLE_CACHE: dict = {}
+_TABLE_LOCK = threading.Lock()
+
+
+def get_tables(p, device) -> Tables:
+    key = (device.index, p.key())
+    t = _TABLE_CACHE.get(key)
+    if t is None:
+        with _TABLE_LOCK:
+            t = _TABLE_CACHE.get(key)
+            if t is None:
+                t = Tables(p, device)
+                _TABLE_CACHE[key] = t
+    return t
+
+
+def check_config(p, tables: Tables):
+    """Reference-equivalent constraints (renderer.py:96-100)."""
+    if p.near_clamp + 1 >= p.pl_len:
+        raise IndexError("path_loss[prev_part+1] out of range (renderer.py:99): "
+                         f"int(0.1/speed*fs)+1 = {p.near_clamp + 1} >= {p.pl_len}")
+    if tables.max_shift + p.T > p.pl_len:
+        raise RuntimeError(
+            "stack expects each tensor to be equal size: receiver delay "
+            f"{tables.max_shift} samples + T={p.T} exceeds the path-loss table ({p.pl_len}); "
+            "the reference fails the same way at renderer.py:100 (needs shift <= 1.5T)")
+
+
+# --------------------------------------------------------------------------
+# launch heuristics
+# --------------------------------------------------------------------------
+def pick_n_split(B, R, S):
+    """Ray splits for the reduction: ~1024 workgroups, <= 2048 rays per split."""
+    want = max(1, math.ceil(1024 / max(1, B * S)))
+    n = min(R, max(want, math.ceil(R / 2048)))
+    while n > 1 and math.ceil(R / n) < 8:
+        n -= 1
+    return max(1, n)
+
+
+def pick_k_split(B, S, T):
+    F = T // 2 + 1
+    nkc = math.ceil(T / 64)
+    base = math.ceil(F / 128) * math.ceil(S / 32) * B
+    ks = max(1, min(nkc, math.ceil(512 / max(1, base))))
+    return ks
+
+
+# --------------------------------------------------------------------------
+# autograd core: (attn, signal) -> spectrum
+# --------------------------------------------------------------------------
+class RenderCore(torch.autograd.Function):
+    """Everything after the network call (renderer.py:75-121) as HIP kernels.
+
+    Inputs: attn [B, R*S] and signal [B, R*S, T] (fp32 or fp16, contiguous),
+    plus the pose geometry.  Output [B, F, 2] fp32.  Gradients flow to attn
+    and signal (poses are constants, as in the reference).
+    """
+
+    @staticmethod
+    def forward(ctx, attn, signal, p, tables, rays_o, position_tx, dirs):
+        dev = signal.device
+        B = signal.size(0)
+        R, S, T = p.n_azi * p.n_ele + 2, p.n_samples, p.T
+        F = T // 2 + 1
+        st = _stream(dev)
+        pref = ctypes_ref(p)
+        w = torch.empty(B, R, S, dtype=torch.float32, device=dev)
+        delay = torch.empty(B, R, S, dtype=torch.int32, device=dev)
+        _lib.call("avr_weights_fwd", pref, B, _ptr(attn), _dtype_code(attn), _ptr(rays_o),
+                  _ptr(position_tx), _ptr(dirs), _ptr(tables.d_vals), _ptr(w), _ptr(delay), st)
+        n_split = pick_n_split(B, R, S)
+        part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
+        timer = KERNEL_TIMER
+        if timer is not None:
+            timer.begin(dev, n_split=n_split)
+        _lib.call("avr_ray_reduce_fwd", pref, B, _ptr(signal), _dtype_code(signal), _ptr(w),
+                  _ptr(delay), n_split, _ptr(part), st)
+        if timer is not None:
+            timer.end(dev)
+        k_split = pick_k_split(B, S, T)
+        P = math.ceil(S / 32) * k_split
+        spart = torch.empty(B, P, F, 2, dtype=torch.float32, device=dev)
+        _lib.call("avr_dft_phase_fwd", pref, B, _ptr(part), n_split, _ptr(tables.pl),
+                  _ptr(tables.shift), _ptr(tables.phase), _ptr(tables.twiddle), k_split,
+                  _ptr(spart), st)
+        out = torch.empty(B, F, 2, dtype=torch.float32, device=dev)
+        _lib.call("avr_spectrum_finalize", B, P, F, _ptr(spart), _ptr(out), st)
+        ctx.p, ctx.tables = p, tables
+        ctx.save_for_backward(attn, signal, w, delay)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        attn, signal, w, delay = ctx.saved_tensors
+        p, tables = ctx.p, ctx.tables
+        dev = signal.device
+        B = signal.size(0)
+        R, S, T = p.n_azi * p.n_ele + 2, p.n_samples, p.T
+        st = _stream(dev)
+        pref = ctypes_ref(p)
+        g = grad_out.contiguous().float()
+        gz = torch.empty(B, S, T, dtype=torch.float32, device=dev)
+        _lib.call("avr_dft_phase_bwd", pref, B, _ptr(g), _ptr(tables.pl), _ptr(tables.shift),
+                  _ptr(tables.phase), _ptr(tables.twiddle), _ptr(gz), st)
+        grad_signal = torch.empty_like(signal)
+        grad_w = torch.empty(B, R, S, dtype=torch.float32, device=dev)
+        _lib.call("avr_ray_reduce_bwd", pref, B, _ptr(signal), _dtype_code(signal), _ptr(gz),
+                  _ptr(w), _ptr(delay), _ptr(grad_signal), _ptr(grad_w), st)
+        grad_attn = None
+        if ctx.needs_input_grad[0]:
+            grad_attn = torch.empty_like(attn)
+            _lib.call("avr_weights_bwd", pref, B, _ptr(attn), _dtype_code(attn),
+                      _ptr(tables.d_vals), _ptr(grad_w), _ptr(grad_attn), st)
+        return (grad_attn, grad_signal if ctx.needs_input_grad[1] else None,
+                None, None, None, None, None)
+
+
+# --------------------------------------------------------------------------
+# reference-named helpers (renderer.py:127-165)
+# --------------------------------------------------------------------------
+def normalize_points(input_pts, xyz_min, xyz_max):
+    """renderer.py:127-128 (torch elementwise; used by callers, not the hot path)."""
+    return 2 * (input_pts - xyz_min) / (xyz_max - xyz_min) - 1
+
+
+def denormalize_points(input_pts, xyz_min, xyz_max):
+    """renderer.py:130-131."""
+    return (input_pts + 1) / 2 * (xyz_max - xyz_min) + xyz_min
+
+
+def draw_jitter(n_azi, n_ele):
+    """The two CPU-generator draws of renderer.py:149,153 (same order)."""
+    u_azi = torch.rand(n_azi)
+    torch.rand(n_ele)  # elevation jitter is multiplied by 0 but consumes the stream
+    return u_azi
+
+
+def ray_directions(n_azi, n_ele, random_azi=True, device=None):
+    """renderer.py:133-165 on the GPU: returns (dir [R,3], None, None).
+
+    The azimuth jitter is drawn from the CPU default generator exactly as the
+    reference does; directions are computed by the `avr_ray_directions`
+    kernel.  (The reference also returns the meshgrid angles; no caller uses
+    them, so they are returned as None.)
+    """
+    device = torch.device("cuda", torch.cuda.current_device()) if device is None else device
+    u = draw_jitter(n_azi, n_ele)
+    if not random_azi:
+        u = torch.zeros_like(u)
+    p = render_params(dict(n_azi=n_azi, n_ele=n_ele, n_samples=1, far=1, near=0, xyz_min=-1,
+                           xyz_max=1, fs=1, speed=1, pathloss=1), 2)
+    dirs = torch.empty(n_azi * n_ele + 2, 3, dtype=torch.float32, device=device)
+    u_dev = u.to(device, non_blocking=True)
+    _lib.call("avr_ray_directions", ctypes_ref(p), _ptr(u_dev), _ptr(dirs), _stream(device))
+    return dirs, None, None
+
+
+# --------------------------------------------------------------------------
+# the drop-in module
+# --------------------------------------------------------------------------
+class AVRRender(nn.Module):
+    """Audio signal rendering (renderer.py:13-124), MI355X-native."""
+
+    def __init__(self, networks_fn, **kwargs) -> None:
+        super().__init__()
+        self.network_fn = networks_fn
+        for k in _RENDER_KEYS:
+            setattr(self, k, kwargs[k])
+        self._cfg = {k: kwargs[k] for k in _RENDER_KEYS}
+        self.last_network_inputs = None
+
+    # -- stages, exposed for tests and for callers that bring their own network
+    def _device(self, rays_o):
+        if rays_o.is_cuda:
+            return rays_o.device
+        if not torch.cuda.is_available():
+            raise RuntimeError("avr_amd.AVRRender needs a HIP device (no CPU fallback)")
+        return torch.device("cuda", torch.cuda.current_device())
+
+    def sample(self, rays_o, position_tx, direction_tx=None, u_azi=None):
+        """Ray generation + sampling (renderer.py:53-62) -> network inputs.
+
+        Returns (pts, view, tx, dir_tx_or_None, geom) where geom carries the
+        device tensors the render core needs.
+        """
+        dev = self._device(rays_o)
+        B = position_tx.size(0)
+        if u_azi is None:
+            u_azi = draw_jitter(self.n_azi, self.n_ele)
+        p0 = render_params(self._cfg, 2)
+        R, S = p0.n_azi * p0.n_ele + 2, p0.n_samples
+        f32 = dict(dtype=torch.float32, device=dev)
+        rays_o = rays_o.to(dev, torch.float32).contiguous()
+        position_tx = position_tx.to(dev, torch.float32).contiguous()
+        if direction_tx is not None:
+            direction_tx = direction_tx.to(dev, torch.float32).contiguous()
+        st = _stream(dev)
+        pref = ctypes_ref(p0)
+        dirs = torch.empty(R, 3, **f32)
+        u_dev = u_azi.to(dev, torch.float32, non_blocking=True)
+        d_vals = torch.empty(S, **f32)
+        with torch.cuda.device(dev):
+            _lib.call("avr_ray_directions", pref, _ptr(u_dev), _ptr(dirs), st)
+            _lib.call("avr_depth_samples", pref, _ptr(d_vals), st)
+            pts = torch.empty(B, R * S, 3, **f32)
+            view = torch.empty(B, R * S, 3, **f32)
+            tx = torch.empty(B, R * S, 3, **f32)
+            dtx = torch.empty(B, R * S, 3, **f32) if direction_tx is not None else None
+            _lib.call("avr_sample_points", pref, B, _ptr(rays_o), _ptr(position_tx),
+                      _ptr(direction_tx), _ptr(dirs), _ptr(d_vals), _ptr(pts), _ptr(view),
+                      _ptr(tx), _ptr(dtx), st)
+        geom = dict(rays_o=rays_o, position_tx=position_tx, dirs=dirs, device=dev, B=B)
+        return pts, view, tx, dtx, geom
+
+    def render_from_network_output(self, attn, signal, geom):
+        """Render core (renderer.py:74-124) on given network outputs."""
+        dev, B = geom["device"], geom["B"]
+        S = int(self.n_samples)
+        if attn.dtype not in (torch.float32, torch.float16):
+            attn = attn.float()
+        if signal.dtype not in (torch.float32, torch.float16):
+            signal = signal.float()
+        attn = attn.to(dev).reshape(B, -1).contiguous()
+        T = signal.size(-1)
+        signal = signal.to(dev).reshape(B, -1, T).contiguous()
+        R = self.n_azi * self.n_ele + 2
+        if attn.size(1) != R * S or signal.size(1) != R * S:
+            raise ValueError(f"network output has {signal.size(1)} ray-samples, expected "
+                             f"{R}x{S}={R * S}")
+        p = render_params(self._cfg, T)
+        with torch.cuda.device(dev):
+            tables = get_tables(p, dev)
+            check_config(p, tables)
+            return RenderCore.apply(attn, signal, p, tables, geom["rays_o"], geom["position_tx"],
+                                    geom["dirs"])
+
+    def forward(self, rays_o, position_tx, direction_tx=None, ch_idx=None):
+        """Render [B, F, 2] (real, imag) spectra; see renderer.py:31-124."""
+        pts, view, tx, dtx, geom = self.sample(rays_o, position_tx, direction_tx)
+        self.last_network_inputs = None
+        kw = {} if ch_idx is None else {"ch_idx": ch_idx}
+        if dtx is not None:
+            attn, signal = self.network_fn(pts, view, tx, dtx, **kw)
+        else:
+            attn, signal = self.network_fn(pts, view, tx, **kw)
+        return self.render_from_network_output(attn, signal, geom)
+
+
+# --------------------------------------------------------------------------
+# a13: IR synthesis (utils/criterion.py:71 applied to the rendered spectrum)
+# --------------------------------------------------------------------------
+def spectrum_to_ir(out):
+    """[B, F, 2] spectrum -> [B, 2(F-1)] IR with the HIP irfft kernel.
+
+    Same result as `torch.real(torch.fft.irfft(out[...,0] + 1j*out[...,1]))`
+    (avr_runner.py:178 + utils/criterion.py:71).  Forward only.
+    """
+    if not out.is_cuda:
+        raise RuntimeError("spectrum_to_ir needs a HIP tensor (no CPU fallback)")
+    dev = out.device
+    out = out.detach().float().contiguous()
+    B, F = out.size(0), out.size(1)
+    n = 2 * (F - 1)
+    tw = _ir_twiddle(n, dev)
+    ir = torch.empty(B, n, dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("avr_irfft", B, F, _ptr(out), _ptr(tw), _ptr(ir), _stream(dev))
+    return ir
+
+
+_IRTW: dict = {}
+
+
+def _ir_twiddle(n, dev):
+    key = (dev.index, n)
+    tw = _IRTW.get(key)
+    if tw is None:
+        with _TABLE_LOCK:
+            tw = _IRTW.get(key)
+            if tw is None:
+                tw = torch.empty(n, 2, dtype=torch.float32, device=dev)
+                with torch.cuda.device(dev):
+                    _lib.call("avr_ir_twiddle", n, _ptr(tw), _stream(dev))
+                _IRTW[key] = tw
+    return tw

@@ -1,0 +1,229 @@
+"""Benchmark: MeshRIR single-listener render (config 2) through the IR.
+
+One step = one pass of the hot path over one pose of synthetic input with the
+network output already resident in HBM (stub network, as the reference's own
+CPU timing does): ray generation + sampling (network inputs) -> weights ->
+ray-reduction stream -> MFMA DFT + phase -> spectrum -> irfft IR.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+
+For N > 1 launch with torch.distributed.run (one process per GPU); each rank
+renders its own poses (weak scaling, no data-path collective), rank 0 prints
+one JSON line with the whole-job ray-samples/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from avr_amd import AVRRender, spectrum_to_ir  # noqa: E402
+from avr_amd import renderer as rmod  # noqa: E402
+from avr_amd.workloads import WORKLOADS  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+class StubNet(torch.nn.Module):
+    def __init__(self, attn, signal):
+        super().__init__()
+        self.attn, self.signal = attn, signal
+
+    def forward(self, pts, view, tx, dir_tx=None, ch_idx=None):
+        return self.attn, self.signal
+
+
+class KernelTimer:
+    """HIP events around the ray-reduction kernel on the stream it runs on."""
+
+    def __init__(self):
+        self.pairs = []
+        self.n_split = None
+        self.enabled = False
+
+    def begin(self, dev, n_split=None):
+        if not self.enabled:
+            return
+        self.n_split = n_split
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream(dev))
+        self.pairs.append([e, None])
+
+    def end(self, dev):
+        if not self.enabled:
+            return
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream(dev))
+        self.pairs[-1][1] = e
+
+    def mean_ms(self):
+        ts = [a.elapsed_time(b) for a, b in self.pairs if b is not None]
+        return sum(ts) / len(ts) if ts else float("nan")
+
+
+def cpu_baseline(w, budget_s=15.0):
+    """Time the CPU oracle (op-for-op torch-CPU restatement of renderer_cpu.py)
+    on this host's cores for a bounded sample of the same workload."""
+    from oracle import avr_oracle as orc
+
+    threads = torch.get_num_threads()
+    g = torch.Generator().manual_seed(1)
+    B, RS, T = w.batch, w.n_rays * w.n_samples, w.T
+    attn = torch.rand(B, RS, 1, generator=g) * 2
+    sig = torch.randn(B, RS, T, generator=g) * 0.1
+    if w.signal_dtype == "float16":
+        sig = sig.half()
+    rays_o = torch.rand(B, 3, generator=g) * 4 - 2
+    tx = torch.rand(B, 3, generator=g) * 4 - 2
+    dtx = torch.nn.functional.normalize(torch.randn(B, 3, generator=g), dim=-1) if w.with_dir_tx else None
+    cfg = orc.RenderConfig.from_kwargs(**w.render)
+    net = orc.StubNetwork(attn, sig)
+    times = []
+    t_start = time.time()
+    while True:
+        t0 = time.time()
+        out = orc.render_spectrum(cfg, net, rays_o, tx, dtx)
+        orc.spectrum_to_ir(out)
+        times.append(time.time() - t0)
+        if time.time() - t_start > budget_s or len(times) >= 20:
+            break
+    best = min(times)
+    return {
+        "value": w.ray_samples / best,
+        "unit": "ray-samples/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{len(times)} full poses of {w.name} (forward + irfft), best of {len(times)}; "
+                  f"median {sorted(times)[len(times) // 2] * 1e3:.1f} ms/pose",
+        "ms_per_pose": best * 1e3,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="c2_meshrir_1024x256x512")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    w = WORKLOADS[args.workload]
+    B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
+    dt = torch.float16 if w.signal_dtype == "float16" else torch.float32
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    attn = (torch.rand(B, R * S, 1, device=dev, generator=gen) * 2).to(dt)
+    signal = (torch.randn(B, R * S, T, device=dev, generator=gen) * 0.1).to(dt)
+    rays_o = torch.rand(B, 3, device=dev, generator=gen) * 4 - 2
+    tx = torch.rand(B, 3, device=dev, generator=gen) * 4 - 2
+    dtx = (torch.nn.functional.normalize(torch.randn(B, 3, device=dev, generator=gen), dim=-1)
+           if w.with_dir_tx else None)
+    renderer = AVRRender(StubNet(attn, signal), **w.render)
+    timer = KernelTimer()
+    rmod.KERNEL_TIMER = timer
+
+    def step():
+        with torch.no_grad():
+            out = renderer(rays_o, tx, dtx)
+            return spectrum_to_ir(out)
+
+    torch.manual_seed(rank)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    timer.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    timer.enabled = False
+    if world > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    total_rs = world * w.ray_samples * args.steps
+    value = total_rs / elapsed
+
+    # roofline for the dominant kernel (ray-reduction stream)
+    k_ms = timer.mean_ms()
+    es = 2 if dt == torch.float16 else 4
+    n_split = timer.n_split or 1
+    alg_bytes = w.ray_samples * (T * es + 8) + n_split * B * S * T * 4
+    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+
+    result = {
+        "metric": "ray-samples/sec/GPU (1024 rays×256 samp×512 freq) + IR render ms/pose",
+        "value": value,
+        "unit": "ray-samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "ir_render_ms_per_pose": ms_per_step / B,
+        "per_gpu_value": value / world,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32" if dt == torch.float32 else "f16-storage/f32-math",
+        "data": "synthetic (stub network, outputs resident in HBM; seeded torch RNG)",
+        "config": {"workload": w.name, "rays": R, "samples": S, "T": T, "freq_bins": w.F,
+                   "poses_per_gpu": B, "parallelism": f"poses x{world} (no data-path collective)"},
+        "roofline": {
+            "kernel": "ray_reduce_fwd_kernel",
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "alg_bytes_per_launch": alg_bytes,
+            "avg_launch_ms": k_ms,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(w, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

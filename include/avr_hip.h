@@ -1,0 +1,172 @@
+/*
+ * avr_hip.h — C-ABI of the MI355X (gfx950) acoustic volume render hot path.
+ *
+ * The reference (KMASAHIRO/AVR) is pure Python; its hot path is
+ * `AVRRender.forward` (renderer.py:31-124, identical math in
+ * renderer_cpu.py:23-102) plus the hash-grid encodings it calls through
+ * tinycudann (model.py:66-68, 258-264) and the irfft in
+ * utils/criterion.py:71.  There is no FFI in the reference: each entry point
+ * below replaces one stage of that Python code, and the Python host package
+ * `avr_amd` (the drop-in `AVRRender`) binds them with ctypes — see
+ * INTEGRATION.md for the binding a maintainer adds on the reference side.
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers allocated by the caller (PyTorch's
+ *     caching allocator); the library never allocates or frees memory and
+ *     keeps no global mutable state, so it is reentrant (nn.DataParallel
+ *     calls forward from several host threads, avr_runner.py:63).
+ *   - `stream` is a hipStream_t (NULL = legacy default stream).
+ *   - Every function returns 0 on success, otherwise a nonzero code
+ *     (AVR_E_* or a hipError_t value); `avr_last_error()` returns a
+ *     thread-local message for the last failure on the calling thread.
+ *   - Layouts are row-major, innermost index last.
+ *     B = poses, R = n_azi*n_ele+2 rays, S = n_samples, T = signal length,
+ *     F = T/2+1 bins.
+ */
+#ifndef AVR_HIP_H
+#define AVR_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AVR_ABI_VERSION 1
+
+/* element types of network outputs / gradients */
+#define AVR_DTYPE_F32 0
+#define AVR_DTYPE_F16 1
+
+/* error codes besides hipError_t values */
+#define AVR_E_ARG 1001      /* bad argument / shape / alignment */
+#define AVR_E_CONFIG 1002   /* render config outside supported range */
+
+/*
+ * Render scalars, rounded on the host exactly the way the reference's torch
+ * ops round them (Python double arithmetic first, fp32 at the tensor op):
+ * AVRRender.__init__ (renderer.py:16-29) reads the same keys.
+ */
+typedef struct avr_render_params {
+    int32_t n_azi;        /* azimuth rays */
+    int32_t n_ele;        /* elevation rings */
+    int32_t n_samples;    /* S */
+    int32_t T;            /* signal_output_dim */
+    float depth_scale;    /* fp32(far - near)            renderer.py:54 */
+    float depth_offset;   /* fp32(near)                  renderer.py:54 */
+    float lo;             /* fp32(xyz_min)               renderer.py:128 */
+    float span;           /* fp32(xyz_max - xyz_min)     renderer.py:128 */
+    float fs;             /* fp32(fs) */
+    float speed;          /* fp32(speed) */
+    float pathloss;       /* fp32(pathloss)              renderer.py:98 */
+    float azi_jitter;     /* fp32(2*pi / n_azi)          renderer.py:149 */
+    float two_pi;         /* fp32(2*pi): linspace end    renderer.py:148 */
+    float phase_c;        /* fp32(-2*pi/T)               renderer.py:108 */
+    int32_t near_clamp;   /* int(0.1/speed*fs)           renderer.py:96 */
+    int32_t pl_len;       /* len(arange(0, 2.5*T))       renderer.py:97 */
+} avr_render_params;
+
+const char* avr_last_error(void);
+int avr_abi_version(void);
+
+/* ---- pose-independent tables (cached per device by the host) ----------
+ * d_vals[S], frac[S] (= pts2rx_idx), shift[S] (int), pl_table[pl_len],
+ * phase[S][F][2] (cos, sin of the fractional-delay phase),
+ * twiddle[T][2] = (cos, -sin)(2*pi*k/T).
+ * Replaces renderer.py:54, 79-80, 95-99, 108. */
+int avr_tables(const avr_render_params* p, float* d_vals, float* frac, int32_t* shift,
+               float* pl_table, float* phase, float* twiddle, void* stream);
+
+/* d_vals[S] alone (needs only n_samples/depth_*), for sampling before the
+ * network has revealed T. */
+int avr_depth_samples(const avr_render_params* p, float* d_vals, void* stream);
+
+/* irfft twiddle for length n: tw[n][2] = (cos, sin)(2*pi*k/n). */
+int avr_ir_twiddle(int32_t n, float* tw, void* stream);
+
+/* ---- a2: spherical ray directions (renderer.py:133-165) ----------------
+ * u_azi[n_azi] are the CPU-generator U[0,1) draws (renderer.py:149);
+ * writes dirs[R][3]. */
+int avr_ray_directions(const avr_render_params* p, const float* u_azi, float* dirs,
+                       void* stream);
+
+/* ---- a3/a4: samples and network inputs (renderer.py:54-62) ------------
+ * rays_o, pos_tx, dir_tx: [B][3] (dir_tx may be NULL).  Writes the four
+ * network inputs [B][R*S][3]; net_dir_tx is ignored when dir_tx is NULL. */
+int avr_sample_points(const avr_render_params* p, int32_t B, const float* rays_o,
+                      const float* pos_tx, const float* dir_tx, const float* dirs,
+                      const float* d_vals, float* net_pts, float* net_view, float* net_tx,
+                      float* net_dir_tx, void* stream);
+
+/* ---- a8 + a11: source delays and compositing weights -------------------
+ * attn [B][R*S] (dtype), writes w[B][R][S] fp32 and delay[B][R][S] int32.
+ * One ray per wavefront, samples strided over lanes, transmittance by a
+ * wavefront shuffle scan.  Replaces renderer.py:86-88, 181-190. */
+int avr_weights_fwd(const avr_render_params* p, int32_t B, const void* attn, int32_t attn_dtype,
+                    const float* rays_o, const float* pos_tx, const float* dirs,
+                    const float* d_vals, float* w, int32_t* delay, void* stream);
+
+/* ---- a7-a12 (time-domain half): ray reduction --------------------------
+ * part[n_split][B][S][T] = sum over the rays of split k of
+ *   w[b,r,s] * [t >= delay[b,r,s]] * signal[b,r,s,t]
+ * signal [B][R][S][T] (dtype).  The HBM stream of the forward pass. */
+int avr_ray_reduce_fwd(const avr_render_params* p, int32_t B, const void* signal,
+                       int32_t sig_dtype, const float* w, const int32_t* delay,
+                       int32_t n_split, float* part, void* stream);
+
+/* ---- a9/a10/a11/a12 (frequency half): DFT + phase + sum over samples ---
+ * z[b,s,t] = pl[shift[s]+t] * [t < T-1-shift[s]] * sum_k part[k,b,s,t]
+ * spart[B][P][F][2], P = ceil(S/32) * k_split: partial spectra
+ *   sum_{s in tile} phase[s,f] * sum_{t in slice} z[b,s,t] * twiddle[(t*f)%T]
+ * computed as an fp32 MFMA GEMM [B*S, T] x [T, 2F]. */
+int avr_dft_phase_fwd(const avr_render_params* p, int32_t B, const float* part,
+                      int32_t n_split, const float* pl_table, const int32_t* shift,
+                      const float* phase, const float* twiddle, int32_t k_split,
+                      float* spart, void* stream);
+
+/* out[B][F][2] = sum_p spart[B][p][F][2] (fixed order, deterministic). */
+int avr_spectrum_finalize(int32_t B, int32_t P, int32_t F, const float* spart, float* out,
+                          void* stream);
+
+/* ---- a13: IR synthesis, torch.fft.irfft (utils/criterion.py:71) --------
+ * spec[B][F][2] -> ir[B][n], n = 2*(F-1), tw = avr_ir_twiddle(n). */
+int avr_irfft(int32_t B, int32_t F, const float* spec, const float* tw, float* ir,
+              void* stream);
+
+/* ---- a14: backward ------------------------------------------------------
+ * grad_out[B][F][2] -> gz[B][S][T] = pl*tail * d out / d z   (adjoint DFT) */
+int avr_dft_phase_bwd(const avr_render_params* p, int32_t B, const float* grad_out,
+                      const float* pl_table, const int32_t* shift, const float* phase,
+                      const float* twiddle, float* gz, void* stream);
+
+/* gz, signal, w, delay -> grad_signal[B][R][S][T] (sig dtype) and
+ * grad_w[B][R][S] = sum_t [t>=delay] gz[b,s,t] * signal[b,r,s,t]. */
+int avr_ray_reduce_bwd(const avr_render_params* p, int32_t B, const void* signal,
+                       int32_t sig_dtype, const float* gz, const float* w,
+                       const int32_t* delay, void* grad_signal, float* grad_w, void* stream);
+
+/* grad_w -> grad_attn[B][R*S] (attn dtype): adjoint of the transmittance
+ * scan and of alpha = 1 - exp(-attn*dist). */
+int avr_weights_bwd(const avr_render_params* p, int32_t B, const void* attn, int32_t attn_dtype,
+                    const float* d_vals, const float* grad_w, void* grad_attn, void* stream);
+
+/* ---- a5: multiresolution hash-grid encoding (tcnn GridEncoding) --------
+ * x[N][3] in [0,1]; params = concatenated level tables [sum_l size_l][2];
+ * level_offset[L+1] (entries), level_scale[L] (fp32), level_res[L] are HOST
+ * arrays (passed by value in the kernel arguments);
+ * out[N][L*2] (out_dtype).  model.py:66-68, 191, 219-220, 315-324. */
+int avr_hashgrid_fwd(int64_t N, int32_t n_levels, const float* x, const void* params,
+                     int32_t param_dtype, const int64_t* level_offset, const float* level_scale,
+                     const int32_t* level_res, void* out, int32_t out_dtype, void* stream);
+
+/* grad_out[N][L*2] -> grad_params (fp32, accumulated with atomics; zero it
+ * first). */
+int avr_hashgrid_bwd(int64_t N, int32_t n_levels, const float* x, const void* grad_out,
+                     int32_t grad_dtype, const int64_t* level_offset, const float* level_scale,
+                     const int32_t* level_res, float* grad_params, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AVR_HIP_H */

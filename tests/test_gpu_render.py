@@ -1,0 +1,236 @@
+"""GPU parity: the HIP render path against the golden vectors of the real
+reference and against the CPU oracle on the same seeded inputs.
+
+Tolerance (BASELINE.json north_star): 1e-4 relative on the rendered complex
+spectrum (L2 and max-norm).  Integer delays: bit-exact except for rare 1-ulp
+trig flips of the ray directions (<= 0.1% of ray-samples)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import Case, case_names, digest_check, rel_l2, rel_max
+from oracle import avr_oracle as orc
+
+from avr_amd import AVRRender, spectrum_to_ir
+from avr_amd import _lib
+from avr_amd.renderer import get_tables, render_params
+from avr_amd.workloads import WORKLOADS, make_inputs
+
+pytestmark = pytest.mark.gpu
+CASES = case_names()
+TOL = 1e-4
+DEV = torch.device("cuda", 0)
+
+
+class Net(torch.nn.Module):
+    """Stub network returning device tensors; records its inputs."""
+
+    def __init__(self, attn, signal):
+        super().__init__()
+        self.attn, self.signal, self.seen = attn, signal, None
+
+    def forward(self, pts, view, tx, dir_tx=None):
+        self.seen = (pts, view, tx, dir_tx)
+        return self.attn, self.signal
+
+
+def hip_render(case_or_w, inp, seed, grads=False):
+    w = case_or_w.workload if isinstance(case_or_w, Case) else case_or_w
+    attn = torch.from_numpy(inp["attn"]).to(DEV).requires_grad_(grads)
+    sig = torch.from_numpy(inp["signal"]).to(DEV).requires_grad_(grads)
+    net = Net(attn, sig)
+    r = AVRRender(net, **w.render)
+    dtx = None if inp["direction_tx"] is None else torch.from_numpy(inp["direction_tx"]).to(DEV)
+    torch.manual_seed(seed)
+    out = r(torch.from_numpy(inp["rays_o"]).to(DEV), torch.from_numpy(inp["position_tx"]).to(DEV), dtx)
+    return out, attn, sig, net
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_spectrum_matches_reference_golden(name):
+    case = Case(name)
+    out, *_ = hip_render(case, case.inputs(), case.seed)
+    o = out.detach().cpu().numpy()
+    ref = case["out"]
+    assert rel_l2(o, ref) < TOL, rel_l2(o, ref)
+    assert rel_max(o, ref) < TOL, rel_max(o, ref)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_ir_matches_reference_golden(name):
+    case = Case(name)
+    out, *_ = hip_render(case, case.inputs(), case.seed)
+    ir = spectrum_to_ir(out.detach()).cpu().numpy()
+    assert rel_l2(ir, case["ir"]) < TOL
+    # the HIP irfft itself, on the reference spectrum
+    ir2 = spectrum_to_ir(torch.from_numpy(case["out"]).to(DEV)).cpu().numpy()
+    assert rel_l2(ir2, case["ir"]) < 1e-5
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_network_inputs_and_directions(name):
+    case = Case(name)
+    inp = case.inputs()
+    out, _, _, net = hip_render(case, inp, case.seed)
+    for k, t in zip(("pts", "view", "tx", "dir_tx"), net.seen):
+        if t is None:
+            assert not case.has("net_" + k + "_sum")
+            continue
+        digest_check(case, "net_" + k, t.cpu().numpy(), rtol=0, atol=3e-6)
+
+
+def _stage_weights(case, inp):
+    """Run ray generation + weights kernel; return (w, delay) as numpy."""
+    w = case.workload
+    r = AVRRender(None, **w.render)
+    torch.manual_seed(case.seed)
+    dtx = None if inp["direction_tx"] is None else torch.from_numpy(inp["direction_tx"]).to(DEV)
+    _, _, _, _, geom = r.sample(torch.from_numpy(inp["rays_o"]).to(DEV),
+                                torch.from_numpy(inp["position_tx"]).to(DEV), dtx)
+    p = render_params(w.render, w.T)
+    tables = get_tables(p, DEV)
+    B, R, S = w.batch, w.n_rays, w.n_samples
+    attn = torch.from_numpy(inp["attn"]).to(DEV).reshape(B, -1).contiguous()
+    wt = torch.empty(B, R, S, device=DEV)
+    dl = torch.empty(B, R, S, dtype=torch.int32, device=DEV)
+    _lib.call("avr_weights_fwd", ctypes.byref(p), B, attn.data_ptr(),
+              0 if attn.dtype == torch.float32 else 1, geom["rays_o"].data_ptr(),
+              geom["position_tx"].data_ptr(), geom["dirs"].data_ptr(), tables.d_vals.data_ptr(),
+              wt.data_ptr(), dl.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return wt.cpu().numpy(), dl.cpu().numpy(), geom["dirs"].cpu().numpy(), tables
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_stage_weights_delays_tables(name):
+    case = Case(name)
+    inp = case.inputs()
+    wt, dl, dirs, tables = _stage_weights(case, inp)
+    np.testing.assert_allclose(dirs, case["dirs"], rtol=0, atol=5e-7)
+    np.testing.assert_allclose(tables.d_vals.cpu().numpy(), case["d_vals"], rtol=0, atol=0)
+    np.testing.assert_array_equal(tables.shift.cpu().numpy(), case["shift"].astype(np.int32))
+    digest_check(case, "weights", wt, rtol=2e-5, atol=1e-9)
+    if case.has("delay"):
+        agree = (dl == case["delay"]).mean()
+    else:
+        agree = (dl.reshape(-1)[case["delay_idx"]] == case["delay_at"]).mean()
+    assert agree > 0.999, agree
+
+
+@pytest.mark.parametrize("name", [c for c in CASES if Case(c).grads])
+def test_backward_matches_reference_golden(name):
+    case = Case(name)
+    out, attn, sig, _ = hip_render(case, case.inputs(), case.seed, grads=True)
+    g = torch.from_numpy(case.grad_probe()).to(DEV)
+    (out * g).sum().backward()
+    ga = attn.grad.float().cpu().numpy()
+    gs = sig.grad.float().cpu().numpy()
+    # relative to the gradient's RMS
+    scale_a = np.sqrt(float(case["grad_attn_sumsq"]) / ga.size)
+    scale_s = np.sqrt(float(case["grad_signal_sumsq"]) / gs.size)
+    fp16 = case.workload.signal_dtype == "float16"
+    tol_s = 2e-3 if fp16 else TOL  # fp16 gradient storage rounds at 2^-11
+    digest_check(case, "grad_attn", ga, rtol=0, atol=TOL * 50 * scale_a + 1e-4 * np.abs(ga).max())
+    digest_check(case, "grad_signal", gs, rtol=tol_s, atol=tol_s * scale_s)
+    s64 = gs.astype(np.float64).sum()
+    assert abs(s64 - float(case["grad_signal_sum"])) <= 1e-3 * np.sqrt(float(case["grad_signal_sumsq"]) * gs.size) + 1e-6
+    dot = float((gs.astype(np.float64) * case.inputs()["signal"].astype(np.float64)).sum())
+    ref_dot = float(case["grad_signal_dot_signal"])
+    assert abs(dot - ref_dot) <= 1e-3 * abs(ref_dot) + 1e-6
+
+
+@pytest.mark.parametrize("name", ["c1_s0", "edge_ragged_s3", "edge_oddT_s4", "c3_s0"])
+def test_matches_oracle_same_seed(name):
+    case = Case(name)
+    inp = case.inputs()
+    w = case.workload
+    torch.manual_seed(case.seed)
+    dtx = None if inp["direction_tx"] is None else torch.from_numpy(inp["direction_tx"])
+    ref = orc.render_spectrum(orc.RenderConfig.from_kwargs(**w.render),
+                              orc.StubNetwork(torch.from_numpy(inp["attn"]), torch.from_numpy(inp["signal"])),
+                              torch.from_numpy(inp["rays_o"]), torch.from_numpy(inp["position_tx"]), dtx).numpy()
+    out, *_ = hip_render(case, inp, case.seed)
+    assert rel_l2(out.detach().cpu().numpy(), ref) < TOL
+
+
+def test_deterministic_bitwise():
+    case = Case("c3_s0")
+    inp = case.inputs()
+    a, *_ = hip_render(case, inp, 0)
+    b, *_ = hip_render(case, inp, 0)
+    assert torch.equal(a, b)
+
+
+def test_unaligned_signal_uses_scalar_path():
+    case = Case("c1_s1")
+    inp = case.inputs()
+    w = case.workload
+    big = torch.zeros(inp["signal"].size + 1, dtype=torch.float32, device=DEV)
+    sig = big[1:].view(inp["signal"].shape)  # 4-byte offset: not 16-byte aligned
+    sig.copy_(torch.from_numpy(inp["signal"]))
+    attn = torch.from_numpy(inp["attn"]).to(DEV)
+    r = AVRRender(Net(attn, sig), **w.render)
+    torch.manual_seed(case.seed)
+    out = r(torch.from_numpy(inp["rays_o"]).to(DEV), torch.from_numpy(inp["position_tx"]).to(DEV))
+    assert rel_l2(out.cpu().numpy(), case["out"]) < TOL
+
+
+def test_ch_idx_passthrough_rules():
+    case = Case("c1_s1")
+    inp = case.inputs()
+    attn = torch.from_numpy(inp["attn"]).to(DEV)
+    sig = torch.from_numpy(inp["signal"]).to(DEV)
+
+    class WithCh(torch.nn.Module):
+        def forward(self, pts, view, tx, ch_idx=None):
+            self.ch = ch_idx
+            return attn, sig
+
+    class NoCh(torch.nn.Module):
+        def forward(self, pts, view, tx):
+            return attn, sig
+
+    ro = torch.from_numpy(inp["rays_o"]).to(DEV)
+    tx = torch.from_numpy(inp["position_tx"]).to(DEV)
+    net = WithCh()
+    AVRRender(net, **case.workload.render)(ro, tx, ch_idx=torch.tensor([3], device=DEV))
+    assert int(net.ch[0]) == 3
+    AVRRender(NoCh(), **case.workload.render)(ro, tx)  # no ch_idx keyword passed
+
+
+def test_config_guard_like_reference():
+    w = WORKLOADS["c1_meshrir_plumbing"].replace(far=40.0)  # shift > 1.5T
+    inp = make_inputs(w, 0)
+    with pytest.raises(RuntimeError, match="stack expects"):
+        hip_render(w, inp, 0)
+
+
+# ------------------------------------------------------------------ full size
+def test_config2_full_size_properties():
+    """Config 2 (headline workload): linearity in the signal, additivity over
+    ray halves, and agreement with the golden spectrum."""
+    case = Case("c2_s0")
+    inp = case.inputs()
+    w = case.workload
+    out, *_ = hip_render(case, inp, case.seed)
+    base = out.detach().cpu().numpy()
+    assert rel_l2(base, case["out"]) < TOL
+    inp2 = dict(inp)
+    inp2["signal"] = inp["signal"] * np.float32(2.0)
+    out2, *_ = hip_render(case, inp2, case.seed)
+    np.testing.assert_allclose(out2.detach().cpu().numpy(), 2 * base, rtol=0, atol=1e-6 * np.abs(base).max())
+    # zero the second half of the rays: spectrum(first) + spectrum(second) == base
+    R, S, T = w.n_rays, w.n_samples, w.T
+    half = R // 2
+    a = inp["signal"].reshape(1, R, S, T).copy()
+    b = a.copy()
+    a[:, half:] = 0
+    b[:, :half] = 0
+    ia, ib = dict(inp), dict(inp)
+    ia["signal"], ib["signal"] = a.reshape(inp["signal"].shape), b.reshape(inp["signal"].shape)
+    oa, *_ = hip_render(case, ia, case.seed)
+    ob, *_ = hip_render(case, ib, case.seed)
+    s = oa.detach().cpu().numpy() + ob.detach().cpu().numpy()
+    assert rel_l2(s, base) < 1e-5

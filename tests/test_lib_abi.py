@@ -1,0 +1,58 @@
+"""CPU: the C-ABI library builds, loads, and exports every declared symbol.
+
+No compute calls here (no GPU in the build container)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from avr_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "avr_hip.h")
+
+
+def _declared():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(avr_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "avr_amd", "csrc"), "-j8"], check=True)
+    return _lib.load()
+
+
+def test_header_declares_expected_entry_points():
+    names = _declared()
+    for n in ("avr_ray_reduce_fwd", "avr_dft_phase_fwd", "avr_weights_fwd", "avr_irfft",
+              "avr_hashgrid_fwd", "avr_hashgrid_bwd", "avr_last_error"):
+        assert n in names
+
+
+def test_every_declared_symbol_is_exported(lib):
+    missing = [n for n in _declared() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_header():
+    assert set(_declared()) == set(_lib.EXPORTS)
+
+
+def test_abi_version(lib):
+    assert lib.avr_abi_version() == 1
+
+
+def test_argument_errors_are_reported_without_gpu(lib):
+    # null params -> AVR_E_ARG with a message; no device work is launched
+    rc = lib.avr_tables(None, None, None, None, None, None, None, None)
+    assert rc == 1001
+    assert b"null" in lib.avr_last_error()
+
+
+def test_code_object_targets_gfx950(lib):
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in blob
