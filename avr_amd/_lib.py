@@ -33,6 +33,7 @@ class RenderParams(ctypes.Structure):
         ("n_ele", _c_i32),
         ("n_samples", _c_i32),
         ("T", _c_i32),
+        ("n_rays", _c_i32),
         ("depth_scale", _c_f32),
         ("depth_offset", _c_f32),
         ("lo", _c_f32),
@@ -55,7 +56,7 @@ def _f32(x) -> float:
     return float(np.float32(x))
 
 
-def render_params(cfg: dict, T: int) -> RenderParams:
+def render_params(cfg: dict, T: int, n_rays: int | None = None) -> RenderParams:
     """Round the `render:` scalars exactly as the reference's torch ops do.
 
     Python evaluates the scalar sub-expressions in double (renderer.py:54,
@@ -66,6 +67,7 @@ def render_params(cfg: dict, T: int) -> RenderParams:
     p.n_ele = int(cfg["n_ele"])
     p.n_samples = int(cfg["n_samples"])
     p.T = int(T)
+    p.n_rays = p.n_azi * p.n_ele + 2 if n_rays is None else int(n_rays)
     p.depth_scale = _f32(cfg["far"] - cfg["near"])
     p.depth_offset = _f32(cfg["near"])
     p.lo = _f32(cfg["xyz_min"])
@@ -124,7 +126,7 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.avr_abi_version() != 1:
+        if lib.avr_abi_version() != 2:
             raise RuntimeError("avr_amd: libavr_hip.so ABI version mismatch")
         _lib = lib
         return lib

@@ -78,6 +78,9 @@ __device__ __forceinline__ int source_delay(const avr_render_params& p, const fl
     return (int)r;
 }
 
-__host__ __device__ inline int n_rays(const avr_render_params& p) { return p.n_azi * p.n_ele + 2; }
+// rays of the render core (a shard of the sphere when rays are split over GPUs)
+__host__ __device__ inline int n_rays(const avr_render_params& p) { return p.n_rays; }
+// all rays of the sphere (ray generation)
+__host__ __device__ inline int grid_rays(const avr_render_params& p) { return p.n_azi * p.n_ele + 2; }
 
 }  // namespace avr

@@ -75,7 +75,7 @@ __global__ void ir_twiddle_kernel(int n, float2* __restrict__ tw) {
 // once (the reference uses SLEEF u10; components may differ by 1 ulp).
 __global__ void ray_directions_kernel(avr_render_params p, const float* __restrict__ u_azi,
                                       float* __restrict__ dirs) {
-    const int R = n_rays(p);
+    const int R = grid_rays(p);
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R) return;
     float x, y, z;
@@ -245,7 +245,7 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
         d_l[i] = delay[idx];
     }
     __syncthreads();
-    if (nr <= 0) return;
+    // an empty split (nr <= 0) falls through both loops and writes zeros
     const int64_t row0 = (((int64_t)b * R + r0) * S + s) * (int64_t)T;
     const int phase = (int)(row0 % VEC);
     const int nchunks = (T + phase + VEC - 1) / VEC;
@@ -474,6 +474,8 @@ int validate(const avr_render_params* p) {
     if (p->n_azi < 1 || p->n_ele < 1 || p->n_samples < 1 || p->T < 2)
         return fail(AVR_E_CONFIG, "n_azi, n_ele, n_samples must be >=1 and T >= 2");
     if (p->T > 16384) return fail(AVR_E_CONFIG, "T > 16384 not supported");
+    if (p->n_rays < 1 || p->n_rays > grid_rays(*p))
+        return fail(AVR_E_CONFIG, "n_rays must be in [1, n_azi*n_ele+2]");
     if (p->n_samples > 8192) return fail(AVR_E_CONFIG, "n_samples > 8192 not supported");
     return 0;
 }
@@ -512,7 +514,7 @@ extern "C" int avr_ray_directions(const avr_render_params* p, const float* u_azi
                                   void* stream) {
     if (int e = validate(p)) return e;
     AVR_REQUIRE(u_azi && dirs, "avr_ray_directions: null pointer");
-    const int R = n_rays(*p);
+    const int R = grid_rays(*p);
     hipLaunchKernelGGL(ray_directions_kernel, dim3((R + 255) / 256), dim3(256), 0,
                        as_stream(stream), *p, u_azi, dirs);
     return check_launch("avr_ray_directions");

@@ -151,7 +151,7 @@ class RenderCore(torch.autograd.Function):
     def forward(ctx, attn, signal, p, tables, rays_o, position_tx, dirs):
         dev = signal.device
         B = signal.size(0)
-        R, S, T = p.n_azi * p.n_ele + 2, p.n_samples, p.T
+        R, S, T = p.n_rays, p.n_samples, p.T
         F = T // 2 + 1
         st = _stream(dev)
         pref = ctypes_ref(p)
@@ -186,7 +186,7 @@ class RenderCore(torch.autograd.Function):
         p, tables = ctx.p, ctx.tables
         dev = signal.device
         B = signal.size(0)
-        R, S, T = p.n_azi * p.n_ele + 2, p.n_samples, p.T
+        R, S, T = p.n_rays, p.n_samples, p.T
         st = _stream(dev)
         pref = ctypes_ref(p)
         g = grad_out.contiguous().float()
@@ -258,7 +258,7 @@ class AVRRender(nn.Module):
         for k in _RENDER_KEYS:
             setattr(self, k, kwargs[k])
         self._cfg = {k: kwargs[k] for k in _RENDER_KEYS}
-        self.last_network_inputs = None
+        self.ray_range = None  # (r0, r1) when rays are sharded over GPUs
 
     # -- stages, exposed for tests and for callers that bring their own network
     def _device(self, rays_o):
@@ -272,14 +272,21 @@ class AVRRender(nn.Module):
         """Ray generation + sampling (renderer.py:53-62) -> network inputs.
 
         Returns (pts, view, tx, dir_tx_or_None, geom) where geom carries the
-        device tensors the render core needs.
+        device tensors the render core needs.  When `self.ray_range` is set
+        (ray sharding, avr_amd.parallel) only rays [r0, r1) are sampled; the
+        jitter draw and the full direction set are still computed so every
+        shard sees the same sphere.
         """
         dev = self._device(rays_o)
         B = position_tx.size(0)
         if u_azi is None:
             u_azi = draw_jitter(self.n_azi, self.n_ele)
-        p0 = render_params(self._cfg, 2)
-        R, S = p0.n_azi * p0.n_ele + 2, p0.n_samples
+        R_all = int(self.n_azi) * int(self.n_ele) + 2
+        r0, r1 = self.ray_range if self.ray_range is not None else (0, R_all)
+        if not (0 <= r0 < r1 <= R_all):
+            raise ValueError(f"ray_range {self.ray_range} outside [0, {R_all})")
+        p0 = render_params(self._cfg, 2, n_rays=r1 - r0)
+        R, S = r1 - r0, p0.n_samples
         f32 = dict(dtype=torch.float32, device=dev)
         rays_o = rays_o.to(dev, torch.float32).contiguous()
         position_tx = position_tx.to(dev, torch.float32).contiguous()
@@ -287,12 +294,13 @@ class AVRRender(nn.Module):
             direction_tx = direction_tx.to(dev, torch.float32).contiguous()
         st = _stream(dev)
         pref = ctypes_ref(p0)
-        dirs = torch.empty(R, 3, **f32)
+        dirs_all = torch.empty(R_all, 3, **f32)
         u_dev = u_azi.to(dev, torch.float32, non_blocking=True)
         d_vals = torch.empty(S, **f32)
         with torch.cuda.device(dev):
-            _lib.call("avr_ray_directions", pref, _ptr(u_dev), _ptr(dirs), st)
+            _lib.call("avr_ray_directions", pref, _ptr(u_dev), _ptr(dirs_all), st)
             _lib.call("avr_depth_samples", pref, _ptr(d_vals), st)
+            dirs = dirs_all[r0:r1]
             pts = torch.empty(B, R * S, 3, **f32)
             view = torch.empty(B, R * S, 3, **f32)
             tx = torch.empty(B, R * S, 3, **f32)
@@ -300,7 +308,8 @@ class AVRRender(nn.Module):
             _lib.call("avr_sample_points", pref, B, _ptr(rays_o), _ptr(position_tx),
                       _ptr(direction_tx), _ptr(dirs), _ptr(d_vals), _ptr(pts), _ptr(view),
                       _ptr(tx), _ptr(dtx), st)
-        geom = dict(rays_o=rays_o, position_tx=position_tx, dirs=dirs, device=dev, B=B)
+        geom = dict(rays_o=rays_o, position_tx=position_tx, dirs=dirs, device=dev, B=B,
+                    n_rays=R, dirs_all=dirs_all)
         return pts, view, tx, dtx, geom
 
     def render_from_network_output(self, attn, signal, geom):
@@ -314,11 +323,11 @@ class AVRRender(nn.Module):
         attn = attn.to(dev).reshape(B, -1).contiguous()
         T = signal.size(-1)
         signal = signal.to(dev).reshape(B, -1, T).contiguous()
-        R = self.n_azi * self.n_ele + 2
+        R = geom["n_rays"]
         if attn.size(1) != R * S or signal.size(1) != R * S:
             raise ValueError(f"network output has {signal.size(1)} ray-samples, expected "
                              f"{R}x{S}={R * S}")
-        p = render_params(self._cfg, T)
+        p = render_params(self._cfg, T, n_rays=R)
         with torch.cuda.device(dev):
             tables = get_tables(p, dev)
             check_config(p, tables)
@@ -328,7 +337,6 @@ class AVRRender(nn.Module):
     def forward(self, rays_o, position_tx, direction_tx=None, ch_idx=None):
         """Render [B, F, 2] (real, imag) spectra; see renderer.py:31-124."""
         pts, view, tx, dtx, geom = self.sample(rays_o, position_tx, direction_tx)
-        self.last_network_inputs = None
         kw = {} if ch_idx is None else {"ch_idx": ch_idx}
         if dtx is not None:
             attn, signal = self.network_fn(pts, view, tx, dtx, **kw)

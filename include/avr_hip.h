@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define AVR_ABI_VERSION 1
+#define AVR_ABI_VERSION 2
 
 /* element types of network outputs / gradients */
 #define AVR_DTYPE_F32 0
@@ -52,6 +52,8 @@ typedef struct avr_render_params {
     int32_t n_ele;        /* elevation rings */
     int32_t n_samples;    /* S */
     int32_t T;            /* signal_output_dim */
+    int32_t n_rays;       /* rays handled by the render-core kernels: n_azi*n_ele+2,
+                             or the size of this rank's contiguous ray shard */
     float depth_scale;    /* fp32(far - near)            renderer.py:54 */
     float depth_offset;   /* fp32(near)                  renderer.py:54 */
     float lo;             /* fp32(xyz_min)               renderer.py:128 */
@@ -86,13 +88,14 @@ int avr_ir_twiddle(int32_t n, float* tw, void* stream);
 
 /* ---- a2: spherical ray directions (renderer.py:133-165) ----------------
  * u_azi[n_azi] are the CPU-generator U[0,1) draws (renderer.py:149);
- * writes dirs[R][3]. */
+ * writes all n_azi*n_ele+2 directions dirs[..][3] (ignores p->n_rays). */
 int avr_ray_directions(const avr_render_params* p, const float* u_azi, float* dirs,
                        void* stream);
 
 /* ---- a3/a4: samples and network inputs (renderer.py:54-62) ------------
- * rays_o, pos_tx, dir_tx: [B][3] (dir_tx may be NULL).  Writes the four
- * network inputs [B][R*S][3]; net_dir_tx is ignored when dir_tx is NULL. */
+ * rays_o, pos_tx, dir_tx: [B][3] (dir_tx may be NULL); dirs points at the
+ * first of the p->n_rays directions to sample.  Writes the four network
+ * inputs [B][R*S][3] (R = p->n_rays); net_dir_tx unused when dir_tx is NULL. */
 int avr_sample_points(const avr_render_params* p, int32_t B, const float* rays_o,
                       const float* pos_tx, const float* dir_tx, const float* dirs,
                       const float* d_vals, float* net_pts, float* net_view, float* net_tx,

@@ -111,7 +111,9 @@ def test_stage_weights_delays_tables(name):
     np.testing.assert_allclose(dirs, case["dirs"], rtol=0, atol=5e-7)
     np.testing.assert_allclose(tables.d_vals.cpu().numpy(), case["d_vals"], rtol=0, atol=0)
     np.testing.assert_array_equal(tables.shift.cpu().numpy(), case["shift"].astype(np.int32))
-    digest_check(case, "weights", wt, rtol=2e-5, atol=1e-9)
+    # weights are <= 1; device expf and the tree-ordered transmittance scan
+    # differ from torch's SLEEF expf + sequential cumprod by a few ulp
+    digest_check(case, "weights", wt, rtol=1e-5, atol=2e-7)
     if case.has("delay"):
         agree = (dl == case["delay"]).mean()
     else:
@@ -234,3 +236,31 @@ def test_config2_full_size_properties():
     ob, *_ = hip_render(case, ib, case.seed)
     s = oa.detach().cpu().numpy() + ob.detach().cpu().numpy()
     assert rel_l2(s, base) < 1e-5
+
+
+@pytest.mark.parametrize("n_shards", [2, 3])
+def test_ray_range_shards_sum_to_full(n_shards):
+    """Rays split into contiguous ranges (the multi-GPU ray sharding) sum to
+    the single-device spectrum."""
+    from avr_amd.parallel import shard_range
+
+    case = Case("c3_s0")
+    inp = case.inputs()
+    w = case.workload
+    B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
+    attn = torch.from_numpy(inp["attn"]).to(DEV).view(B, R, S, 1)
+    sig = torch.from_numpy(inp["signal"]).to(DEV).view(B, R, S, T)
+    ro = torch.from_numpy(inp["rays_o"]).to(DEV)
+    tx = torch.from_numpy(inp["position_tx"]).to(DEV)
+    dtx = torch.from_numpy(inp["direction_tx"]).to(DEV)
+    total = None
+    for k in range(n_shards):
+        r0, r1 = shard_range(R, k, n_shards)
+        net = Net(attn[:, r0:r1].reshape(B, -1, 1).contiguous(), sig[:, r0:r1].reshape(B, -1, T).contiguous())
+        r = AVRRender(net, **w.render)
+        r.ray_range = (r0, r1)
+        torch.manual_seed(case.seed)
+        part = r(ro, tx, dtx)
+        assert net.seen[0].shape[1] == (r1 - r0) * S
+        total = part if total is None else total + part
+    assert rel_l2(total.cpu().numpy(), case["out"]) < TOL

@@ -43,7 +43,7 @@ def test_python_binding_covers_header():
 
 
 def test_abi_version(lib):
-    assert lib.avr_abi_version() == 1
+    assert lib.avr_abi_version() == 2
 
 
 def test_argument_errors_are_reported_without_gpu(lib):

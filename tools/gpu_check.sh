@@ -1,0 +1,27 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, kernel-trace profile.
+# Stops at the first crash/timeout (exit >= 124 or signal); test assertion
+# failures (pytest exit 1) do not stop the later steps.
+set -u
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+step() {  # name, timeout, command...
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 $t "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 25 $OUT/$name.log
+  if [ $rc -ge 124 ] || [ $rc -gt 1 -a $rc -ne 5 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py ;;
+    benchq) step bench_q 300 python bench.py --no-cpu-baseline --steps 100 ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 50 --warmup 5 ;;
+  esac
+done
