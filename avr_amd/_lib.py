@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(_HERE, "libavr_hip.so")
 
 DTYPE_F32 = 0
 DTYPE_F16 = 1
+MAX_AZI = 512  # AVR_MAX_AZI
 
 _c_i32 = ctypes.c_int32
 _c_i64 = ctypes.c_int64
@@ -91,6 +92,7 @@ _SIGS = {
     "avr_ir_twiddle": (ctypes.c_int, [_c_i32, _vp, _vp]),
     "avr_ray_directions": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
     "avr_sample_points": (ctypes.c_int, [_vp, _c_i32] + [_vp] * 10),
+    "avr_sample_rays": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32] + [_vp] * 9),
     "avr_weights_fwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32] + [_vp] * 7),
     "avr_ray_reduce_fwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32, _vp, _vp, _c_i32, _vp, _vp]),
     "avr_dft_phase_fwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32, _vp, _vp, _vp, _vp, _c_i32, _vp, _vp]),

@@ -8,6 +8,8 @@
 // roofline of each kernel.
 #include "common.h"
 
+#include <cstdlib>
+
 using namespace avr;
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -73,33 +75,38 @@ __global__ void ir_twiddle_kernel(int n, float2* __restrict__ tw) {
 // renderer.py:147-165: azimuth linspace + jitter, elevation acos ring,
 // meshgrid(ij) azimuth-major, then the two poles.  Trig in double, rounded
 // once (the reference uses SLEEF u10; components may differ by 1 ulp).
-__global__ void ray_directions_kernel(avr_render_params p, const float* __restrict__ u_azi,
-                                      float* __restrict__ dirs) {
-    const int R = grid_rays(p);
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= R) return;
-    float x, y, z;
+__device__ __forceinline__ void ray_direction(const avr_render_params& p, float u, int r,
+                                              float* out) {
     const int grid = p.n_azi * p.n_ele;
     if (r < grid) {
         const int ia = r / p.n_ele, ie = r % p.n_ele;
         const float base = linspace_at(0.0f, p.two_pi, p.n_azi + 1, ia);
-        const float jit = p.azi_jitter * u_azi[ia];
+        const float jit = p.azi_jitter * u;
         const float azi = base + jit;
         const float el_lin = linspace_at(0.0f, 1.0f, p.n_ele + 2, ie + 1);
         const float el_arg = 2.0f * el_lin - 1.0f;
         const float ele = (float)acos((double)el_arg);
         const float se = (float)sin((double)ele);
-        x = (float)cos((double)azi) * se;
-        y = (float)sin((double)azi) * se;
-        z = (float)cos((double)ele);
+        out[0] = (float)cos((double)azi) * se;
+        out[1] = (float)sin((double)azi) * se;
+        out[2] = (float)cos((double)ele);
     } else {
-        x = 0.0f;
-        y = 0.0f;
-        z = (r == grid) ? 1.0f : -1.0f;
+        out[0] = 0.0f;
+        out[1] = 0.0f;
+        out[2] = (r == grid) ? 1.0f : -1.0f;
     }
-    dirs[r * 3 + 0] = x;
-    dirs[r * 3 + 1] = y;
-    dirs[r * 3 + 2] = z;
+}
+
+__global__ void ray_directions_kernel(avr_render_params p, const float* __restrict__ u_azi,
+                                      float* __restrict__ dirs) {
+    const int R = grid_rays(p);
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= R) return;
+    float d[3];
+    ray_direction(p, r < p.n_azi * p.n_ele ? u_azi[r / p.n_ele] : 0.0f, r, d);
+    dirs[r * 3 + 0] = d[0];
+    dirs[r * 3 + 1] = d[1];
+    dirs[r * 3 + 2] = d[2];
 }
 
 // ------------------------------------------------- a3/a4: network inputs
@@ -127,6 +134,47 @@ __global__ void sample_points_kernel(avr_render_params p, int B, const float* __
             const float world = rays_o[b * 3 + c] + dc * d;
             net_pts[i * 3 + c] = to_unit(world, p.lo, p.span);
             net_view[i * 3 + c] = -dc;
+            net_tx[i * 3 + c] = to_unit(pos_tx[b * 3 + c], p.lo, p.span);
+            if (dir_tx) net_dir_tx[i * 3 + c] = dir_tx[b * 3 + c];
+        }
+    }
+}
+
+// Fused a2+a3+a4 for the hot path: the azimuth jitter arrives by value in the
+// kernel arguments (no host->device copy), every wave derives its ray's
+// direction and depth itself, and the shard's directions are written once
+// for the weights kernel.  One launch instead of three plus a copy.
+struct AziJitter {
+    float u[AVR_MAX_AZI];
+};
+
+__global__ __launch_bounds__(256) void sample_rays_kernel(
+    avr_render_params p, int B, AziJitter jit, int r_begin, const float* __restrict__ rays_o,
+    const float* __restrict__ pos_tx, const float* __restrict__ dir_tx, float* __restrict__ dirs,
+    float* __restrict__ net_pts, float* __restrict__ net_view, float* __restrict__ net_tx,
+    float* __restrict__ net_dir_tx) {
+    const int R = n_rays(p), S = p.n_samples;
+    const int64_t n = (int64_t)B * R * S;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int s = (int)(i % S);
+        const int64_t br = i / S;
+        const int rl = (int)(br % R);
+        const int b = (int)(br / R);
+        const int r = r_begin + rl;
+        float dir[3];
+        ray_direction(p, r < p.n_azi * p.n_ele ? jit.u[r / p.n_ele] : 0.0f, r, dir);
+        const float d = linspace_at(0.0f, 1.0f, S, s) * p.depth_scale + p.depth_offset;
+        if (b == 0 && s == 0) {
+            dirs[rl * 3 + 0] = dir[0];
+            dirs[rl * 3 + 1] = dir[1];
+            dirs[rl * 3 + 2] = dir[2];
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float world = rays_o[b * 3 + c] + dir[c] * d;
+            net_pts[i * 3 + c] = to_unit(world, p.lo, p.span);
+            net_view[i * 3 + c] = -dir[c];
             net_tx[i * 3 + c] = to_unit(pos_tx[b * 3 + c], p.lo, p.span);
             if (dir_tx) net_dir_tx[i * 3 + c] = dir_tx[b * 3 + c];
         }
@@ -201,20 +249,22 @@ __global__ __launch_bounds__(256) void weights_fwd_kernel(
 // split are gathered into LDS once.
 template <typename Tin>
 struct Vec16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <>
 struct Vec16<float> {
     static constexpr int N = 4;
-    using raw = float4;
+    using raw = f32x4;
     __device__ static void cvt(const raw& v, float* o) {
-        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+        o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
     }
 };
 template <>
 struct Vec16<__half> {
     static constexpr int N = 8;
-    using raw = uint4;
+    using raw = u32x4;
     __device__ static void cvt(const raw& v, float* o) {
-        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t u[4] = {v[0], v[1], v[2], v[3]};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             __half2 h = *reinterpret_cast<const __half2*>(&u[i]);
@@ -227,9 +277,7 @@ struct Vec16<__half> {
 
 constexpr int kReduceThreads = 256;
 constexpr int kMaxRaysPerSplit = 2048;
-constexpr int kUnroll = 4;
-
-template <typename Tin, bool VECTOR, int CPT>
+template <typename Tin, bool VECTOR, int CPT, int kUnroll, bool NT>
 __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
     const Tin* __restrict__ sig, const float* __restrict__ w, const int32_t* __restrict__ delay,
     float* __restrict__ part, int B, int R, int S, int T, int rays_per_split, int64_t total) {
@@ -270,8 +318,12 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
         const int64_t e0 = rowbase + (int64_t)j * VEC;  // first element of the chunk
         if constexpr (VECTOR) {
             if (e0 + VEC <= total) {
-                typename Vec16<Tin>::raw v =
-                    *reinterpret_cast<const typename Vec16<Tin>::raw*>(sig + e0);
+                const auto* vp = reinterpret_cast<const typename Vec16<Tin>::raw*>(sig + e0);
+                typename Vec16<Tin>::raw v;
+                if constexpr (NT)
+                    v = __builtin_nontemporal_load(vp);
+                else
+                    v = *vp;
                 Vec16<Tin>::cvt(v, x);
                 return;
             }
@@ -338,8 +390,14 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
 constexpr int kDftThreads = 256;
 constexpr int kKc = 64;  // t per LDS stage
 
+// A-tile staging (see `stage` below): thread owns column t = kc + (tid & 63)
+// of rows (tid >> 6) + 4i, i < 8.  Addresses are clamped to valid locations
+// and masked afterwards, so all 8*NS partial loads (+ 8 path-loss loads)
+// issue back to back with no per-element branch, and the next tile's loads
+// are in flight while the MFMAs consume the current one.
+template <int NS>
 __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
-    const float* __restrict__ part, int n_split, const float* __restrict__ pl,
+    const float* __restrict__ part, const float* __restrict__ pl,
     const int32_t* __restrict__ shift, const float2* __restrict__ phase,
     const float2* __restrict__ twg, float2* __restrict__ spart, int B, int S, int T, int KS,
     int kchunk) {
@@ -356,6 +414,22 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
     const int half = lane >> 5;
     for (int i = threadIdx.x; i < T; i += kDftThreads) tw[i] = twg[i];
 
+    // this thread's staging rows
+    const int col = threadIdx.x & 63, row0 = threadIdx.x >> 6;
+    int sh[8];
+    bool srow[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int s = stile * 32 + row0 + 4 * i;
+        srow[i] = s < S;
+        sh[i] = shift[min(s, S - 1)];
+    }
+    const int64_t slab = (int64_t)B * S * T;
+    // rows beyond S are clamped to row S-1 (masked by srow)
+    const int s_first = min(stile * 32 + row0, S - 1);
+    const int64_t rowbase0 = ((int64_t)b * S + s_first) * T;
+    const int64_t max_row_off = ((int64_t)b * S + (S - 1)) * T;
+
     const int k0 = ks * kchunk;
     const int k1 = min(T, k0 + kchunk);
     floatx16 acc_re, acc_im;
@@ -364,26 +438,36 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
         acc_re[i] = 0.0f;
         acc_im[i] = 0.0f;
     }
-    const int64_t slab = (int64_t)B * S * T;
     const int inc = (int)((2LL * fm) % T);
+    float cur[8];
+    auto stage = [&](int kc, float* v) {
+        // per-row clamp: the shared rowbase0 + 4i*T may exceed the last row for ragged S
+        const int t = kc + col;
+        const int tc = min(t, T - 1);
+        float acc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int64_t ro = min(rowbase0 + (int64_t)(4 * i) * T, max_row_off);
+                acc[i] += part[k * slab + ro + tc];
+            }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const bool ok = srow[i] && t < k1 && t < T - 1 - sh[i];
+            const float g = pl[sh[i] + tc];
+            v[i] = ok ? acc[i] * g : 0.0f;
+        }
+    };
+    if (k0 < k1) stage(k0, cur);
     for (int kc = k0; kc < k1; kc += kKc) {
         __syncthreads();
-        for (int e = threadIdx.x; e < 32 * kKc; e += kDftThreads) {
-            const int row = e / kKc, col = e % kKc;
-            const int s = stile * 32 + row, t = kc + col;
-            float v = 0.0f;
-            if (s < S && t < k1) {
-                const int sh = shift[s];
-                if (t < T - 1 - sh) {
-                    const float* src = part + ((int64_t)b * S + s) * T + t;
-                    float sum = 0.0f;
-                    for (int k = 0; k < n_split; ++k) sum += src[k * slab];
-                    v = sum * pl[sh + t];
-                }
-            }
-            As[row][col] = v;
-        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) As[row0 + 4 * i][col] = cur[i];
         __syncthreads();
+        if (kc + kKc < k1) stage(kc + kKc, cur);  // next tile's loads fly under the MFMAs
         int idx = (int)(((int64_t)(kc + half) * fm) % T);
 #pragma unroll 8
         for (int kk = 0; kk < kKc; kk += 2) {
@@ -416,29 +500,53 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
     }
 }
 
-__global__ void spectrum_finalize_kernel(int B, int P, int F, const float2* __restrict__ spart,
-                                         float2* __restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)B * F) return;
-    const int b = (int)(i / F), f = (int)(i % F);
-    float re = 0.0f, im = 0.0f;
-    const float2* src = spart + (int64_t)b * P * F + f;
-    for (int q = 0; q < P; ++q) {
-        const float2 v = src[(int64_t)q * F];
-        re += v.x;
-        im += v.y;
+// out[b,f] = sum_p spart[b,p,f]: 4 partial-groups x 64 bins per block,
+// coalesced loads, fixed-order LDS combine (deterministic).
+__global__ __launch_bounds__(256) void spectrum_finalize_kernel(int B, int P, int F,
+                                                                const float2* __restrict__ spart,
+                                                                float2* __restrict__ out) {
+    __shared__ float2 red[4][64];
+    const int b = blockIdx.y;
+    const int g = threadIdx.x >> 6, j = threadIdx.x & 63;
+    const int f = blockIdx.x * 64 + j;
+    const int fc = min(f, F - 1);
+    const float2* src = spart + (int64_t)b * P * F + fc;
+    float2 a0 = make_float2(0.f, 0.f), a1 = a0;
+    int q = g;
+    for (; q + 4 < P; q += 8) {
+        const float2 v0 = src[(int64_t)q * F];
+        const float2 v1 = src[(int64_t)(q + 4) * F];
+        a0.x += v0.x; a0.y += v0.y;
+        a1.x += v1.x; a1.y += v1.y;
     }
-    out[i] = make_float2(re, im);
+    if (q < P) {
+        const float2 v0 = src[(int64_t)q * F];
+        a0.x += v0.x; a0.y += v0.y;
+    }
+    red[g][j] = make_float2(a0.x + a1.x, a0.y + a1.y);
+    __syncthreads();
+    if (g == 0 && f < F) {
+        float2 r = red[0][j];
+        for (int k = 1; k < 4; ++k) {
+            r.x += red[k][j].x;
+            r.y += red[k][j].y;
+        }
+        out[(int64_t)b * F + f] = r;
+    }
 }
 
 // -------------------------------------------------- a13: irfft -> IR
 // torch.fft.irfft semantics (n = 2(F-1), backward norm 1/n, imaginary parts
 // of the DC and Nyquist bins ignored):
 //   ir[t] = (X0 + (-1)^t X_{n/2} + 2 sum_{k=1}^{n/2-1} Re(X_k e^{2 pi i k t/n})) / n
+// Block = 32 output samples x 8 bin-slices; each thread walks bins
+// k = 1 + slice + 8j with four independent index chains (ILP over the LDS
+// latency), then the 8 slices are combined in LDS in a fixed order.
 __global__ __launch_bounds__(256) void irfft_kernel(int F, const float2* __restrict__ spec,
                                                     const float2* __restrict__ twg,
                                                     float* __restrict__ ir) {
     extern __shared__ float2 lds[];
+    __shared__ float red[8][33];
     const int n = 2 * (F - 1);
     float2* X = lds;       // [F]
     float2* tw = lds + F;  // [n]
@@ -446,20 +554,42 @@ __global__ __launch_bounds__(256) void irfft_kernel(int F, const float2* __restr
     for (int i = threadIdx.x; i < F; i += blockDim.x) X[i] = spec[(int64_t)b * F + i];
     for (int i = threadIdx.x; i < n; i += blockDim.x) tw[i] = twg[i];
     __syncthreads();
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
-    float acc = 0.0f;
-    int idx = t % n;  // k = 1
-    for (int k = 1; k < F - 1; ++k) {
-        const float2 c = tw[idx];
-        const float2 x = X[k];
-        acc += x.x * c.x - x.y * c.y;
-        idx += t;
-        if (idx >= n) idx -= n;
+    const int tl = threadIdx.x & 31, slice = threadIdx.x >> 5;
+    const int t = blockIdx.x * 32 + tl;
+    const int tm = (t < n) ? t : 0;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    int idx[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) idx[c] = (int)(((int64_t)(1 + slice + 8 * c) * tm) % n);
+    const int step4 = (int)((32LL * tm) % n);
+    int k = 1 + slice;
+    for (; k + 24 < F - 1; k += 32) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const float2 w = tw[idx[c]];
+            const float2 x = X[k + 8 * c];
+            acc[c] += x.x * w.x - x.y * w.y;
+            idx[c] += step4;
+            if (idx[c] >= n) idx[c] -= n;
+        }
     }
-    const float nyq = (t & 1) ? -X[F - 1].x : X[F - 1].x;
-    const float v = (X[0].x + nyq) + 2.0f * acc;
-    ir[(int64_t)b * n + t] = v / (float)n;
+    for (; k < F - 1; k += 8) {
+        // tail bins of this slice
+        const int id = (int)(((int64_t)k * tm) % n);
+        const float2 w = tw[id];
+        const float2 x = X[k];
+        acc[0] += x.x * w.x - x.y * w.y;
+    }
+    red[slice][tl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    __syncthreads();
+    if (slice == 0 && t < n) {
+        float s = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s += red[q][tl];
+        const float nyq = (t & 1) ? -X[F - 1].x : X[F - 1].x;
+        const float v = (X[0].x + nyq) + 2.0f * s;
+        ir[(int64_t)b * n + t] = v / (float)n;
+    }
 }
 
 int pick_blocks(int64_t n, int threads, int cap = 4096) {
@@ -535,6 +665,26 @@ extern "C" int avr_sample_points(const avr_render_params* p, int32_t B, const fl
     return check_launch("avr_sample_points");
 }
 
+extern "C" int avr_sample_rays(const avr_render_params* p, int32_t B, const float* u_azi_host,
+                               int32_t ray_begin, const float* rays_o, const float* pos_tx,
+                               const float* dir_tx, float* dirs, float* net_pts, float* net_view,
+                               float* net_tx, float* net_dir_tx, void* stream) {
+    if (int e = validate(p)) return e;
+    AVR_REQUIRE(B >= 1 && u_azi_host && rays_o && pos_tx && dirs && net_pts && net_view && net_tx,
+                "avr_sample_rays: bad args");
+    AVR_REQUIRE(!dir_tx || net_dir_tx, "avr_sample_rays: dir_tx given without net_dir_tx");
+    AVR_REQUIRE(p->n_azi <= AVR_MAX_AZI, "avr_sample_rays: n_azi > AVR_MAX_AZI (use avr_ray_directions)");
+    AVR_REQUIRE(ray_begin >= 0 && ray_begin + p->n_rays <= grid_rays(*p),
+                "avr_sample_rays: ray range outside the sphere");
+    AziJitter jit;
+    for (int i = 0; i < AVR_MAX_AZI; ++i) jit.u[i] = (i < p->n_azi) ? u_azi_host[i] : 0.0f;
+    const int64_t n = (int64_t)B * n_rays(*p) * p->n_samples;
+    hipLaunchKernelGGL(sample_rays_kernel, dim3(pick_blocks(n, 256, 8192)), dim3(256), 0,
+                       as_stream(stream), *p, (int)B, jit, (int)ray_begin, rays_o, pos_tx, dir_tx,
+                       dirs, net_pts, net_view, net_tx, dir_tx ? net_dir_tx : nullptr);
+    return check_launch("avr_sample_rays");
+}
+
 extern "C" int avr_weights_fwd(const avr_render_params* p, int32_t B, const void* attn,
                                int32_t attn_dtype, const float* rays_o, const float* pos_tx,
                                const float* dirs, const float* d_vals, float* w, int32_t* delay,
@@ -563,6 +713,42 @@ extern "C" int avr_weights_fwd(const avr_render_params* p, int32_t B, const void
 }
 
 namespace {
+// Streaming variant of the reduction (rows in flight per thread, non-temporal
+// loads).  AVR_REDUCE_VARIANT selects one for tuning runs ("u4", "u8",
+// "u4nt", "u8nt"); the default is the measured best.
+int reduce_variant() {
+    const char* v = getenv("AVR_REDUCE_VARIANT");
+    if (!v) return 1;
+    const std::string s(v);
+    if (s == "u4") return 0;
+    if (s == "u8") return 1;
+    if (s == "u4nt") return 2;
+    if (s == "u8nt") return 3;
+    return 1;
+}
+
+template <typename Tin, bool VECTOR, int C>
+void launch_reduce_cpt(dim3 grid, hipStream_t st, const Tin* s, const float* w, const int32_t* delay,
+                       float* part, int B, int R, int S, int T, int rps, int64_t total) {
+    switch (reduce_variant()) {
+        case 0:
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, false>), grid,
+                               dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T, rps, total);
+            break;
+        case 2:
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, true>), grid,
+                               dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T, rps, total);
+            break;
+        case 3:
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, true>), grid,
+                               dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T, rps, total);
+            break;
+        default:
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, false>), grid,
+                               dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T, rps, total);
+    }
+}
+
 template <typename Tin, bool VECTOR>
 int launch_reduce(const avr_render_params* p, int B, const void* sig, const float* w,
                   const int32_t* delay, int n_split, float* part, hipStream_t st) {
@@ -574,29 +760,15 @@ int launch_reduce(const avr_render_params* p, int B, const void* sig, const floa
     const int64_t total = (int64_t)B * R * S * T;
     const dim3 grid(n_split, S, B);
     const Tin* s = (const Tin*)sig;
-#define AVR_RR(C)                                                                            \
-    case C:                                                                                  \
-        hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C>), grid, dim3(kReduceThreads), \
-                           0, st, s, w, delay, part, B, R, S, T, rps, total);                \
-        break;
-    switch (cpt) {
-        AVR_RR(1) AVR_RR(2) AVR_RR(3) AVR_RR(4) AVR_RR(5) AVR_RR(6) AVR_RR(7) AVR_RR(8)
-        AVR_RR(12) AVR_RR(16)
-        default: {
-            if (cpt <= 12) {
-                hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, 12>), grid,
-                                   dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T,
-                                   rps, total);
-            } else if (cpt <= 16) {
-                hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, 16>), grid,
-                                   dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T,
-                                   rps, total);
-            } else {
-                return fail(AVR_E_CONFIG, "ray_reduce: T too long for this build");
-            }
-        }
-    }
-#undef AVR_RR
+    if (cpt <= 1) launch_reduce_cpt<Tin, VECTOR, 1>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
+    else if (cpt <= 2) launch_reduce_cpt<Tin, VECTOR, 2>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
+    else if (cpt <= 3) launch_reduce_cpt<Tin, VECTOR, 3>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
+    else if (cpt <= 4) launch_reduce_cpt<Tin, VECTOR, 4>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
+    else if (cpt <= 6) launch_reduce_cpt<Tin, VECTOR, 6>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
+    else if (cpt <= 8) launch_reduce_cpt<Tin, VECTOR, 8>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
+    else if (cpt <= 12) launch_reduce_cpt<Tin, VECTOR, 12>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
+    else if (cpt <= 16) launch_reduce_cpt<Tin, VECTOR, 16>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
+    else return fail(AVR_E_CONFIG, "ray_reduce: T too long for this build");
     return check_launch("avr_ray_reduce_fwd");
 }
 }  // namespace
@@ -637,21 +809,30 @@ extern "C" int avr_dft_phase_fwd(const avr_render_params* p, int32_t B, const fl
     const int kchunk = ((nkc + k_split - 1) / k_split) * kKc;
     const dim3 grid((F + 127) / 128, ((S + 31) / 32) * k_split, B);
     const size_t lds = (size_t)T * sizeof(float2);
-    if (lds > 65536)
-        (void)hipFuncSetAttribute((const void*)dft_phase_fwd_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(dft_phase_fwd_kernel, grid, dim3(kDftThreads), lds, as_stream(stream), part,
-                       (int)n_split, pl_table, shift, reinterpret_cast<const float2*>(phase),
-                       reinterpret_cast<const float2*>(twiddle), reinterpret_cast<float2*>(spart),
-                       (int)B, S, T, (int)k_split, kchunk);
+    auto go = [&](auto kern) {
+        if (lds > 65536)
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)lds);
+        hipLaunchKernelGGL(kern, grid, dim3(kDftThreads), lds, as_stream(stream), part, pl_table,
+                           shift, reinterpret_cast<const float2*>(phase),
+                           reinterpret_cast<const float2*>(twiddle),
+                           reinterpret_cast<float2*>(spart), (int)B, S, T, (int)k_split, kchunk);
+    };
+    switch (n_split) {
+        case 1: go(dft_phase_fwd_kernel<1>); break;
+        case 2: go(dft_phase_fwd_kernel<2>); break;
+        case 4: go(dft_phase_fwd_kernel<4>); break;
+        case 8: go(dft_phase_fwd_kernel<8>); break;
+        case 16: go(dft_phase_fwd_kernel<16>); break;
+        default: return fail(AVR_E_ARG, "avr_dft_phase_fwd: n_split must be 1, 2, 4, 8 or 16");
+    }
     return check_launch("avr_dft_phase_fwd");
 }
 
 extern "C" int avr_spectrum_finalize(int32_t B, int32_t P, int32_t F, const float* spart,
                                      float* out, void* stream) {
     AVR_REQUIRE(B >= 1 && P >= 1 && F >= 1 && spart && out, "avr_spectrum_finalize: bad args");
-    const int64_t n = (int64_t)B * F;
-    hipLaunchKernelGGL(spectrum_finalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+    hipLaunchKernelGGL(spectrum_finalize_kernel, dim3((unsigned)((F + 63) / 64), B), dim3(256), 0,
                        as_stream(stream), (int)B, (int)P, (int)F,
                        reinterpret_cast<const float2*>(spart), reinterpret_cast<float2*>(out));
     return check_launch("avr_spectrum_finalize");
@@ -663,7 +844,7 @@ extern "C" int avr_irfft(int32_t B, int32_t F, const float* spec, const float* t
     const int n = 2 * (F - 1);
     AVR_REQUIRE(n <= 16384, "avr_irfft: n too large");
     const size_t lds = (size_t)(F + n) * sizeof(float2);
-    hipLaunchKernelGGL(irfft_kernel, dim3((n + 255) / 256, B), dim3(256), lds, as_stream(stream),
+    hipLaunchKernelGGL(irfft_kernel, dim3((n + 31) / 32, B), dim3(256), lds, as_stream(stream),
                        (int)F, reinterpret_cast<const float2*>(spec),
                        reinterpret_cast<const float2*>(tw), ir);
     return check_launch("avr_irfft");

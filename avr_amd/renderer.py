@@ -19,6 +19,7 @@ and `signal` outputs through `RenderCore`.  There is no CPU fallback.
 from __future__ import annotations
 
 import math
+import os
 import threading
 
 import numpy as np
@@ -119,21 +120,35 @@ def check_config(p, tables: Tables):
 # --------------------------------------------------------------------------
 # launch heuristics
 # --------------------------------------------------------------------------
+def _env_int(name):
+    v = os.environ.get(name)
+    return int(v) if v else None
+
+
 def pick_n_split(B, R, S):
-    """Ray splits for the reduction: ~1024 workgroups, <= 2048 rays per split."""
-    want = max(1, math.ceil(1024 / max(1, B * S)))
-    n = min(R, max(want, math.ceil(R / 2048)))
-    while n > 1 and math.ceil(R / n) < 8:
-        n -= 1
-    return max(1, n)
+    """Ray splits for the reduction (a power of two <= 16): about 1024
+    workgroups of 256 threads, at most 2048 rays per split.
+    AVR_NSPLIT overrides (tuning)."""
+    forced = _env_int("AVR_NSPLIT")
+    if forced:
+        return forced
+    n = 1
+    while n < 16 and (B * S * n < 1024 or math.ceil(R / n) > 2048) and math.ceil(R / (2 * n)) >= 8:
+        n *= 2
+    if math.ceil(R / n) > 2048:
+        raise ValueError(f"{R} rays need more than 16 splits of <= 2048")
+    return n
 
 
 def pick_k_split(B, S, T):
+    """t-slices of the DFT GEMM: about 256 workgroups. AVR_KSPLIT overrides."""
     F = T // 2 + 1
     nkc = math.ceil(T / 64)
+    forced = _env_int("AVR_KSPLIT")
+    if forced:
+        return max(1, min(nkc, forced))
     base = math.ceil(F / 128) * math.ceil(S / 32) * B
-    ks = max(1, min(nkc, math.ceil(512 / max(1, base))))
-    return ks
+    return max(1, min(nkc, math.ceil(256 / max(1, base))))
 
 
 # --------------------------------------------------------------------------
@@ -294,22 +309,30 @@ class AVRRender(nn.Module):
             direction_tx = direction_tx.to(dev, torch.float32).contiguous()
         st = _stream(dev)
         pref = ctypes_ref(p0)
-        dirs_all = torch.empty(R_all, 3, **f32)
-        u_dev = u_azi.to(dev, torch.float32, non_blocking=True)
-        d_vals = torch.empty(S, **f32)
+        pts = torch.empty(B, R * S, 3, **f32)
+        view = torch.empty(B, R * S, 3, **f32)
+        tx = torch.empty(B, R * S, 3, **f32)
+        dtx = torch.empty(B, R * S, 3, **f32) if direction_tx is not None else None
         with torch.cuda.device(dev):
-            _lib.call("avr_ray_directions", pref, _ptr(u_dev), _ptr(dirs_all), st)
-            _lib.call("avr_depth_samples", pref, _ptr(d_vals), st)
-            dirs = dirs_all[r0:r1]
-            pts = torch.empty(B, R * S, 3, **f32)
-            view = torch.empty(B, R * S, 3, **f32)
-            tx = torch.empty(B, R * S, 3, **f32)
-            dtx = torch.empty(B, R * S, 3, **f32) if direction_tx is not None else None
-            _lib.call("avr_sample_points", pref, B, _ptr(rays_o), _ptr(position_tx),
-                      _ptr(direction_tx), _ptr(dirs), _ptr(d_vals), _ptr(pts), _ptr(view),
-                      _ptr(tx), _ptr(dtx), st)
+            if p0.n_azi <= _lib.MAX_AZI:
+                # one fused launch; the jitter travels in the kernel arguments
+                u_host = np.ascontiguousarray(u_azi.detach().cpu().numpy(), dtype=np.float32)
+                dirs = torch.empty(R, 3, **f32)
+                _lib.call("avr_sample_rays", pref, B, u_host.ctypes.data, r0, _ptr(rays_o),
+                          _ptr(position_tx), _ptr(direction_tx), _ptr(dirs), _ptr(pts), _ptr(view),
+                          _ptr(tx), _ptr(dtx), st)
+            else:
+                dirs_all = torch.empty(R_all, 3, **f32)
+                u_dev = u_azi.to(dev, torch.float32)
+                d_vals = torch.empty(S, **f32)
+                _lib.call("avr_ray_directions", pref, _ptr(u_dev), _ptr(dirs_all), st)
+                _lib.call("avr_depth_samples", pref, _ptr(d_vals), st)
+                dirs = dirs_all[r0:r1]
+                _lib.call("avr_sample_points", pref, B, _ptr(rays_o), _ptr(position_tx),
+                          _ptr(direction_tx), _ptr(dirs), _ptr(d_vals), _ptr(pts), _ptr(view),
+                          _ptr(tx), _ptr(dtx), st)
         geom = dict(rays_o=rays_o, position_tx=position_tx, dirs=dirs, device=dev, B=B,
-                    n_rays=R, dirs_all=dirs_all)
+                    n_rays=R)
         return pts, view, tx, dtx, geom
 
     def render_from_network_output(self, attn, signal, geom):

@@ -101,6 +101,17 @@ int avr_sample_points(const avr_render_params* p, int32_t B, const float* rays_o
                       const float* d_vals, float* net_pts, float* net_view, float* net_tx,
                       float* net_dir_tx, void* stream);
 
+/* ---- a2+a3+a4 fused (the hot path's single launch before the network) --
+ * u_azi_host: HOST pointer to the n_azi jitter draws, passed by value in the
+ * kernel arguments (n_azi <= AVR_MAX_AZI).  Samples rays
+ * [ray_begin, ray_begin + p->n_rays) of the sphere, writes their directions
+ * dirs[p->n_rays][3] and the four network inputs [B][n_rays*S][3]. */
+#define AVR_MAX_AZI 512
+int avr_sample_rays(const avr_render_params* p, int32_t B, const float* u_azi_host,
+                    int32_t ray_begin, const float* rays_o, const float* pos_tx,
+                    const float* dir_tx, float* dirs, float* net_pts, float* net_view,
+                    float* net_tx, float* net_dir_tx, void* stream);
+
 /* ---- a8 + a11: source delays and compositing weights -------------------
  * attn [B][R*S] (dtype), writes w[B][R][S] fp32 and delay[B][R][S] int32.
  * One ray per wavefront, samples strided over lanes, transmittance by a
