@@ -80,6 +80,25 @@ __device__ __forceinline__ int source_delay(const avr_render_params& p, const fl
 
 // rays of the render core (a shard of the sphere when rays are split over GPUs)
 __host__ __device__ inline int n_rays(const avr_render_params& p) { return p.n_rays; }
+
+// Copy n float2 from global into LDS with every load of a round in flight
+// before the first LDS store (a plain strided loop serialises load->store
+// pairs).  Indices are clamped so no load sits behind a branch.
+template <int THREADS>
+__device__ __forceinline__ void stage_table(float2* __restrict__ dst, const float2* __restrict__ src,
+                                            int n) {
+    constexpr int R = 8;
+    for (int base = 0; base < n; base += R * THREADS) {
+        float2 v[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) v[i] = src[min(base + i * THREADS + (int)threadIdx.x, n - 1)];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int j = base + i * THREADS + (int)threadIdx.x;
+            if (j < n) dst[j] = v[i];
+        }
+    }
+}
 // all rays of the sphere (ray generation)
 __host__ __device__ inline int grid_rays(const avr_render_params& p) { return p.n_azi * p.n_ele + 2; }
 

@@ -40,7 +40,7 @@ __global__ __launch_bounds__(kBwdThreads) void dft_phase_bwd_kernel(
     const int tm = (t < T) ? t : 0;
     const int kq = lane >> 4;            // 0..3
     const int fo = kq >> 1, comp = kq & 1;
-    for (int i = threadIdx.x; i < T; i += kBwdThreads) tw[i] = twg[i];
+    stage_table<kBwdThreads>(tw, twg, T);
     floatx4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     const int inc = (int)((2LL * tm) % T);
     for (int fc = 0; fc < F; fc += kFc) {

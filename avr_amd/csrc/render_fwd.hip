@@ -148,36 +148,45 @@ struct AziJitter {
     float u[AVR_MAX_AZI];
 };
 
-__global__ __launch_bounds__(256) void sample_rays_kernel(
+constexpr int kSampleThreads = 256;
+
+__global__ __launch_bounds__(kSampleThreads) void sample_rays_kernel(
     avr_render_params p, int B, AziJitter jit, int r_begin, const float* __restrict__ rays_o,
     const float* __restrict__ pos_tx, const float* __restrict__ dir_tx, float* __restrict__ dirs,
     float* __restrict__ net_pts, float* __restrict__ net_view, float* __restrict__ net_tx,
     float* __restrict__ net_dir_tx) {
+    // directions of the (at most 256/S + 2) rays this block touches, once each
+    __shared__ float sdir[kSampleThreads + 1][3];
     const int R = n_rays(p), S = p.n_samples;
     const int64_t n = (int64_t)B * R * S;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int s = (int)(i % S);
-        const int64_t br = i / S;
-        const int rl = (int)(br % R);
-        const int b = (int)(br / R);
-        const int r = r_begin + rl;
-        float dir[3];
-        ray_direction(p, r < p.n_azi * p.n_ele ? jit.u[r / p.n_ele] : 0.0f, r, dir);
-        const float d = linspace_at(0.0f, 1.0f, S, s) * p.depth_scale + p.depth_offset;
-        if (b == 0 && s == 0) {
-            dirs[rl * 3 + 0] = dir[0];
-            dirs[rl * 3 + 1] = dir[1];
-            dirs[rl * 3 + 2] = dir[2];
-        }
+    const int64_t i0 = (int64_t)blockIdx.x * kSampleThreads;
+    const int64_t br0 = i0 / S;
+    const int64_t br1 = (min(n, i0 + kSampleThreads) - 1) / S;
+    for (int k = threadIdx.x; k <= (int)(br1 - br0); k += kSampleThreads) {
+        const int r = r_begin + (int)((br0 + k) % R);
+        ray_direction(p, r < p.n_azi * p.n_ele ? jit.u[r / p.n_ele] : 0.0f, r, sdir[k]);
+    }
+    __syncthreads();
+    const int64_t i = i0 + threadIdx.x;
+    if (i >= n) return;
+    const int s = (int)(i % S);
+    const int64_t br = i / S;
+    const int rl = (int)(br % R);
+    const int b = (int)(br / R);
+    const float* dir = sdir[br - br0];
+    const float d = linspace_at(0.0f, 1.0f, S, s) * p.depth_scale + p.depth_offset;
+    if (b == 0 && s == 0) {
+        dirs[rl * 3 + 0] = dir[0];
+        dirs[rl * 3 + 1] = dir[1];
+        dirs[rl * 3 + 2] = dir[2];
+    }
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float world = rays_o[b * 3 + c] + dir[c] * d;
-            net_pts[i * 3 + c] = to_unit(world, p.lo, p.span);
-            net_view[i * 3 + c] = -dir[c];
-            net_tx[i * 3 + c] = to_unit(pos_tx[b * 3 + c], p.lo, p.span);
-            if (dir_tx) net_dir_tx[i * 3 + c] = dir_tx[b * 3 + c];
-        }
+    for (int c = 0; c < 3; ++c) {
+        const float world = rays_o[b * 3 + c] + dir[c] * d;
+        net_pts[i * 3 + c] = to_unit(world, p.lo, p.span);
+        net_view[i * 3 + c] = -dir[c];
+        net_tx[i * 3 + c] = to_unit(pos_tx[b * 3 + c], p.lo, p.span);
+        if (dir_tx) net_dir_tx[i * 3 + c] = dir_tx[b * 3 + c];
     }
 }
 
@@ -209,12 +218,23 @@ __global__ __launch_bounds__(256) void weights_fwd_kernel(
             dir[c] = dirs[r * 3 + c];
         }
         const int64_t base = ray * S;
-        for (int s = lane; s < S; s += 64) {
-            const float a = load_f(attn, base + s);
-            const float d = d_vals[s];
-            const float gap = (s + 1 < S) ? d_vals[s + 1] - d : 1e10f;
-            alpha[s] = 1.0f - expf(-a * gap);
-            delay[base + s] = source_delay(p, o, txn, dir, d);
+        // rounds of 8 coalesced attn loads per lane, all in flight before use
+        for (int s0 = 0; s0 < S; s0 += 8 * 64) {
+            float av[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) av[j] = load_f(attn, base + min(s0 + j * 64 + lane, S - 1));
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int s = s0 + j * 64 + lane;
+                if (s < S) {
+                    const float d = linspace_at(0.0f, 1.0f, S, s) * p.depth_scale + p.depth_offset;
+                    const float dn =
+                        linspace_at(0.0f, 1.0f, S, s + 1) * p.depth_scale + p.depth_offset;
+                    const float gap = (s + 1 < S) ? dn - d : 1e10f;
+                    alpha[s] = 1.0f - expf(-av[j] * gap);
+                    delay[base + s] = source_delay(p, o, txn, dir, d);
+                }
+            }
         }
     }
     __syncthreads();
@@ -412,7 +432,7 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
     const int f = fbase + (lane & 31);
     const int fm = (f < F) ? f : 0;
     const int half = lane >> 5;
-    for (int i = threadIdx.x; i < T; i += kDftThreads) tw[i] = twg[i];
+    stage_table<kDftThreads>(tw, twg, T);
 
     // this thread's staging rows
     const int col = threadIdx.x & 63, row0 = threadIdx.x >> 6;
@@ -551,8 +571,8 @@ __global__ __launch_bounds__(256) void irfft_kernel(int F, const float2* __restr
     float2* X = lds;       // [F]
     float2* tw = lds + F;  // [n]
     const int b = blockIdx.y;
-    for (int i = threadIdx.x; i < F; i += blockDim.x) X[i] = spec[(int64_t)b * F + i];
-    for (int i = threadIdx.x; i < n; i += blockDim.x) tw[i] = twg[i];
+    stage_table<256>(X, spec + (int64_t)b * F, F);
+    stage_table<256>(tw, twg, n);
     __syncthreads();
     const int tl = threadIdx.x & 31, slice = threadIdx.x >> 5;
     const int t = blockIdx.x * 32 + tl;
@@ -679,7 +699,8 @@ extern "C" int avr_sample_rays(const avr_render_params* p, int32_t B, const floa
     AziJitter jit;
     for (int i = 0; i < AVR_MAX_AZI; ++i) jit.u[i] = (i < p->n_azi) ? u_azi_host[i] : 0.0f;
     const int64_t n = (int64_t)B * n_rays(*p) * p->n_samples;
-    hipLaunchKernelGGL(sample_rays_kernel, dim3(pick_blocks(n, 256, 8192)), dim3(256), 0,
+    hipLaunchKernelGGL(sample_rays_kernel, dim3((unsigned)((n + kSampleThreads - 1) / kSampleThreads)),
+                       dim3(kSampleThreads), 0,
                        as_stream(stream), *p, (int)B, jit, (int)ray_begin, rays_o, pos_tx, dir_tx,
                        dirs, net_pts, net_view, net_tx, dir_tx ? net_dir_tx : nullptr);
     return check_launch("avr_sample_rays");
@@ -718,13 +739,13 @@ namespace {
 // "u4nt", "u8nt"); the default is the measured best.
 int reduce_variant() {
     const char* v = getenv("AVR_REDUCE_VARIANT");
-    if (!v) return 1;
+    if (!v) return 2;  // u4nt: best of the sweep in profiles/r01_tune_c2.jsonl
     const std::string s(v);
     if (s == "u4") return 0;
     if (s == "u8") return 1;
     if (s == "u4nt") return 2;
     if (s == "u8nt") return 3;
-    return 1;
+    return 2;
 }
 
 template <typename Tin, bool VECTOR, int C>
@@ -735,16 +756,16 @@ void launch_reduce_cpt(dim3 grid, hipStream_t st, const Tin* s, const float* w, 
             hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, false>), grid,
                                dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T, rps, total);
             break;
-        case 2:
-            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, true>), grid,
-                               dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T, rps, total);
-            break;
         case 3:
             hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, true>), grid,
                                dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T, rps, total);
             break;
-        default:
+        case 1:
             hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, false>), grid,
+                               dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T, rps, total);
+            break;
+        default:
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, true>), grid,
                                dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T, rps, total);
     }
 }
@@ -755,7 +776,10 @@ int launch_reduce(const avr_render_params* p, int B, const void* sig, const floa
     constexpr int VEC = VECTOR ? Vec16<Tin>::N : 1;
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
     const int rps = (R + n_split - 1) / n_split;
-    const int nchunks_max = (T + VEC - 1 + VEC - 1) / VEC;
+    // alignment phase of a (b,s) column is (s*T) mod VEC (S*T is a multiple of VEC)
+    int max_phase = 0;
+    for (int s = 0; s < S && s < VEC; ++s) max_phase = max(max_phase, (int)(((int64_t)s * T) % VEC));
+    const int nchunks_max = (T + max_phase + VEC - 1) / VEC;
     const int cpt = (nchunks_max + kReduceThreads - 1) / kReduceThreads;
     const int64_t total = (int64_t)B * R * S * T;
     const dim3 grid(n_split, S, B);

@@ -126,14 +126,15 @@ def _env_int(name):
 
 
 def pick_n_split(B, R, S):
-    """Ray splits for the reduction (a power of two <= 16): about 1024
-    workgroups of 256 threads, at most 2048 rays per split.
+    """Ray splits for the reduction (a power of two <= 16): about 512
+    workgroups of 256 threads (2 per CU; the sweep in
+    profiles/r01_tune_c2.jsonl), at most 2048 rays per split.
     AVR_NSPLIT overrides (tuning)."""
     forced = _env_int("AVR_NSPLIT")
     if forced:
         return forced
     n = 1
-    while n < 16 and (B * S * n < 1024 or math.ceil(R / n) > 2048) and math.ceil(R / (2 * n)) >= 8:
+    while n < 16 and (B * S * n < 512 or math.ceil(R / n) > 2048) and math.ceil(R / (2 * n)) >= 8:
         n *= 2
     if math.ceil(R / n) > 2048:
         raise ValueError(f"{R} rays need more than 16 splits of <= 2048")

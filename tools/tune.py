@@ -29,9 +29,9 @@ def main():
     ap.add_argument("--workload", default="c2_meshrir_1024x256x512")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--variants", default="u4,u8,u4nt,u8nt")
-    ap.add_argument("--nsplit", default="2,4,8,16")
-    ap.add_argument("--ksplit", default="0")
+    ap.add_argument("--variants", default="u4nt,u8nt")
+    ap.add_argument("--nsplit", default="1,2,4")
+    ap.add_argument("--ksplit", default="4,8,16")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     w = WORKLOADS[args.workload]
