@@ -167,26 +167,44 @@ __global__ __launch_bounds__(kSampleThreads) void sample_rays_kernel(
         ray_direction(p, r < p.n_azi * p.n_ele ? jit.u[r / p.n_ele] : 0.0f, r, sdir[k]);
     }
     __syncthreads();
+    // stage the block's 256 x 3 outputs per tensor in LDS, then write them
+    // as coalesced 4-byte rows (one 1 KiB wave store instead of 12-byte strides)
+    __shared__ float obuf[4][kSampleThreads * 3];
     const int64_t i = i0 + threadIdx.x;
-    if (i >= n) return;
-    const int s = (int)(i % S);
-    const int64_t br = i / S;
-    const int rl = (int)(br % R);
-    const int b = (int)(br / R);
-    const float* dir = sdir[br - br0];
-    const float d = linspace_at(0.0f, 1.0f, S, s) * p.depth_scale + p.depth_offset;
-    if (b == 0 && s == 0) {
-        dirs[rl * 3 + 0] = dir[0];
-        dirs[rl * 3 + 1] = dir[1];
-        dirs[rl * 3 + 2] = dir[2];
-    }
+    const bool live = i < n;
+    if (live) {
+        const int s = (int)(i % S);
+        const int64_t br = i / S;
+        const int rl = (int)(br % R);
+        const int b = (int)(br / R);
+        const float* dir = sdir[br - br0];
+        const float d = linspace_at(0.0f, 1.0f, S, s) * p.depth_scale + p.depth_offset;
+        if (b == 0 && s == 0) {
+            dirs[rl * 3 + 0] = dir[0];
+            dirs[rl * 3 + 1] = dir[1];
+            dirs[rl * 3 + 2] = dir[2];
+        }
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const float world = rays_o[b * 3 + c] + dir[c] * d;
-        net_pts[i * 3 + c] = to_unit(world, p.lo, p.span);
-        net_view[i * 3 + c] = -dir[c];
-        net_tx[i * 3 + c] = to_unit(pos_tx[b * 3 + c], p.lo, p.span);
-        if (dir_tx) net_dir_tx[i * 3 + c] = dir_tx[b * 3 + c];
+        for (int c = 0; c < 3; ++c) {
+            const float world = rays_o[b * 3 + c] + dir[c] * d;
+            obuf[0][threadIdx.x * 3 + c] = to_unit(world, p.lo, p.span);
+            obuf[1][threadIdx.x * 3 + c] = -dir[c];
+            obuf[2][threadIdx.x * 3 + c] = to_unit(pos_tx[b * 3 + c], p.lo, p.span);
+            obuf[3][threadIdx.x * 3 + c] = dir_tx ? dir_tx[b * 3 + c] : 0.0f;
+        }
+    }
+    __syncthreads();
+    const int64_t lim = (n - i0) * 3;  // valid floats in this block
+    float* outs[4] = {net_pts, net_view, net_tx, net_dir_tx};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (q == 3 && !dir_tx) break;
+        float* o = outs[q] + i0 * 3;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int e = threadIdx.x + k * kSampleThreads;
+            if (e < lim) o[e] = obuf[q][e];
+        }
     }
 }
 
@@ -238,26 +256,30 @@ __global__ __launch_bounds__(256) void weights_fwd_kernel(
         }
     }
     __syncthreads();
-    if (!active) return;
     const int64_t base = ray * S;
-    const int per = (S + 63) / 64;
-    const int s0 = min(S, lane * per), s1 = min(S, s0 + per);
-    float run = 1.0f;
-    for (int s = s0; s < s1; ++s) run = run * ((1.0f - alpha[s]) + 1e-6f);
-    // inclusive multiplicative scan over lanes, then shift to exclusive
-    float incl = run;
+    if (active) {
+        const int per = (S + 63) / 64;
+        const int s0 = min(S, lane * per), s1 = min(S, s0 + per);
+        float run = 1.0f;
+        for (int s = s0; s < s1; ++s) run = run * ((1.0f - alpha[s]) + 1e-6f);
+        // inclusive multiplicative scan over lanes, then shift to exclusive
+        float incl = run;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const float v = __shfl_up(incl, off, 64);
-        if (lane >= off) incl = incl * v;
+        for (int off = 1; off < 64; off <<= 1) {
+            const float v = __shfl_up(incl, off, 64);
+            if (lane >= off) incl = incl * v;
+        }
+        float trans = __shfl_up(incl, 1, 64);
+        if (lane == 0) trans = 1.0f;
+        for (int s = s0; s < s1; ++s) {
+            const float al = alpha[s];
+            alpha[s] = trans * al;  // w_s, written back in place
+            trans = trans * ((1.0f - al) + 1e-6f);
+        }
     }
-    float trans = __shfl_up(incl, 1, 64);
-    if (lane == 0) trans = 1.0f;
-    for (int s = s0; s < s1; ++s) {
-        const float al = alpha[s];
-        w_out[base + s] = trans * al;
-        trans = trans * ((1.0f - al) + 1e-6f);
-    }
+    __syncthreads();
+    if (active)
+        for (int s = lane; s < S; s += 64) w_out[base + s] = alpha[s];  // coalesced
 }
 
 // --------------------------------------------- the HBM stream: ray reduce
@@ -315,18 +337,26 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
     __syncthreads();
     // an empty split (nr <= 0) falls through both loops and writes zeros
     const int64_t row0 = (((int64_t)b * R + r0) * S + s) * (int64_t)T;
+    // A row starts `phase` elements past a 16-byte boundary; its first
+    // `head` elements are picked up by lane 0 with scalar loads and the rest
+    // is covered by aligned VEC-element chunks (the last may run past T).
     const int phase = (int)(row0 % VEC);
-    const int nchunks = (T + phase + VEC - 1) / VEC;
+    const int head = min((VEC - phase) % VEC, T);
+    const int nchunks = (T - head + VEC - 1) / VEC;
     const int64_t row_stride = (int64_t)S * T;
 
     float acc[CPT][VEC];
+    float acc_h[VEC];
     int t0[CPT];
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
-        t0[c] = (threadIdx.x + c * kReduceThreads) * VEC - phase;
+        t0[c] = head + (threadIdx.x + c * kReduceThreads) * VEC;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) acc[c][k] = 0.0f;
     }
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) acc_h[k] = 0.0f;
+    const bool head_lane = (threadIdx.x == 0) && head > 0;
 
     auto load_chunk = [&](int64_t rowbase, int c, float* x) {
         const int j = threadIdx.x + c * kReduceThreads;
@@ -351,13 +381,20 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
 #pragma unroll
         for (int k = 0; k < VEC; ++k) x[k] = (e0 + k < total) ? load_f(sig, e0 + k) : 0.0f;
     };
+    auto add_head = [&](int64_t row_start, float wr, int dr) {
+        if (head_lane) {
+#pragma unroll
+            for (int k = 0; k < VEC - 1; ++k)
+                if (k < head) acc_h[k] = fmaf(k >= dr ? wr : 0.0f, load_f(sig, row_start + k), acc_h[k]);
+        }
+    };
 
     int r = 0;
     for (; r + kUnroll <= nr; r += kUnroll) {
         float x[kUnroll][CPT][VEC];
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
-            const int64_t rowbase = row0 + (int64_t)(r + u) * row_stride - phase;
+            const int64_t rowbase = row0 + (int64_t)(r + u) * row_stride + head;
 #pragma unroll
             for (int c = 0; c < CPT; ++c) load_chunk(rowbase, c, x[u][c]);
         }
@@ -372,10 +409,11 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
                     const float wm = (t0[c] + k >= dr) ? wr : 0.0f;
                     acc[c][k] = fmaf(wm, x[u][c][k], acc[c][k]);
                 }
+            add_head(row0 + (int64_t)(r + u) * row_stride, wr, dr);
         }
     }
     for (; r < nr; ++r) {
-        const int64_t rowbase = row0 + (int64_t)r * row_stride - phase;
+        const int64_t rowbase = row0 + (int64_t)r * row_stride + head;
         const float wr = w_l[r];
         const int dr = d_l[r];
 #pragma unroll
@@ -388,6 +426,7 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
                 acc[c][k] = fmaf(wm, x[k], acc[c][k]);
             }
         }
+        add_head(row0 + (int64_t)r * row_stride, wr, dr);
     }
     float* out = part + (((int64_t)split * B + b) * S + s) * (int64_t)T;
 #pragma unroll
@@ -395,8 +434,13 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const int t = t0[c] + k;
-            if (t >= 0 && t < T) out[t] = acc[c][k];
+            if (t < T) out[t] = acc[c][k];
         }
+    if (head_lane) {
+#pragma unroll
+        for (int k = 0; k < VEC - 1; ++k)
+            if (k < head) out[k] = acc_h[k];
+    }
 }
 
 // ------------------------------- DFT + phase + sum over samples (MFMA f32)
@@ -417,7 +461,7 @@ constexpr int kKc = 64;  // t per LDS stage
 // are in flight while the MFMAs consume the current one.
 template <int NS>
 __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
-    const float* __restrict__ part, const float* __restrict__ pl,
+    avr_render_params pp, const float* __restrict__ part, const float* __restrict__ pl,
     const int32_t* __restrict__ shift, const float2* __restrict__ phase,
     const float2* __restrict__ twg, float2* __restrict__ spart, int B, int S, int T, int KS,
     int kchunk) {
@@ -432,9 +476,8 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
     const int f = fbase + (lane & 31);
     const int fm = (f < F) ? f : 0;
     const int half = lane >> 5;
-    stage_table<kDftThreads>(tw, twg, T);
-
-    // this thread's staging rows
+    // this thread's staging rows; shift[s] recomputed (renderer.py:79-80),
+    // identical to the table, so the path-loss gather is not a dependent load
     const int col = threadIdx.x & 63, row0 = threadIdx.x >> 6;
     int sh[8];
     bool srow[8];
@@ -442,8 +485,10 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
     for (int i = 0; i < 8; ++i) {
         const int s = stile * 32 + row0 + 4 * i;
         srow[i] = s < S;
-        sh[i] = shift[min(s, S - 1)];
+        const float d = linspace_at(0.0f, 1.0f, S, min(s, S - 1)) * pp.depth_scale + pp.depth_offset;
+        sh[i] = (int)rintf((pp.fs * d) / pp.speed);
     }
+    (void)shift;
     const int64_t slab = (int64_t)B * S * T;
     // rows beyond S are clamped to row S-1 (masked by srow)
     const int s_first = min(stile * 32 + row0, S - 1);
@@ -482,6 +527,7 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
         }
     };
     if (k0 < k1) stage(k0, cur);
+    stage_table<kDftThreads>(tw, twg, T);  // its loads overlap the first tile's
     for (int kc = k0; kc < k1; kc += kKc) {
         __syncthreads();
 #pragma unroll
@@ -520,34 +566,35 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
     }
 }
 
-// out[b,f] = sum_p spart[b,p,f]: 4 partial-groups x 64 bins per block,
-// coalesced loads, fixed-order LDS combine (deterministic).
+// out[b,f] = sum_p spart[b,p,f]: 16 partial-groups x 16 bins per block; each
+// thread's loads of a round (4 partials) are issued together, then the 16
+// groups are combined in LDS in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void spectrum_finalize_kernel(int B, int P, int F,
                                                                 const float2* __restrict__ spart,
                                                                 float2* __restrict__ out) {
-    __shared__ float2 red[4][64];
+    __shared__ float2 red[16][17];
     const int b = blockIdx.y;
-    const int g = threadIdx.x >> 6, j = threadIdx.x & 63;
-    const int f = blockIdx.x * 64 + j;
+    const int g = threadIdx.x >> 4, j = threadIdx.x & 15;
+    const int f = blockIdx.x * 16 + j;
     const int fc = min(f, F - 1);
     const float2* src = spart + (int64_t)b * P * F + fc;
-    float2 a0 = make_float2(0.f, 0.f), a1 = a0;
-    int q = g;
-    for (; q + 4 < P; q += 8) {
-        const float2 v0 = src[(int64_t)q * F];
-        const float2 v1 = src[(int64_t)(q + 4) * F];
-        a0.x += v0.x; a0.y += v0.y;
-        a1.x += v1.x; a1.y += v1.y;
+    float ax = 0.f, ay = 0.f;
+    for (int q0 = 0; q0 < P; q0 += 64) {
+        float2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = src[(int64_t)min(q0 + g + 16 * u, P - 1) * F];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (q0 + g + 16 * u < P) {
+                ax += v[u].x;
+                ay += v[u].y;
+            }
     }
-    if (q < P) {
-        const float2 v0 = src[(int64_t)q * F];
-        a0.x += v0.x; a0.y += v0.y;
-    }
-    red[g][j] = make_float2(a0.x + a1.x, a0.y + a1.y);
+    red[g][j] = make_float2(ax, ay);
     __syncthreads();
     if (g == 0 && f < F) {
         float2 r = red[0][j];
-        for (int k = 1; k < 4; ++k) {
+        for (int k = 1; k < 16; ++k) {
             r.x += red[k][j].x;
             r.y += red[k][j].y;
         }
@@ -776,10 +823,8 @@ int launch_reduce(const avr_render_params* p, int B, const void* sig, const floa
     constexpr int VEC = VECTOR ? Vec16<Tin>::N : 1;
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
     const int rps = (R + n_split - 1) / n_split;
-    // alignment phase of a (b,s) column is (s*T) mod VEC (S*T is a multiple of VEC)
-    int max_phase = 0;
-    for (int s = 0; s < S && s < VEC; ++s) max_phase = max(max_phase, (int)(((int64_t)s * T) % VEC));
-    const int nchunks_max = (T + max_phase + VEC - 1) / VEC;
+    // aligned chunks per row (the unaligned head goes to lane 0)
+    const int nchunks_max = (T + VEC - 1) / VEC;
     const int cpt = (nchunks_max + kReduceThreads - 1) / kReduceThreads;
     const int64_t total = (int64_t)B * R * S * T;
     const dim3 grid(n_split, S, B);
@@ -837,7 +882,7 @@ extern "C" int avr_dft_phase_fwd(const avr_render_params* p, int32_t B, const fl
         if (lds > 65536)
             (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)lds);
-        hipLaunchKernelGGL(kern, grid, dim3(kDftThreads), lds, as_stream(stream), part, pl_table,
+        hipLaunchKernelGGL(kern, grid, dim3(kDftThreads), lds, as_stream(stream), *p, part, pl_table,
                            shift, reinterpret_cast<const float2*>(phase),
                            reinterpret_cast<const float2*>(twiddle),
                            reinterpret_cast<float2*>(spart), (int)B, S, T, (int)k_split, kchunk);
@@ -856,7 +901,7 @@ extern "C" int avr_dft_phase_fwd(const avr_render_params* p, int32_t B, const fl
 extern "C" int avr_spectrum_finalize(int32_t B, int32_t P, int32_t F, const float* spart,
                                      float* out, void* stream) {
     AVR_REQUIRE(B >= 1 && P >= 1 && F >= 1 && spart && out, "avr_spectrum_finalize: bad args");
-    hipLaunchKernelGGL(spectrum_finalize_kernel, dim3((unsigned)((F + 63) / 64), B), dim3(256), 0,
+    hipLaunchKernelGGL(spectrum_finalize_kernel, dim3((unsigned)((F + 15) / 16), B), dim3(256), 0,
                        as_stream(stream), (int)B, (int)P, (int)F,
                        reinterpret_cast<const float2*>(spart), reinterpret_cast<float2*>(out));
     return check_launch("avr_spectrum_finalize");
