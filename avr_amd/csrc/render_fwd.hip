@@ -337,26 +337,18 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
     __syncthreads();
     // an empty split (nr <= 0) falls through both loops and writes zeros
     const int64_t row0 = (((int64_t)b * R + r0) * S + s) * (int64_t)T;
-    // A row starts `phase` elements past a 16-byte boundary; its first
-    // `head` elements are picked up by lane 0 with scalar loads and the rest
-    // is covered by aligned VEC-element chunks (the last may run past T).
     const int phase = (int)(row0 % VEC);
-    const int head = min((VEC - phase) % VEC, T);
-    const int nchunks = (T - head + VEC - 1) / VEC;
+    const int nchunks = (T + phase + VEC - 1) / VEC;
     const int64_t row_stride = (int64_t)S * T;
 
     float acc[CPT][VEC];
-    float acc_h[VEC];
     int t0[CPT];
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
-        t0[c] = head + (threadIdx.x + c * kReduceThreads) * VEC;
+        t0[c] = (threadIdx.x + c * kReduceThreads) * VEC - phase;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) acc[c][k] = 0.0f;
     }
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) acc_h[k] = 0.0f;
-    const bool head_lane = (threadIdx.x == 0) && head > 0;
 
     auto load_chunk = [&](int64_t rowbase, int c, float* x) {
         const int j = threadIdx.x + c * kReduceThreads;
@@ -381,20 +373,13 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
 #pragma unroll
         for (int k = 0; k < VEC; ++k) x[k] = (e0 + k < total) ? load_f(sig, e0 + k) : 0.0f;
     };
-    auto add_head = [&](int64_t row_start, float wr, int dr) {
-        if (head_lane) {
-#pragma unroll
-            for (int k = 0; k < VEC - 1; ++k)
-                if (k < head) acc_h[k] = fmaf(k >= dr ? wr : 0.0f, load_f(sig, row_start + k), acc_h[k]);
-        }
-    };
 
     int r = 0;
     for (; r + kUnroll <= nr; r += kUnroll) {
         float x[kUnroll][CPT][VEC];
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
-            const int64_t rowbase = row0 + (int64_t)(r + u) * row_stride + head;
+            const int64_t rowbase = row0 + (int64_t)(r + u) * row_stride - phase;
 #pragma unroll
             for (int c = 0; c < CPT; ++c) load_chunk(rowbase, c, x[u][c]);
         }
@@ -409,11 +394,10 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
                     const float wm = (t0[c] + k >= dr) ? wr : 0.0f;
                     acc[c][k] = fmaf(wm, x[u][c][k], acc[c][k]);
                 }
-            add_head(row0 + (int64_t)(r + u) * row_stride, wr, dr);
         }
     }
     for (; r < nr; ++r) {
-        const int64_t rowbase = row0 + (int64_t)r * row_stride + head;
+        const int64_t rowbase = row0 + (int64_t)r * row_stride - phase;
         const float wr = w_l[r];
         const int dr = d_l[r];
 #pragma unroll
@@ -426,7 +410,6 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
                 acc[c][k] = fmaf(wm, x[k], acc[c][k]);
             }
         }
-        add_head(row0 + (int64_t)r * row_stride, wr, dr);
     }
     float* out = part + (((int64_t)split * B + b) * S + s) * (int64_t)T;
 #pragma unroll
@@ -434,13 +417,8 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const int t = t0[c] + k;
-            if (t < T) out[t] = acc[c][k];
+            if (t >= 0 && t < T) out[t] = acc[c][k];
         }
-    if (head_lane) {
-#pragma unroll
-        for (int k = 0; k < VEC - 1; ++k)
-            if (k < head) out[k] = acc_h[k];
-    }
 }
 
 // ------------------------------- DFT + phase + sum over samples (MFMA f32)
@@ -504,36 +482,40 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
         acc_im[i] = 0.0f;
     }
     const int inc = (int)((2LL * fm) % T);
-    float cur[8];
-    auto stage = [&](int kc, float* v) {
-        // per-row clamp: the shared rowbase0 + 4i*T may exceed the last row for ragged S
-        const int t = kc + col;
-        const int tc = min(t, T - 1);
-        float acc[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
+    // raw loads of one tile (NS partial slabs + path loss), kept in registers
+    // until the tile is committed to LDS, so the next tile's loads stay in
+    // flight under the current tile's MFMAs
+    float raw[NS][8], g[8];
+    auto issue = [&](int kc) {
+        const int tc = min(kc + col, T - 1);
 #pragma unroll
         for (int k = 0; k < NS; ++k)
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int64_t ro = min(rowbase0 + (int64_t)(4 * i) * T, max_row_off);
-                acc[i] += part[k * slab + ro + tc];
+                raw[k][i] = part[k * slab + ro + tc];
             }
 #pragma unroll
+        for (int i = 0; i < 8; ++i) g[i] = pl[sh[i] + tc];
+    };
+    auto commit = [&](int kc) {
+        const int t = kc + col;
+#pragma unroll
         for (int i = 0; i < 8; ++i) {
+            float sum = raw[0][i];
+#pragma unroll
+            for (int k = 1; k < NS; ++k) sum += raw[k][i];
             const bool ok = srow[i] && t < k1 && t < T - 1 - sh[i];
-            const float g = pl[sh[i] + tc];
-            v[i] = ok ? acc[i] * g : 0.0f;
+            As[row0 + 4 * i][col] = ok ? sum * g[i] : 0.0f;
         }
     };
-    if (k0 < k1) stage(k0, cur);
+    if (k0 < k1) issue(k0);
     stage_table<kDftThreads>(tw, twg, T);  // its loads overlap the first tile's
     for (int kc = k0; kc < k1; kc += kKc) {
         __syncthreads();
-#pragma unroll
-        for (int i = 0; i < 8; ++i) As[row0 + 4 * i][col] = cur[i];
+        commit(kc);
         __syncthreads();
-        if (kc + kKc < k1) stage(kc + kKc, cur);  // next tile's loads fly under the MFMAs
+        if (kc + kKc < k1) issue(kc + kKc);  // next tile's loads fly under the MFMAs
         int idx = (int)(((int64_t)(kc + half) * fm) % T);
 #pragma unroll 8
         for (int kk = 0; kk < kKc; kk += 2) {
@@ -545,17 +527,25 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
             if (idx >= T) idx -= T;
         }
     }
-    // epilogue: rows (reg&3) + 8*(reg>>2) + 4*half, column lane&31
+    // epilogue: rows (reg&3) + 8*(reg>>2) + 4*half, column lane&31; the 16
+    // phase loads are issued together (clamped, masked after)
     float re = 0.0f, im = 0.0f;
-    if (f < F) {
+    {
+        float2 ph[16];
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int s = stile * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * half;
+            ph[reg] = phase[(int64_t)min(s, S - 1) * F + fm];
+        }
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) asm volatile("" ::"v"(ph[reg].x), "v"(ph[reg].y));
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
             const int s = stile * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * half;
             if (s < S) {
-                const float2 ph = phase[(int64_t)s * F + f];
                 const float zr = acc_re[reg], zi = acc_im[reg];
-                re += zr * ph.x - zi * ph.y;
-                im += zr * ph.y + zi * ph.x;
+                re += zr * ph[reg].x - zi * ph[reg].y;
+                im += zr * ph[reg].y + zi * ph[reg].x;
             }
         }
     }
@@ -823,8 +813,11 @@ int launch_reduce(const avr_render_params* p, int B, const void* sig, const floa
     constexpr int VEC = VECTOR ? Vec16<Tin>::N : 1;
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
     const int rps = (R + n_split - 1) / n_split;
-    // aligned chunks per row (the unaligned head goes to lane 0)
-    const int nchunks_max = (T + VEC - 1) / VEC;
+    // a (b,s) column's rows start (s*T) mod VEC elements past a 16-byte
+    // boundary (S*T is a multiple of VEC): chunks per row = (T + phase)/VEC
+    int max_phase = 0;
+    for (int s = 0; s < S && s < VEC; ++s) max_phase = max(max_phase, (int)(((int64_t)s * T) % VEC));
+    const int nchunks_max = (T + max_phase + VEC - 1) / VEC;
     const int cpt = (nchunks_max + kReduceThreads - 1) / kReduceThreads;
     const int64_t total = (int64_t)B * R * S * T;
     const dim3 grid(n_split, S, B);

@@ -23,7 +23,7 @@ for s in "$@"; do
     bench) step bench 600 python bench.py ;;
     benchq) step bench_q 300 python bench.py --no-cpu-baseline --steps 100 ;;
     tune) step tune 600 python tools/tune.py ;;
-    tune5) step tune5 600 python tools/tune.py --workload c5_simu_4096x512x2048 --rounds 3 --steps 5 --nsplit 2,4 ;;
+    tune5) step tune5 600 python tools/tune.py --workload c5_simu_4096x512x2048 --rounds 3 --steps 5 --nsplit 2,4,8 --ksplit 8 --variants u4nt,u8nt,u4 ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 50 --warmup 5 ;;
   esac
 done
