@@ -22,8 +22,10 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchq) step bench_q 300 python bench.py --no-cpu-baseline --steps 100 ;;
+    streams) step bench_s1 200 python bench.py --no-cpu-baseline --steps 200 --streams 1 && step bench_s2 200 python bench.py --no-cpu-baseline --steps 200 --streams 2 && step bench_s3 200 python bench.py --no-cpu-baseline --steps 200 --streams 3 ;;
     tune) step tune 600 python tools/tune.py ;;
     tune5) step tune5 600 python tools/tune.py --workload c5_simu_4096x512x2048 --rounds 3 --steps 5 --nsplit 2,4,8 --ksplit 8 --variants u4nt,u8nt,u4 ;;
-    prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 50 --warmup 5 ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 50 --warmup 5 --streams 1 ;;
+    pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 3 --streams 1 && step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 3 --streams 1 ;;
   esac
 done
