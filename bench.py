@@ -69,6 +69,26 @@ class KernelTimer:
         return sum(ts) / len(ts) if ts else float("nan")
 
 
+def pmc_traffic(workload, dtype_name):
+    """HBM bytes per launch of the reduction kernel from the newest committed
+    rocprofv3 --pmc summary for this workload (tools/pmc_summary.py; the
+    gfx950 FETCH_SIZE x2 correction applied there), or None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_*.json")))
+    for path in reversed(files):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") != workload:
+            continue
+        for k, v in d["kernels"].items():
+            if k.startswith("void ray_reduce_fwd_kernel<" + dtype_name):
+                return v["hbm_bytes"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(w, budget_s=15.0):
     """Time the CPU oracle (op-for-op torch-CPU restatement of renderer_cpu.py)
     on this host's cores for a bounded sample of the same workload."""
@@ -110,7 +130,7 @@ def cpu_baseline(w, budget_s=15.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c2_meshrir_1024x256x512")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -209,6 +229,7 @@ def main():
     n_split = timer.n_split or 1
     alg_bytes = w.ray_samples * (T * es + 8) + n_split * B * S * T * 4
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(w.name, "__half" if dt == torch.float16 else "float")
 
     result = {
         "metric": "ray-samples/sec/GPU (1024 rays×256 samp×512 freq) + IR render ms/pose",
@@ -237,7 +258,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "alg_bytes_per_launch": alg_bytes,
             "avg_launch_ms": k_ms,
         },
