@@ -317,41 +317,65 @@ struct Vec16<__half> {
     }
 };
 
-constexpr int kReduceThreads = 256;
-constexpr int kMaxRaysPerSplit = 2048;
-template <typename Tin, bool VECTOR, int CPT, int kUnroll, bool NT>
-__global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
+constexpr int kMaxReduceThreads = 1024;
+constexpr int kMaxGroupRays = 4096;  // G * rays_per_split (LDS: 32 KiB of w/delay)
+
+// One workgroup per (ray split, column group, b).  A column group is G
+// consecutive samples s0..s0+G-1 whose rows are contiguous in memory for
+// every ray (the sample index is the second-fastest), so the workgroup
+// streams one "super-row" of G*T elements per ray with 16-byte loads.  G is
+// chosen so a super-row is ~256*VEC elements (short rows: fp16 or small T);
+// the block size is chosen so every lane owns CPT chunks of it.  Lane slots
+// have fixed (g, t) coordinates, so the accumulators need no shuffling.
+template <typename Tin, bool VECTOR, int CPT, int kUnroll, bool NT, int G>
+__global__ __launch_bounds__(kMaxReduceThreads) void ray_reduce_fwd_kernel(
     const Tin* __restrict__ sig, const float* __restrict__ w, const int32_t* __restrict__ delay,
     float* __restrict__ part, int B, int R, int S, int T, int rays_per_split, int64_t total) {
     constexpr int VEC = VECTOR ? Vec16<Tin>::N : 1;
-    __shared__ float w_l[kMaxRaysPerSplit];
-    __shared__ int d_l[kMaxRaysPerSplit];
-    const int split = blockIdx.x, s = blockIdx.y, b = blockIdx.z;
+    extern __shared__ float lds_wd[];  // w_l[G][nr], then d_l[G][nr]
+    const int nthreads = blockDim.x;
+    const int split = blockIdx.x, s0 = blockIdx.y * G, b = blockIdx.z;
+    const int gcount = min(G, S - s0);
     const int r0 = split * rays_per_split;
-    const int nr = min(R, r0 + rays_per_split) - r0;
-    for (int i = threadIdx.x; i < nr; i += kReduceThreads) {
-        const int64_t idx = ((int64_t)b * R + r0 + i) * S + s;
-        w_l[i] = w[idx];
-        d_l[i] = delay[idx];
+    const int nr = max(0, min(R, r0 + rays_per_split) - r0);
+    float* w_l = lds_wd;
+    int* d_l = reinterpret_cast<int*>(lds_wd + G * max(nr, 1));
+    for (int i = threadIdx.x; i < G * nr; i += nthreads) {
+        const int g = i / nr, rr = i - g * nr;
+        if (g < gcount) {
+            const int64_t idx = ((int64_t)b * R + r0 + rr) * S + s0 + g;
+            w_l[i] = w[idx];
+            d_l[i] = delay[idx];
+        } else {
+            w_l[i] = 0.0f;
+            d_l[i] = 0x7fffffff;
+        }
     }
     __syncthreads();
-    // an empty split (nr <= 0) falls through both loops and writes zeros
-    const int64_t row0 = (((int64_t)b * R + r0) * S + s) * (int64_t)T;
+    // an empty split (nr == 0) falls through both loops and writes zeros
+    const int64_t row0 = (((int64_t)b * R + r0) * S + s0) * (int64_t)T;
+    const int L = gcount * T;  // super-row length
     const int phase = (int)(row0 % VEC);
-    const int nchunks = (T + phase + VEC - 1) / VEC;
+    const int nchunks = (L + phase + VEC - 1) / VEC;
     const int64_t row_stride = (int64_t)S * T;
 
     float acc[CPT][VEC];
-    int t0[CPT];
+    int tk[CPT][VEC];  // t of each slot (-1: outside the super-row)
+    int gk[CPT][VEC];  // column of each slot within the group
 #pragma unroll
-    for (int c = 0; c < CPT; ++c) {
-        t0[c] = (threadIdx.x + c * kReduceThreads) * VEC - phase;
+    for (int c = 0; c < CPT; ++c)
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) acc[c][k] = 0.0f;
-    }
+        for (int k = 0; k < VEC; ++k) {
+            acc[c][k] = 0.0f;
+            const int e = (threadIdx.x + c * nthreads) * VEC + k - phase;
+            const bool ok = e >= 0 && e < L;
+            const int g = (G == 1) ? 0 : (ok ? e / T : 0);
+            gk[c][k] = g;
+            tk[c][k] = ok ? e - g * T : -1;
+        }
 
     auto load_chunk = [&](int64_t rowbase, int c, float* x) {
-        const int j = threadIdx.x + c * kReduceThreads;
+        const int j = threadIdx.x + c * nthreads;
         if (j >= nchunks) {
 #pragma unroll
             for (int k = 0; k < VEC; ++k) x[k] = 0.0f;
@@ -373,6 +397,30 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
 #pragma unroll
         for (int k = 0; k < VEC; ++k) x[k] = (e0 + k < total) ? load_f(sig, e0 + k) : 0.0f;
     };
+    auto accumulate = [&](int r, float (*x)[VEC]) {
+        float wg[G];
+        int dg[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            wg[g] = w_l[g * nr + r];
+            dg[g] = d_l[g * nr + r];
+        }
+#pragma unroll
+        for (int c = 0; c < CPT; ++c)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                float ws = wg[0];
+                int ds = dg[0];
+#pragma unroll
+                for (int g = 1; g < G; ++g)
+                    if (gk[c][k] == g) {
+                        ws = wg[g];
+                        ds = dg[g];
+                    }
+                const float wm = (tk[c][k] >= ds) ? ws : 0.0f;
+                acc[c][k] = fmaf(wm, x[c][k], acc[c][k]);
+            }
+    };
 
     int r = 0;
     for (; r + kUnroll <= nr; r += kUnroll) {
@@ -384,40 +432,21 @@ __global__ __launch_bounds__(kReduceThreads) void ray_reduce_fwd_kernel(
             for (int c = 0; c < CPT; ++c) load_chunk(rowbase, c, x[u][c]);
         }
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const float wr = w_l[r + u];
-            const int dr = d_l[r + u];
-#pragma unroll
-            for (int c = 0; c < CPT; ++c)
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) {
-                    const float wm = (t0[c] + k >= dr) ? wr : 0.0f;
-                    acc[c][k] = fmaf(wm, x[u][c][k], acc[c][k]);
-                }
-        }
+        for (int u = 0; u < kUnroll; ++u) accumulate(r + u, x[u]);
     }
     for (; r < nr; ++r) {
         const int64_t rowbase = row0 + (int64_t)r * row_stride - phase;
-        const float wr = w_l[r];
-        const int dr = d_l[r];
+        float x[CPT][VEC];
 #pragma unroll
-        for (int c = 0; c < CPT; ++c) {
-            float x[VEC];
-            load_chunk(rowbase, c, x);
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                const float wm = (t0[c] + k >= dr) ? wr : 0.0f;
-                acc[c][k] = fmaf(wm, x[k], acc[c][k]);
-            }
-        }
+        for (int c = 0; c < CPT; ++c) load_chunk(rowbase, c, x[c]);
+        accumulate(r, x);
     }
-    float* out = part + (((int64_t)split * B + b) * S + s) * (int64_t)T;
 #pragma unroll
     for (int c = 0; c < CPT; ++c)
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
-            const int t = t0[c] + k;
-            if (t >= 0 && t < T) out[t] = acc[c][k];
+            const int t = tk[c][k];
+            if (t >= 0) part[(((int64_t)split * B + b) * S + s0 + gk[c][k]) * T + t] = acc[c][k];
         }
 }
 
@@ -771,12 +800,12 @@ extern "C" int avr_weights_fwd(const avr_render_params* p, int32_t B, const void
 }
 
 namespace {
-// Streaming variant of the reduction (rows in flight per thread, non-temporal
+// Streaming variant of the reduction (rows in flight per lane, non-temporal
 // loads).  AVR_REDUCE_VARIANT selects one for tuning runs ("u4", "u8",
 // "u4nt", "u8nt"); the default is the measured best.
 int reduce_variant() {
     const char* v = getenv("AVR_REDUCE_VARIANT");
-    if (!v) return 2;  // u4nt: best of the sweep in profiles/r01_tune_c2.jsonl
+    if (!v) return 2;  // u4nt: best of the sweeps in profiles/r01_tune*_c2.jsonl
     const std::string s(v);
     if (s == "u4") return 0;
     if (s == "u8") return 1;
@@ -785,25 +814,47 @@ int reduce_variant() {
     return 2;
 }
 
-template <typename Tin, bool VECTOR, int C>
-void launch_reduce_cpt(dim3 grid, hipStream_t st, const Tin* s, const float* w, const int32_t* delay,
-                       float* part, int B, int R, int S, int T, int rps, int64_t total) {
+struct ReduceShape {
+    int G, cpt, threads;
+};
+
+// Column group, chunks per lane and block size for one (T, VEC, S).
+template <int VEC>
+ReduceShape reduce_shape(int S, int T) {
+    ReduceShape sh;
+    sh.G = 1;
+    while (sh.G < 4 && 2 * sh.G * T <= 256 * VEC && 2 * sh.G <= S) sh.G *= 2;
+    int max_phase = 0;  // group starts are s0 = multiples of G; S*T % VEC == 0
+    for (int s0 = 0; s0 < S && s0 < VEC * sh.G; s0 += sh.G)
+        max_phase = max(max_phase, (int)(((int64_t)s0 * T) % VEC));
+    const int nch = (sh.G * T + max_phase + VEC - 1) / VEC;
+    sh.cpt = 1;
+    while ((nch + sh.cpt - 1) / sh.cpt > kMaxReduceThreads) ++sh.cpt;
+    const int need = (nch + sh.cpt - 1) / sh.cpt;
+    sh.threads = max(64, (need + 63) / 64 * 64);
+    return sh;
+}
+
+template <typename Tin, bool VECTOR, int C, int G>
+void launch_reduce_v(dim3 grid, dim3 block, size_t lds, hipStream_t st, const Tin* s, const float* w,
+                     const int32_t* delay, float* part, int B, int R, int S, int T, int rps,
+                     int64_t total) {
     switch (reduce_variant()) {
         case 0:
-            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, false>), grid,
-                               dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T, rps, total);
-            break;
-        case 3:
-            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, true>), grid,
-                               dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T, rps, total);
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, false, G>), grid, block, lds,
+                               st, s, w, delay, part, B, R, S, T, rps, total);
             break;
         case 1:
-            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, false>), grid,
-                               dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T, rps, total);
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, false, G>), grid, block, lds,
+                               st, s, w, delay, part, B, R, S, T, rps, total);
+            break;
+        case 3:
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, true, G>), grid, block, lds,
+                               st, s, w, delay, part, B, R, S, T, rps, total);
             break;
         default:
-            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, true>), grid,
-                               dim3(kReduceThreads), 0, st, s, w, delay, part, B, R, S, T, rps, total);
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, true, G>), grid, block, lds,
+                               st, s, w, delay, part, B, R, S, T, rps, total);
     }
 }
 
@@ -813,27 +864,48 @@ int launch_reduce(const avr_render_params* p, int B, const void* sig, const floa
     constexpr int VEC = VECTOR ? Vec16<Tin>::N : 1;
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
     const int rps = (R + n_split - 1) / n_split;
-    // a (b,s) column's rows start (s*T) mod VEC elements past a 16-byte
-    // boundary (S*T is a multiple of VEC): chunks per row = (T + phase)/VEC
-    int max_phase = 0;
-    for (int s = 0; s < S && s < VEC; ++s) max_phase = max(max_phase, (int)(((int64_t)s * T) % VEC));
-    const int nchunks_max = (T + max_phase + VEC - 1) / VEC;
-    const int cpt = (nchunks_max + kReduceThreads - 1) / kReduceThreads;
+    const ReduceShape sh = reduce_shape<VEC>(S, T);
+    if (sh.G * rps > kMaxGroupRays)
+        return fail(AVR_E_ARG, "avr_ray_reduce_fwd: too many rays per split (raise n_split)");
     const int64_t total = (int64_t)B * R * S * T;
-    const dim3 grid(n_split, S, B);
+    const dim3 grid(n_split, (S + sh.G - 1) / sh.G, B);
+    const dim3 block(sh.threads);
+    const size_t lds = (size_t)sh.G * max(rps, 1) * 8;
     const Tin* s = (const Tin*)sig;
-    if (cpt <= 1) launch_reduce_cpt<Tin, VECTOR, 1>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
-    else if (cpt <= 2) launch_reduce_cpt<Tin, VECTOR, 2>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
-    else if (cpt <= 3) launch_reduce_cpt<Tin, VECTOR, 3>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
-    else if (cpt <= 4) launch_reduce_cpt<Tin, VECTOR, 4>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
-    else if (cpt <= 6) launch_reduce_cpt<Tin, VECTOR, 6>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
-    else if (cpt <= 8) launch_reduce_cpt<Tin, VECTOR, 8>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
-    else if (cpt <= 12) launch_reduce_cpt<Tin, VECTOR, 12>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
-    else if (cpt <= 16) launch_reduce_cpt<Tin, VECTOR, 16>(grid, st, s, w, delay, part, B, R, S, T, rps, total);
-    else return fail(AVR_E_CONFIG, "ray_reduce: T too long for this build");
-    return check_launch("avr_ray_reduce_fwd");
+#define AVR_RR(C, GG)                                                                              \
+    if (sh.cpt == C && sh.G == GG)                                                                 \
+        return launch_reduce_v<Tin, VECTOR, C, GG>(grid, block, lds, st, s, w, delay, part, B, R, S, \
+                                                   T, rps, total),                                 \
+               check_launch("avr_ray_reduce_fwd");
+    AVR_RR(1, 1) AVR_RR(1, 2) AVR_RR(1, 4) AVR_RR(2, 1) AVR_RR(3, 1) AVR_RR(4, 1)
+#undef AVR_RR
+    return fail(AVR_E_CONFIG, "ray_reduce: T too long for this build");
 }
 }  // namespace
+
+extern "C" int avr_reduce_splits(const avr_render_params* p, int32_t B, int32_t sig_dtype,
+                                 int32_t* n_split) {
+    if (int e = validate(p)) return e;
+    AVR_REQUIRE(B >= 1 && n_split, "avr_reduce_splits: bad args");
+    const int R = n_rays(*p), S = p->n_samples, T = p->T;
+    const int vec = (sig_dtype == AVR_DTYPE_F16) ? 8 : 4;
+    const ReduceShape sh = vec == 8 ? reduce_shape<8>(S, T) : reduce_shape<4>(S, T);
+    const int groups = (S + sh.G - 1) / sh.G;
+    if (const char* f = getenv("AVR_NSPLIT")) {  // tuning override
+        *n_split = atoi(f);
+        return 0;
+    }
+    // power of two <= 16 (the DFT staging is templated on it): at least ~2
+    // workgroups per CU, and a split's w/delay fits the 32 KiB LDS slab
+    int n = 1;
+    auto rps = [&](int k) { return (R + k - 1) / k; };
+    while (n < 16 && ((int64_t)n * groups * B < 512 || rps(n) * sh.G > kMaxGroupRays) &&
+           rps(2 * n) >= 8)
+        n *= 2;
+    if (rps(n) * sh.G > kMaxGroupRays) return fail(AVR_E_CONFIG, "avr_reduce_splits: too many rays");
+    *n_split = n;
+    return 0;
+}
 
 extern "C" int avr_ray_reduce_fwd(const avr_render_params* p, int32_t B, const void* signal,
                                   int32_t sig_dtype, const float* w, const int32_t* delay,
@@ -842,7 +914,7 @@ extern "C" int avr_ray_reduce_fwd(const avr_render_params* p, int32_t B, const v
     AVR_REQUIRE(B >= 1 && signal && w && delay && part, "avr_ray_reduce_fwd: null pointer");
     const int R = n_rays(*p);
     AVR_REQUIRE(n_split >= 1 && n_split <= R, "avr_ray_reduce_fwd: n_split out of range");
-    AVR_REQUIRE((R + n_split - 1) / n_split <= kMaxRaysPerSplit,
+    AVR_REQUIRE((R + n_split - 1) / n_split <= kMaxGroupRays,
                 "avr_ray_reduce_fwd: too many rays per split (raise n_split)");
     const int64_t st = (int64_t)p->n_samples * p->T;
     const bool aligned = (reinterpret_cast<uintptr_t>(signal) % 16) == 0;

@@ -125,20 +125,13 @@ def _env_int(name):
     return int(v) if v else None
 
 
-def pick_n_split(B, R, S):
-    """Ray splits for the reduction (a power of two <= 16): about 512
-    workgroups of 256 threads (2 per CU; the sweep in
-    profiles/r01_tune_c2.jsonl), at most 2048 rays per split.
-    AVR_NSPLIT overrides (tuning)."""
-    forced = _env_int("AVR_NSPLIT")
-    if forced:
-        return forced
-    n = 1
-    while n < 16 and (B * S * n < 512 or math.ceil(R / n) > 2048) and math.ceil(R / (2 * n)) >= 8:
-        n *= 2
-    if math.ceil(R / n) > 2048:
-        raise ValueError(f"{R} rays need more than 16 splits of <= 2048")
-    return n
+def reduce_splits(p, B, sig_code):
+    """Ray splits of the reduction, decided by the library for this shape."""
+    import ctypes
+
+    n = ctypes.c_int32(0)
+    _lib.call("avr_reduce_splits", ctypes_ref(p), B, sig_code, ctypes.byref(n))
+    return int(n.value)
 
 
 def pick_k_split(B, S, T):
@@ -175,7 +168,7 @@ class RenderCore(torch.autograd.Function):
         delay = torch.empty(B, R, S, dtype=torch.int32, device=dev)
         _lib.call("avr_weights_fwd", pref, B, _ptr(attn), _dtype_code(attn), _ptr(rays_o),
                   _ptr(position_tx), _ptr(dirs), _ptr(tables.d_vals), _ptr(w), _ptr(delay), st)
-        n_split = pick_n_split(B, R, S)
+        n_split = reduce_splits(p, B, _dtype_code(signal))
         part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
         timer = KERNEL_TIMER
         if timer is not None:

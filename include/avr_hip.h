@@ -128,6 +128,10 @@ int avr_ray_reduce_fwd(const avr_render_params* p, int32_t B, const void* signal
                        int32_t sig_dtype, const float* w, const int32_t* delay,
                        int32_t n_split, float* part, void* stream);
 
+/* Number of ray splits avr_ray_reduce_fwd should use for this shape (a power
+ * of two <= 16); the caller sizes `part` with it. */
+int avr_reduce_splits(const avr_render_params* p, int32_t B, int32_t sig_dtype, int32_t* n_split);
+
 /* ---- a9/a10/a11/a12 (frequency half): DFT + phase + sum over samples ---
  * z[b,s,t] = pl[shift[s]+t] * [t < T-1-shift[s]] * sum_k part[k,b,s,t]
  * spart[B][P][F][2], P = ceil(S/32) * k_split: partial spectra

@@ -25,6 +25,15 @@ for s in "$@"; do
     streams) step bench_s1 200 python bench.py --no-cpu-baseline --steps 200 --streams 1 && step bench_s2 200 python bench.py --no-cpu-baseline --steps 200 --streams 2 && step bench_s3 200 python bench.py --no-cpu-baseline --steps 200 --streams 3 ;;
     tune) step tune 600 python tools/tune.py ;;
     tune5) step tune5 600 python tools/tune.py --workload c5_simu_4096x512x2048 --rounds 3 --steps 5 --nsplit 2,4,8 --ksplit 8 --variants u4nt,u8nt,u4 ;;
+    sweep) step sw_c2 300 python tools/tune.py --variants u4nt,u8nt --nsplit 1,2,4 --ksplit 8 --rounds 3 \
+            && step sw_c2h 300 python tools/tune.py --dtype float16 --variants u4nt,u8nt --nsplit 2,4,8 --ksplit 8 --rounds 3 \
+            && step sw_c3 300 python tools/tune.py --workload c3_raf_furnished_b4 --variants u4nt,u8nt --nsplit 2,4,8 --ksplit 8 --rounds 3 \
+            && step sw_c5 300 python tools/tune.py --workload c5_simu_4096x512x2048 --variants u4nt,u8nt --nsplit 1,2,4,8 --ksplit 8 --rounds 2 --steps 5 \
+            && step sw_c1 300 python tools/tune.py --workload c1_meshrir_plumbing --variants u4nt --nsplit 1,2,4 --ksplit 4 --rounds 3 ;;
+    exp5) step exp_c2h 300 python tools/tune.py --dtype float16 --variants u4nt,u4 --nsplit 2,4 --ksplit 8 --rounds 3 \
+            && step exp_c5_4088 300 python tools/tune.py --workload c5_simu_4096x512x2048 --T 4088 --variants u4nt,u4 --nsplit 4,8 --ksplit 8 --rounds 2 --steps 5 \
+            && step exp_c5_S128 300 python tools/tune.py --workload c5_simu_4096x512x2048 --S 128 --variants u4nt,u4 --nsplit 4,8 --ksplit 8 --rounds 2 --steps 5 \
+            && step exp_c5_fp32 300 python tools/tune.py --workload c5_simu_4096x512x2048 --S 128 --dtype float32 --variants u4nt --nsplit 2,4,8 --ksplit 8 --rounds 2 --steps 5 ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 50 --warmup 5 --streams 1 ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 3 --streams 1 && step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 3 --streams 1 ;;
   esac

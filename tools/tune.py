@@ -32,9 +32,27 @@ def main():
     ap.add_argument("--variants", default="u4nt,u8nt")
     ap.add_argument("--nsplit", default="1,2,4")
     ap.add_argument("--ksplit", default="4,8,16")
+    ap.add_argument("--T", type=int, default=0)
+    ap.add_argument("--S", type=int, default=0)
+    ap.add_argument("--nazi", type=int, default=0)
+    ap.add_argument("--dtype", default="")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     w = WORKLOADS[args.workload]
+    over = {}
+    if args.T:
+        over["T"] = args.T
+    if args.S:
+        over["n_samples"] = args.S
+    if args.nazi:
+        over["n_azi"] = args.nazi
+    if args.dtype:
+        over["signal_dtype"] = args.dtype
+        over["attn_dtype"] = args.dtype
+    if over:
+        w = w.replace(**over)
+    print(json.dumps({"workload": w.name, "R": w.n_rays, "S": w.n_samples, "T": w.T,
+                      "dtype": w.signal_dtype}))
     B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
     dt = torch.float16 if w.signal_dtype == "float16" else torch.float32
     g = torch.Generator(device=dev).manual_seed(0)
