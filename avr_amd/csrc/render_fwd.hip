@@ -895,11 +895,15 @@ extern "C" int avr_reduce_splits(const avr_render_params* p, int32_t B, int32_t 
         *n_split = atoi(f);
         return 0;
     }
-    // power of two <= 16 (the DFT staging is templated on it): at least ~2
-    // workgroups per CU, and a split's w/delay fits the 32 KiB LDS slab
+    // power of two <= 16 (the DFT staging is templated on it) giving ~8 (fp32)
+    // or ~16 (fp16: twice the VALU work per byte) resident waves per CU, and
+    // a split's w/delay within the 32 KiB LDS slab.  Sweeps:
+    // profiles/r01_sweep_*.jsonl.
+    const int64_t waves_target = (vec == 8) ? 4096 : 2048;
+    const int64_t waves_per_split = (int64_t)groups * B * (sh.threads / 64);
     int n = 1;
     auto rps = [&](int k) { return (R + k - 1) / k; };
-    while (n < 16 && ((int64_t)n * groups * B < 512 || rps(n) * sh.G > kMaxGroupRays) &&
+    while (n < 16 && (n * waves_per_split < waves_target || rps(n) * sh.G > kMaxGroupRays) &&
            rps(2 * n) >= 8)
         n *= 2;
     if (rps(n) * sh.G > kMaxGroupRays) return fail(AVR_E_CONFIG, "avr_reduce_splits: too many rays");
