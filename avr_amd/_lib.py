@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(_HERE, "libavr_hip.so")
 
 DTYPE_F32 = 0
 DTYPE_F16 = 1
+DTYPE_BF16 = 2
 MAX_AZI = 512  # AVR_MAX_AZI
 
 _c_i32 = ctypes.c_int32

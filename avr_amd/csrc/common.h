@@ -8,6 +8,7 @@
 
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
+#include <hip/hip_bf16.h>
 #include <stdint.h>
 #include <string>
 
@@ -30,8 +31,17 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 // ---------------------------------------------------------------- dtypes
 __device__ __forceinline__ float load_f(const float* p, int64_t i) { return p[i]; }
 __device__ __forceinline__ float load_f(const __half* p, int64_t i) { return __half2float(p[i]); }
+__device__ __forceinline__ float load_f(const __hip_bfloat16* p, int64_t i) {
+    return __bfloat162float(p[i]);
+}
 __device__ __forceinline__ void store_f(float* p, int64_t i, float v) { p[i] = v; }
 __device__ __forceinline__ void store_f(__half* p, int64_t i, float v) { p[i] = __float2half(v); }
+__device__ __forceinline__ void store_f(__hip_bfloat16* p, int64_t i, float v) {
+    p[i] = __float2bfloat16(v);  // round to nearest even
+}
+// bf16 pair packed in a dword -> two floats (exact)
+__device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 
 // ---------------------------------------------------------------- geometry
 // torch.linspace(a, b, n)[i] on CPU: step = (b-a)/(n-1) in fp32, lower half

@@ -128,6 +128,31 @@ struct V16<__half> {
     }
 };
 
+template <>
+struct V16<__hip_bfloat16> {
+    static constexpr int N = 8;
+    __device__ static void load(const __hip_bfloat16* p, float* o) {
+        uint4 v = *reinterpret_cast<const uint4*>(p);
+        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            o[2 * i] = bf16_lo(u[i]);
+            o[2 * i + 1] = bf16_hi(u[i]);
+        }
+    }
+    __device__ static void store(__hip_bfloat16* p, const float* o) {
+        uint32_t u[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const __hip_bfloat16 a = __float2bfloat16(o[2 * i]);
+            const __hip_bfloat16 b = __float2bfloat16(o[2 * i + 1]);
+            u[i] = (uint32_t)(*reinterpret_cast<const uint16_t*>(&a)) |
+                   ((uint32_t)(*reinterpret_cast<const uint16_t*>(&b)) << 16);
+        }
+        *reinterpret_cast<uint4*>(p) = make_uint4(u[0], u[1], u[2], u[3]);
+    }
+};
+
 constexpr int kRbThreads = 256;
 
 template <typename Tin, bool VECTOR, int CPL>
@@ -383,6 +408,11 @@ extern "C" int avr_ray_reduce_bwd(const avr_render_params* p, int32_t B, const v
             return launch_rb<__half, true>(p, B, signal, gz, w, delay, grad_signal, grad_w, s);
         return launch_rb<__half, false>(p, B, signal, gz, w, delay, grad_signal, grad_w, s);
     }
+    if (sig_dtype == AVR_DTYPE_BF16) {
+        if (aligned && st % 8 == 0)
+            return launch_rb<__hip_bfloat16, true>(p, B, signal, gz, w, delay, grad_signal, grad_w, s);
+        return launch_rb<__hip_bfloat16, false>(p, B, signal, gz, w, delay, grad_signal, grad_w, s);
+    }
     return fail(AVR_E_ARG, "avr_ray_reduce_bwd: unknown signal dtype");
 }
 
@@ -400,8 +430,11 @@ extern "C" int avr_weights_bwd(const avr_render_params* p, int32_t B, const void
         if (attn_dtype == AVR_DTYPE_F32)
             (void)hipFuncSetAttribute((const void*)weights_bwd_kernel<float>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        else
+        else if (attn_dtype == AVR_DTYPE_F16)
             (void)hipFuncSetAttribute((const void*)weights_bwd_kernel<__half>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        else
+            (void)hipFuncSetAttribute((const void*)weights_bwd_kernel<__hip_bfloat16>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
     if (attn_dtype == AVR_DTYPE_F32)
@@ -411,6 +444,10 @@ extern "C" int avr_weights_bwd(const avr_render_params* p, int32_t B, const void
         hipLaunchKernelGGL(weights_bwd_kernel<__half>, grid, dim3(64 * wpb), lds,
                            as_stream(stream), *p, (int)B, (const __half*)attn, d_vals, grad_w,
                            (__half*)grad_attn, wpb);
+    else if (attn_dtype == AVR_DTYPE_BF16)
+        hipLaunchKernelGGL(weights_bwd_kernel<__hip_bfloat16>, grid, dim3(64 * wpb), lds,
+                           as_stream(stream), *p, (int)B, (const __hip_bfloat16*)attn, d_vals, grad_w,
+                           (__hip_bfloat16*)grad_attn, wpb);
     else
         return fail(AVR_E_ARG, "avr_weights_bwd: unknown attn dtype");
     return check_launch("avr_weights_bwd");

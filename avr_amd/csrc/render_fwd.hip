@@ -317,6 +317,19 @@ struct Vec16<__half> {
     }
 };
 
+template <>
+struct Vec16<__hip_bfloat16> {
+    static constexpr int N = 8;
+    using raw = u32x4;
+    __device__ static void cvt(const raw& v, float* o) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            o[2 * i] = bf16_lo(v[i]);
+            o[2 * i + 1] = bf16_hi(v[i]);
+        }
+    }
+};
+
 constexpr int kMaxReduceThreads = 1024;
 constexpr int kMaxGroupRays = 4096;  // G * rays_per_split (LDS: 32 KiB of w/delay)
 
@@ -787,6 +800,8 @@ extern "C" int avr_weights_fwd(const avr_render_params* p, int32_t B, const void
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         (void)hipFuncSetAttribute((const void*)weights_fwd_kernel<__half>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)weights_fwd_kernel<__hip_bfloat16>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
     if (attn_dtype == AVR_DTYPE_F32)
         hipLaunchKernelGGL(weights_fwd_kernel<float>, grid, dim3(256), lds, as_stream(stream), *p,
@@ -794,6 +809,10 @@ extern "C" int avr_weights_fwd(const avr_render_params* p, int32_t B, const void
     else if (attn_dtype == AVR_DTYPE_F16)
         hipLaunchKernelGGL(weights_fwd_kernel<__half>, grid, dim3(256), lds, as_stream(stream),
                            *p, (int)B, (const __half*)attn, rays_o, pos_tx, dirs, d_vals, w, delay);
+    else if (attn_dtype == AVR_DTYPE_BF16)
+        hipLaunchKernelGGL(weights_fwd_kernel<__hip_bfloat16>, grid, dim3(256), lds,
+                           as_stream(stream), *p, (int)B, (const __hip_bfloat16*)attn, rays_o,
+                           pos_tx, dirs, d_vals, w, delay);
     else
         return fail(AVR_E_ARG, "avr_weights_fwd: unknown attn dtype");
     return check_launch("avr_weights_fwd");
@@ -888,7 +907,7 @@ extern "C" int avr_reduce_splits(const avr_render_params* p, int32_t B, int32_t 
     if (int e = validate(p)) return e;
     AVR_REQUIRE(B >= 1 && n_split, "avr_reduce_splits: bad args");
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
-    const int vec = (sig_dtype == AVR_DTYPE_F16) ? 8 : 4;
+    const int vec = (sig_dtype == AVR_DTYPE_F16 || sig_dtype == AVR_DTYPE_BF16) ? 8 : 4;
     const ReduceShape sh = vec == 8 ? reduce_shape<8>(S, T) : reduce_shape<4>(S, T);
     const int groups = (S + sh.G - 1) / sh.G;
     if (const char* f = getenv("AVR_NSPLIT")) {  // tuning override
@@ -930,6 +949,11 @@ extern "C" int avr_ray_reduce_fwd(const avr_render_params* p, int32_t B, const v
     if (sig_dtype == AVR_DTYPE_F16) {
         if (aligned && st % 8 == 0) return launch_reduce<__half, true>(p, B, signal, w, delay, n_split, part, s);
         return launch_reduce<__half, false>(p, B, signal, w, delay, n_split, part, s);
+    }
+    if (sig_dtype == AVR_DTYPE_BF16) {
+        if (aligned && st % 8 == 0)
+            return launch_reduce<__hip_bfloat16, true>(p, B, signal, w, delay, n_split, part, s);
+        return launch_reduce<__hip_bfloat16, false>(p, B, signal, w, delay, n_split, part, s);
     }
     return fail(AVR_E_ARG, "avr_ray_reduce_fwd: unknown signal dtype");
 }

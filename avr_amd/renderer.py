@@ -27,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from ._lib import DTYPE_F16, DTYPE_F32, render_params
+from ._lib import DTYPE_BF16, DTYPE_F16, DTYPE_F32, render_params
 
 # Optional instrumentation for bench.py: an object with begin(stream) / end(stream)
 # called around the dominant kernel (the ray-reduction stream).  None in normal use.
@@ -50,7 +50,9 @@ def _dtype_code(t):
         return DTYPE_F32
     if t.dtype == torch.float16:
         return DTYPE_F16
-    raise TypeError(f"unsupported dtype {t.dtype} (float32 or float16)")
+    if t.dtype == torch.bfloat16:
+        return DTYPE_BF16
+    raise TypeError(f"unsupported dtype {t.dtype} (float32, float16 or bfloat16)")
 
 
 # --------------------------------------------------------------------------
@@ -333,9 +335,10 @@ class AVRRender(nn.Module):
         """Render core (renderer.py:74-124) on given network outputs."""
         dev, B = geom["device"], geom["B"]
         S = int(self.n_samples)
-        if attn.dtype not in (torch.float32, torch.float16):
+        native = (torch.float32, torch.float16, torch.bfloat16)
+        if attn.dtype not in native:
             attn = attn.float()
-        if signal.dtype not in (torch.float32, torch.float16):
+        if signal.dtype not in native:
             signal = signal.float()
         attn = attn.to(dev).reshape(B, -1).contiguous()
         T = signal.size(-1)

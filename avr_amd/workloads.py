@@ -106,3 +106,29 @@ def grad_probe(w: Workload, seed: int):
     """Fixed upstream gradient dL/d(out) [B,F,2] used by the backward fixtures."""
     rng = np.random.default_rng(10_000 + seed)
     return rng.standard_normal(size=(w.batch, w.F, 2)).astype(np.float32)
+
+
+def _grid(log2):
+    return dict(otype="HashGrid", n_levels=20, n_features_per_level=2, log2_hashmap_size=log2,
+                base_resolution=16)
+
+
+def _mlp(n_hidden, width):
+    return dict(otype="FullyFusedMLP", activation="ReLU", output_activation="None",
+                n_neurons=width, n_hidden_layers=n_hidden)
+
+
+# `model:` blocks of the reference configs (shapes only; weights are random)
+MESHRIR_MODEL = dict(  # config_files/avr_meshrir.yml:44-89
+    signal_output_dim=2400, leaky_relu=0.03,
+    pos_encoding_sigma=_grid(18), dir_encoding_sig=_grid(20), tx_encoding_sig=_grid(18),
+    sigma_encoder_network=_mlp(3, 128), sigma_decoder_network=_mlp(3, 128),
+    signal_network=dict(_mlp(3, 512), otype="CutlassMLP"),
+)
+RAF_MODEL = dict(  # config_files/avr_raf_furnished.yml:37-100
+    signal_output_dim=1600, leaky_relu=0.03,
+    pos_encoding_sigma=_grid(18), pos_encoding_sig=_grid(18), dir_encoding_sig=_grid(18),
+    tx_pos_encoding_sigma=_grid(18), tx_pos_encoding_sig=_grid(18), tx_dir_encoding_sig=_grid(18),
+    sigma_encoder_network=_mlp(3, 128), sigma_decoder_network=_mlp(1, 128),
+    signal_network=dict(_mlp(4, 512), otype="CutlassMLP"),
+)

@@ -37,6 +37,7 @@ extern "C" {
 /* element types of network outputs / gradients */
 #define AVR_DTYPE_F32 0
 #define AVR_DTYPE_F16 1
+#define AVR_DTYPE_BF16 2  /* network outputs of bf16 MLPs (render kernels only) */
 
 /* error codes besides hipError_t values */
 #define AVR_E_ARG 1001      /* bad argument / shape / alignment */

@@ -264,3 +264,39 @@ def test_ray_range_shards_sum_to_full(n_shards):
         assert net.seen[0].shape[1] == (r1 - r0) * S
         total = part if total is None else total + part
     assert rel_l2(total.cpu().numpy(), case["out"]) < TOL
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_reduced_precision_storage_matches_oracle_on_rounded_inputs(dtype):
+    """Network outputs stored in bf16/fp16 are upcast exactly in-kernel, so the
+    render matches the oracle fed the same rounded values."""
+    case = Case("c3_s0")
+    inp = case.inputs()
+    w = case.workload
+    attn_r = torch.from_numpy(inp["attn"]).to(dtype)
+    sig_r = torch.from_numpy(inp["signal"]).to(dtype)
+    torch.manual_seed(case.seed)
+    ref = orc.render_spectrum(orc.RenderConfig.from_kwargs(**w.render),
+                              orc.StubNetwork(attn_r.float(), sig_r.float()),
+                              torch.from_numpy(inp["rays_o"]), torch.from_numpy(inp["position_tx"]),
+                              torch.from_numpy(inp["direction_tx"])).numpy()
+    a = attn_r.to(DEV).requires_grad_(True)
+    sgn = sig_r.to(DEV).requires_grad_(True)
+    r = AVRRender(Net(a, sgn), **w.render)
+    torch.manual_seed(case.seed)
+    out = r(torch.from_numpy(inp["rays_o"]).to(DEV), torch.from_numpy(inp["position_tx"]).to(DEV),
+            torch.from_numpy(inp["direction_tx"]).to(DEV))
+    assert rel_l2(out.detach().cpu().numpy(), ref) < TOL
+    (out * torch.from_numpy(case.grad_probe()).to(DEV)).sum().backward()
+    assert sgn.grad.dtype == dtype and a.grad.dtype == dtype
+    # gradients agree with the fp32 path up to the storage rounding
+    a32 = torch.from_numpy(inp["attn"]).to(DEV).requires_grad_(True)
+    s32 = torch.from_numpy(inp["signal"]).to(DEV).requires_grad_(True)
+    r32 = AVRRender(Net(a32, s32), **w.render)
+    torch.manual_seed(case.seed)
+    o32 = r32(torch.from_numpy(inp["rays_o"]).to(DEV), torch.from_numpy(inp["position_tx"]).to(DEV),
+              torch.from_numpy(inp["direction_tx"]).to(DEV))
+    (o32 * torch.from_numpy(case.grad_probe()).to(DEV)).sum().backward()
+    gs, gs32 = sgn.grad.float().cpu().numpy(), s32.grad.cpu().numpy()
+    tol = 2e-2 if dtype == torch.bfloat16 else 3e-3
+    assert rel_l2(gs, gs32) < tol

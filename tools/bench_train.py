@@ -1,0 +1,110 @@
+"""Training-step benchmark for BASELINE configs[2]/[3] (RAF, batch 4 per GPU).
+
+Two numbers, both fwd+bwd:
+  * render core only: stub network outputs resident in HBM, grads to attn and
+    signal (the hot path's backward);
+  * full step: AVRModel_complex (6 HIP hash grids + PyTorch MLPs) ->
+    renderer -> L1 spectrum loss -> backward -> grad clip -> Adam
+    (avr_runner.py:181-200 without the auraloss criterion).
+
+    python tools/bench_train.py [--workload c3_raf_furnished_b4] [--steps 20] [--mlp-dtype bf16]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from avr_amd import AVRRender  # noqa: E402
+from avr_amd.model import AVRModel_complex  # noqa: E402
+from avr_amd.workloads import RAF_MODEL, WORKLOADS  # noqa: E402
+
+
+class Stub(torch.nn.Module):
+    def __init__(self, attn, signal):
+        super().__init__()
+        self.attn, self.signal = attn, signal
+
+    def forward(self, pts, view, tx, dir_tx=None):
+        return self.attn, self.signal
+
+
+def timeit(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="c3_raf_furnished_b4")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mlp-dtype", default="bf16", choices=["bf16", "fp32"])
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    w = WORKLOADS[args.workload]
+    B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
+    g = torch.Generator(device=dev).manual_seed(0)
+    ro = torch.rand(B, 3, device=dev, generator=g) * 4 - 2
+    tx = torch.rand(B, 3, device=dev, generator=g) * 4 - 2
+    dtx = torch.nn.functional.normalize(torch.randn(B, 3, device=dev, generator=g), dim=-1)
+    res = {"workload": w.name, "ray_samples_per_step": w.ray_samples}
+
+    # render core fwd+bwd
+    attn = (torch.rand(B, R * S, 1, device=dev, generator=g) * 2).requires_grad_(True)
+    sig = (torch.randn(B, R * S, T, device=dev, generator=g) * 0.1).requires_grad_(True)
+    rc = AVRRender(Stub(attn, sig), **w.render)
+    gout = torch.randn(B, T // 2 + 1, 2, device=dev, generator=g)
+
+    def core():
+        attn.grad = None
+        sig.grad = None
+        out = rc(ro, tx, dtx)
+        out.backward(gout)
+
+    t = timeit(core, args.steps, args.warmup)
+    res["render_core_fwd_bwd_ms"] = t * 1e3
+    res["render_core_ray_samples_per_s"] = w.ray_samples / t
+    # algorithmic bytes: read x twice (fwd, bwd), write grad x, attn/grad attn, w/delay
+    alg = w.ray_samples * (3 * T * 4 + 4 * 4)
+    res["render_core_alg_GBps"] = alg / t / 1e9
+    del attn, sig, rc
+
+    # full training step
+    mlp_dtype = torch.bfloat16 if args.mlp_dtype == "bf16" else torch.float32
+    cfg = dict(RAF_MODEL, signal_output_dim=T)
+    model = AVRModel_complex(cfg, mlp_dtype=mlp_dtype).to(dev)
+    r = AVRRender(model, **w.render).to(dev)
+    opt = torch.optim.Adam(r.parameters(), lr=2e-4)
+    target = torch.randn(B, T // 2 + 1, 2, device=dev, generator=g)
+
+    def train_step():
+        out = r(ro, tx, dtx)
+        loss = (out - target).abs().mean()
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(r.parameters(), max_norm=1)
+        opt.step()
+
+    t = timeit(train_step, args.steps, args.warmup)
+    res["train_step_ms"] = t * 1e3
+    res["train_ray_samples_per_s"] = w.ray_samples / t
+    res["mlp_dtype"] = args.mlp_dtype
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
