@@ -118,22 +118,35 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(int64_t N, int L,
     store_pair(out, q, acc);
 }
 
+// Backward: scatter-add of w_corner * dL/dy into the tables.  One thread per
+// point for ONE level (blockIdx.y), so a wavefront holds 64 consecutive
+// points of one level.  Consecutive points are often identical or share a
+// cell (tx and dir_tx are constant over a pose, view over a ray, coarse
+// levels are shared by neighbouring samples), and float atomics to one
+// address serialise at the memory side (MI355X_MICROARCH.md, Global float
+// atomics, 'contention').  So each corner's contributions are first summed
+// over runs of equal table index inside the wavefront (head-flag segmented
+// scan, 6 shuffle steps) and only the last lane of each run issues the
+// atomic: a pose-constant input costs one atomic per corner per wavefront
+// instead of 64.
 template <typename Tg>
 __global__ __launch_bounds__(256) void hashgrid_bwd_kernel(int64_t N, int L,
                                                            const float* __restrict__ x,
                                                            const Tg* __restrict__ gout,
                                                            LevelTable lt,
                                                            float* __restrict__ gparams) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= N * L) return;
-    const int64_t i = q / L;
-    const int l = (int)(q % L);
-    const float xi[3] = {x[i * 3 + 0], x[i * 3 + 1], x[i * 3 + 2]};
+    const int l = blockIdx.y;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const bool live = i < N;
+    const int64_t ic = live ? i : N - 1;
+    const float xi[3] = {x[ic * 3 + 0], x[ic * 3 + 1], x[ic * 3 + 2]};
     const Corner c = locate(xi, lt.scale[l]);
     const uint32_t size = (uint32_t)(lt.offset[l + 1] - lt.offset[l]);
     const uint32_t res = lt.res[l];
     float* table = gparams + 2 * lt.offset[l];
-    const float2 g = load_pair(gout, q);
+    float2 g = load_pair(gout, ic * L + l);
+    if (!live) g = make_float2(0.0f, 0.0f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         float wgt = 1.0f;
@@ -148,9 +161,28 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_kernel(int64_t N, int L,
                 gg[d] = c.grid[d];
             }
         }
-        const int64_t e = grid_index(size, res, gg[0], gg[1], gg[2]);
-        atomicAdd(table + 2 * e, wgt * g.x);
-        atomicAdd(table + 2 * e + 1, wgt * g.y);
+        const uint32_t e = grid_index(size, res, gg[0], gg[1], gg[2]);
+        float vx = wgt * g.x, vy = wgt * g.y;
+        // runs of equal e: head flags -> start lane of this lane's run
+        const uint32_t prev = __shfl_up(e, 1, 64);
+        const bool head = lane == 0 || prev != e;
+        const unsigned long long heads = __ballot(head);
+        const unsigned long long upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
+        const int start = 63 - __clzll(heads & upto);
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const float ox = __shfl_up(vx, off, 64);
+            const float oy = __shfl_up(vy, off, 64);
+            if (lane - off >= start) {
+                vx += ox;
+                vy += oy;
+            }
+        }
+        const bool tail = lane == 63 || ((heads >> (lane + 1)) & 1ull);
+        if (tail && (vx != 0.0f || vy != 0.0f)) {
+            atomicAdd(table + 2 * (int64_t)e, vx);
+            atomicAdd(table + 2 * (int64_t)e + 1, vy);
+        }
     }
 }
 
@@ -208,8 +240,7 @@ extern "C" int avr_hashgrid_bwd(int64_t N, int32_t n_levels, const float* x, con
     if (N == 0) return 0;
     LevelTable lt;
     if (int e = make_table(n_levels, level_offset, level_scale, level_res, &lt)) return e;
-    const int64_t work = N * n_levels;
-    const dim3 grid((unsigned)((work + 255) / 256));
+    const dim3 grid((unsigned)((N + 255) / 256), (unsigned)n_levels);
     hipStream_t st = as_stream(stream);
     if (grad_dtype == AVR_DTYPE_F32)
         hipLaunchKernelGGL(hashgrid_bwd_kernel<float>, grid, dim3(256), 0, st, N, (int)n_levels, x,
