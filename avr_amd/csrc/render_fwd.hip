@@ -842,7 +842,13 @@ template <int VEC>
 ReduceShape reduce_shape(int S, int T) {
     ReduceShape sh;
     sh.G = 1;
-    while (sh.G < 4 && 2 * sh.G * T <= 256 * VEC && 2 * sh.G <= S) sh.G *= 2;
+    // super-rows of up to 512 chunks (G = 2 at config 2: measured 5% faster
+    // than G = 1 in the same process, profiles/r01_sweep_g*.jsonl)
+    while (sh.G < 4 && 2 * sh.G * T <= 512 * VEC && 2 * sh.G <= S) sh.G *= 2;
+    if (const char* g = getenv("AVR_REDUCE_G")) {  // tuning override (1, 2 or 4)
+        const int v = atoi(g);
+        if ((v == 1 || v == 2 || v == 4) && v <= S) sh.G = v;
+    }
     int max_phase = 0;  // group starts are s0 = multiples of G; S*T % VEC == 0
     for (int s0 = 0; s0 < S && s0 < VEC * sh.G; s0 += sh.G)
         max_phase = max(max_phase, (int)(((int64_t)s0 * T) % VEC));
@@ -896,7 +902,8 @@ int launch_reduce(const avr_render_params* p, int B, const void* sig, const floa
         return launch_reduce_v<Tin, VECTOR, C, GG>(grid, block, lds, st, s, w, delay, part, B, R, S, \
                                                    T, rps, total),                                 \
                check_launch("avr_ray_reduce_fwd");
-    AVR_RR(1, 1) AVR_RR(1, 2) AVR_RR(1, 4) AVR_RR(2, 1) AVR_RR(3, 1) AVR_RR(4, 1)
+    AVR_RR(1, 1) AVR_RR(1, 2) AVR_RR(1, 4) AVR_RR(2, 1) AVR_RR(2, 2) AVR_RR(2, 4) AVR_RR(3, 1)
+    AVR_RR(4, 1)
 #undef AVR_RR
     return fail(AVR_E_CONFIG, "ray_reduce: T too long for this build");
 }

@@ -36,6 +36,9 @@ for s in "$@"; do
             && step exp_c5_fp32 300 python tools/tune.py --workload c5_simu_4096x512x2048 --S 128 --dtype float32 --variants u4nt --nsplit 2,4,8 --ksplit 8 --rounds 2 --steps 5 ;;
     train) step train_c3 600 python tools/bench_train.py && step train_c4 600 python tools/bench_train.py --workload c4_raf_empty_b4_per_gpu ;;
     proftrain) step proftrain 600 rocprofv3 --kernel-trace --stats -d $OUT/proftrain -o run --output-format csv -- python tools/bench_train.py --steps 5 --warmup 2 ;;
+    gexp) step g1 200 python tools/tune.py --variants u4nt --nsplit 2,4 --ksplit 8 --rounds 3 \
+          && AVR_REDUCE_G=2 step g2 200 python tools/tune.py --variants u4nt --nsplit 1,2,4 --ksplit 8 --rounds 3 \
+          && AVR_REDUCE_G=4 step g4 200 python tools/tune.py --variants u4nt --nsplit 1,2 --ksplit 8 --rounds 3 ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 50 --warmup 5 --streams 1 ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 3 --streams 1 && step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 3 --streams 1 ;;
   esac
