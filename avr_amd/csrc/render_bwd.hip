@@ -153,77 +153,153 @@ struct V16<__hip_bfloat16> {
     }
 };
 
-constexpr int kRbThreads = 256;
+constexpr int kMaxRbThreads = 1024;
+constexpr int kMaxRbRays = 4096;  // G * rays per split
 
-template <typename Tin, bool VECTOR, int CPL>
-__global__ __launch_bounds__(kRbThreads) void ray_reduce_bwd_kernel(
+// The forward reduction's twin: one workgroup per (ray split, column group of
+// G samples, b) streams the group's contiguous super-rows ray by ray.  Each
+// lane keeps gz for its fixed (g, t) chunk slots in registers, reads the
+// signal chunk once, writes grad_x = w*[t>=delay]*gz with 16-byte stores
+// (masked scalar stores only where a chunk leaves the super-row) and adds
+// its share of grad_w = sum_t [t>=delay]*gz*x, reduced per ray by a wave
+// shuffle tree and one LDS atomic per wave.
+template <typename Tin, bool VECTOR, int CPT, int G, int MAXT>
+__global__ __launch_bounds__(MAXT) void ray_reduce_bwd_kernel(
     const Tin* __restrict__ sig, const float* __restrict__ gz, const float* __restrict__ w,
     const int32_t* __restrict__ delay, Tin* __restrict__ gsig, float* __restrict__ gw, int B,
-    int R, int S, int T, int rays_per_block) {
+    int R, int S, int T, int rays_per_split, int64_t total) {
     constexpr int VEC = VECTOR ? V16<Tin>::N : 1;
-    const int split = blockIdx.x, s = blockIdx.y, b = blockIdx.z;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int r0 = split * rays_per_block;
-    const int r1 = min(R, r0 + rays_per_block);
-    const int64_t row_stride = (int64_t)S * T;
-    const int64_t rowA = (((int64_t)b * R + r0) * S + s) * (int64_t)T;
-    const int phase = (int)(rowA % VEC);
-    const int nchunks = (T + phase + VEC - 1) / VEC;
-    // this lane's gz values
-    float g[CPL][VEC];
-    int t0[CPL];
-    const float* gzr = gz + ((int64_t)b * S + s) * T;
-#pragma unroll
-    for (int c = 0; c < CPL; ++c) {
-        t0[c] = (lane + c * 64) * VEC - phase;
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            const int t = t0[c] + k;
-            g[c][k] = (t >= 0 && t < T) ? gzr[t] : 0.0f;
+    extern __shared__ float lds_rb[];  // w_l[G][nr], d_l[G][nr], dot_l[G][nr]
+    const int nthreads = blockDim.x, lane = threadIdx.x & 63;
+    const int split = blockIdx.x, s0 = blockIdx.y * G, b = blockIdx.z;
+    const int gcount = min(G, S - s0);
+    const int r0 = split * rays_per_split;
+    const int nr = max(0, min(R, r0 + rays_per_split) - r0);
+    const int stride_l = G * max(nr, 1);
+    float* w_l = lds_rb;
+    int* d_l = reinterpret_cast<int*>(lds_rb + stride_l);
+    float* dot_l = lds_rb + 2 * stride_l;
+    for (int i = threadIdx.x; i < G * nr; i += nthreads) {
+        const int g = i / nr, rr = i - g * nr;
+        dot_l[i] = 0.0f;
+        if (g < gcount) {
+            const int64_t idx = ((int64_t)b * R + r0 + rr) * S + s0 + g;
+            w_l[i] = w[idx];
+            d_l[i] = delay[idx];
+        } else {
+            w_l[i] = 0.0f;
+            d_l[i] = 0x7fffffff;
         }
     }
-    for (int r = r0 + wave; r < r1; r += kRbThreads / 64) {
-        const int64_t ridx = ((int64_t)b * R + r) * S + s;
-        const float wr = w[ridx];
-        const int dr = delay[ridx];
-        const int64_t rowbase = rowA + (int64_t)(r - r0) * row_stride - phase;
-        float dot = 0.0f;
+    const int64_t row0 = (((int64_t)b * R + r0) * S + s0) * (int64_t)T;
+    const int L = gcount * T;
+    const int phase = (int)(row0 % VEC);
+    const int nchunks = (L + phase + VEC - 1) / VEC;
+    const int64_t row_stride = (int64_t)S * T;
+
+    float gv[CPT][VEC];
+    int tk[CPT][VEC], gk[CPT][VEC];
+    bool full[CPT];  // chunk lies inside the super-row: vector store allowed
+    const float* gzc = gz + ((int64_t)b * S + s0) * T;  // gz rows of the group are contiguous
 #pragma unroll
-        for (int c = 0; c < CPL; ++c) {
-            const int j = lane + c * 64;
-            if (j >= nchunks) continue;
-            const int64_t e0 = rowbase + (int64_t)j * VEC;
-            const bool interior = VECTOR && t0[c] >= 0 && t0[c] + VEC <= T;
-            float x[VEC], o[VEC];
-            if (interior) {
-                V16<Tin>::load(sig + e0, x);
-            } else {
+    for (int c = 0; c < CPT; ++c) {
+        const int j = threadIdx.x + c * nthreads;
+        const int ebase = j * VEC - phase;
+        full[c] = j < nchunks && ebase >= 0 && ebase + VEC <= L;
 #pragma unroll
-                for (int k = 0; k < VEC; ++k) {
-                    const int t = t0[c] + k;
-                    x[k] = (t >= 0 && t < T) ? load_f(sig, e0 + k) : 0.0f;
-                }
-            }
+        for (int k = 0; k < VEC; ++k) {
+            const int e = ebase + k;
+            const bool ok = j < nchunks && e >= 0 && e < L;
+            const int g = (G == 1) ? 0 : (ok ? e / T : 0);
+            gk[c][k] = g;
+            tk[c][k] = ok ? e - g * T : -1;
+            gv[c][k] = ok ? gzc[e] : 0.0f;
+        }
+    }
+    __syncthreads();
+
+    auto load_chunk = [&](int64_t rowbase, int c, float* x) {
+        const int j = threadIdx.x + c * nthreads;
+        const int64_t e0 = rowbase + (int64_t)j * VEC;
+        if (VECTOR && j < nchunks && e0 + VEC <= total) {
+            if constexpr (VECTOR) V16<Tin>::load(sig + e0, x);
+            return;
+        }
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) x[k] = (j < nchunks && e0 + k < total) ? load_f(sig, e0 + k) : 0.0f;
+    };
+    auto finish = [&](int r, int64_t rowbase, float (*x)[VEC]) {
+        float wg[G], dotg[G];
+        int dg[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            wg[g] = w_l[g * nr + r];
+            dg[g] = d_l[g * nr + r];
+            dotg[g] = 0.0f;
+        }
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            float o[VEC];
 #pragma unroll
             for (int k = 0; k < VEC; ++k) {
-                const bool keep = (t0[c] + k) >= dr;
-                const float gk = keep ? g[c][k] : 0.0f;
-                o[k] = wr * gk;
-                dot = fmaf(gk, x[k], dot);
+                float ws = wg[0];
+                int ds = dg[0];
+#pragma unroll
+                for (int g = 1; g < G; ++g)
+                    if (gk[c][k] == g) {
+                        ws = wg[g];
+                        ds = dg[g];
+                    }
+                const int t = tk[c][k];
+                const float gm = (t >= 0 && t >= ds) ? gv[c][k] : 0.0f;
+                o[k] = ws * gm;
+                const float pd = gm * x[c][k];
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+                    if (gk[c][k] == g) dotg[g] += pd;
             }
-            if (interior) {
+            const int j = threadIdx.x + c * nthreads;
+            const int64_t e0 = rowbase + (int64_t)j * VEC;
+            if (VECTOR && full[c]) {
                 if constexpr (VECTOR) V16<Tin>::store(gsig + e0, o);
             } else {
 #pragma unroll
-                for (int k = 0; k < VEC; ++k) {
-                    const int t = t0[c] + k;
-                    if (t >= 0 && t < T) store_f(gsig, e0 + k, o[k]);
-                }
+                for (int k = 0; k < VEC; ++k)
+                    if (tk[c][k] >= 0) store_f(gsig, e0 + k, o[k]);
             }
         }
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) dot += __shfl_xor(dot, off, 64);
-        if (lane == 0) gw[ridx] = dot;
+        for (int g = 0; g < G; ++g) {
+            float v = dotg[g];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+            if (lane == 0) atomicAdd(&dot_l[g * nr + r], v);
+        }
+    };
+
+    int r = 0;
+    for (; r + 2 <= nr; r += 2) {
+        float xa[CPT][VEC], xb[CPT][VEC];
+        const int64_t ba = row0 + (int64_t)r * row_stride - phase;
+        const int64_t bb = ba + row_stride;
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) load_chunk(ba, c, xa[c]);
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) load_chunk(bb, c, xb[c]);
+        finish(r, ba, xa);
+        finish(r + 1, bb, xb);
+    }
+    for (; r < nr; ++r) {
+        float xa[CPT][VEC];
+        const int64_t ba = row0 + (int64_t)r * row_stride - phase;
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) load_chunk(ba, c, xa[c]);
+        finish(r, ba, xa);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < G * nr; i += nthreads) {
+        const int g = i / nr, rr = i - g * nr;
+        if (g < gcount) gw[((int64_t)b * R + r0 + rr) * S + s0 + g] = dot_l[i];
     }
 }
 
@@ -339,51 +415,44 @@ int launch_rb(const avr_render_params* p, int B, const void* sig, const float* g
               const int32_t* delay, void* gsig, float* gw, hipStream_t st) {
     constexpr int VEC = VECTOR ? V16<Tin>::N : 1;
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
-    const int nch = (T + 2 * VEC - 2) / VEC;
-    const int cpl = (nch + 63) / 64;
-    // ~4 rows per wave per block; enough blocks to fill the chip
-    int rpb = 16;
-    const int64_t cols = (int64_t)B * S;
-    while (rpb > 4 && cols * ((R + rpb - 1) / rpb) < 2048) rpb /= 2;
-    const dim3 grid((R + rpb - 1) / rpb, S, B);
+    // same super-row shape rule as the forward reduction
+    int G = 1;
+    while (G < 4 && 2 * G * T <= 512 * VEC && 2 * G <= S) G *= 2;
+    int max_phase = 0;
+    for (int s0 = 0; s0 < S && s0 < VEC * G; s0 += G)
+        max_phase = max(max_phase, (int)(((int64_t)s0 * T) % VEC));
+    const int nch = (G * T + max_phase + VEC - 1) / VEC;
+    int cpt = 1;
+    while ((nch + cpt - 1) / cpt > kMaxRbThreads) ++cpt;
+    const int threads = max(64, ((nch + cpt - 1) / cpt + 63) / 64 * 64);
+    const int groups = (S + G - 1) / G;
+    // ~8 resident waves per CU, rays per split within the LDS slab
+    int n = 1;
+    const int64_t wps = (int64_t)groups * B * (threads / 64);
+    auto rps_of = [&](int k) { return (R + k - 1) / k; };
+    while (n < 64 && (n * wps < 2048 || rps_of(n) * G > kMaxRbRays) && rps_of(2 * n) >= 4) n *= 2;
+    const int rps = rps_of(n);
+    if (rps * G > kMaxRbRays) return fail(AVR_E_CONFIG, "ray_reduce_bwd: too many rays per split");
+    const int64_t total = (int64_t)B * R * S * T;
+    const dim3 grid((R + rps - 1) / rps, groups, B);
+    const size_t lds = (size_t)3 * G * max(rps, 1) * 4;
     const Tin* x = (const Tin*)sig;
     Tin* gx = (Tin*)gsig;
-#define AVR_RB(C)                                                                                \
-    case C:                                                                                      \
-        hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, C>), grid, dim3(kRbThreads), 0, st, \
-                           x, gz, w, delay, gx, gw, B, R, S, T, rpb);                            \
-        break;
-    switch (cpl) {
-        AVR_RB(1) AVR_RB(2) AVR_RB(3) AVR_RB(4) AVR_RB(5) AVR_RB(6) AVR_RB(8) AVR_RB(12) AVR_RB(16)
-        AVR_RB(24) AVR_RB(32) AVR_RB(48) AVR_RB(64)
-        default:
-            if (cpl == 7) {
-                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 8>), grid, dim3(kRbThreads), 0,
-                                   st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
-            } else if (cpl <= 12) {
-                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 12>), grid, dim3(kRbThreads),
-                                   0, st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
-            } else if (cpl <= 16) {
-                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 16>), grid, dim3(kRbThreads),
-                                   0, st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
-            } else if (cpl <= 24) {
-                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 24>), grid, dim3(kRbThreads),
-                                   0, st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
-            } else if (cpl <= 32) {
-                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 32>), grid, dim3(kRbThreads),
-                                   0, st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
-            } else if (cpl <= 48) {
-                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 48>), grid, dim3(kRbThreads),
-                                   0, st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
-            } else if (cpl <= 64) {
-                hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, 64>), grid, dim3(kRbThreads),
-                                   0, st, x, gz, w, delay, gx, gw, B, R, S, T, rpb);
-            } else {
-                return fail(AVR_E_CONFIG, "ray_reduce_bwd: T too long");
-            }
+#define AVR_RB(C, GG)                                                                              \
+    if (cpt == C && G == GG) {                                                                     \
+        if (threads <= 512)                                                                        \
+            hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, C, GG, 512>), grid, dim3(threads), \
+                               lds, st, x, gz, w, delay, gx, gw, B, R, S, T, rps, total);          \
+        else                                                                                       \
+            hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, C, GG, 1024>), grid,            \
+                               dim3(threads), lds, st, x, gz, w, delay, gx, gw, B, R, S, T, rps,   \
+                               total);                                                             \
+        return check_launch("avr_ray_reduce_bwd");                                                 \
     }
+    AVR_RB(1, 1) AVR_RB(1, 2) AVR_RB(1, 4) AVR_RB(2, 1) AVR_RB(2, 2) AVR_RB(2, 4) AVR_RB(3, 1)
+    AVR_RB(4, 1)
 #undef AVR_RB
-    return check_launch("avr_ray_reduce_bwd");
+    return fail(AVR_E_CONFIG, "ray_reduce_bwd: T too long for this build");
 }
 }  // namespace
 

@@ -340,8 +340,8 @@ constexpr int kMaxGroupRays = 4096;  // G * rays_per_split (LDS: 32 KiB of w/del
 // chosen so a super-row is ~256*VEC elements (short rows: fp16 or small T);
 // the block size is chosen so every lane owns CPT chunks of it.  Lane slots
 // have fixed (g, t) coordinates, so the accumulators need no shuffling.
-template <typename Tin, bool VECTOR, int CPT, int kUnroll, bool NT, int G>
-__global__ __launch_bounds__(kMaxReduceThreads) void ray_reduce_fwd_kernel(
+template <typename Tin, bool VECTOR, int CPT, int kUnroll, bool NT, int G, int MAXT>
+__global__ __launch_bounds__(MAXT) void ray_reduce_fwd_kernel(
     const Tin* __restrict__ sig, const float* __restrict__ w, const int32_t* __restrict__ delay,
     float* __restrict__ part, int B, int R, int S, int T, int rays_per_split, int64_t total) {
     constexpr int VEC = VECTOR ? Vec16<Tin>::N : 1;
@@ -819,18 +819,12 @@ extern "C" int avr_weights_fwd(const avr_render_params* p, int32_t B, const void
 }
 
 namespace {
-// Streaming variant of the reduction (rows in flight per lane, non-temporal
-// loads).  AVR_REDUCE_VARIANT selects one for tuning runs ("u4", "u8",
-// "u4nt", "u8nt"); the default is the measured best.
+// Streaming variant of the reduction: rows in flight per lane with
+// non-temporal loads.  AVR_REDUCE_VARIANT="u8nt" selects 8 rows for tuning
+// runs; the default "u4nt" is the best of the sweeps (profiles/r01_tune*).
 int reduce_variant() {
     const char* v = getenv("AVR_REDUCE_VARIANT");
-    if (!v) return 2;  // u4nt: best of the sweeps in profiles/r01_tune*_c2.jsonl
-    const std::string s(v);
-    if (s == "u4") return 0;
-    if (s == "u8") return 1;
-    if (s == "u4nt") return 2;
-    if (s == "u8nt") return 3;
-    return 2;
+    return (v && std::string(v) == "u8nt") ? 3 : 2;
 }
 
 struct ReduceShape {
@@ -860,26 +854,27 @@ ReduceShape reduce_shape(int S, int T) {
     return sh;
 }
 
+// Variants: rows in flight per lane (4 or 8, non-temporal loads) x launch
+// bound (512 threads leaves 256 VGPRs per lane, 1024 only 128).
 template <typename Tin, bool VECTOR, int C, int G>
 void launch_reduce_v(dim3 grid, dim3 block, size_t lds, hipStream_t st, const Tin* s, const float* w,
                      const int32_t* delay, float* part, int B, int R, int S, int T, int rps,
                      int64_t total) {
-    switch (reduce_variant()) {
-        case 0:
-            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, false, G>), grid, block, lds,
-                               st, s, w, delay, part, B, R, S, T, rps, total);
-            break;
-        case 1:
-            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, false, G>), grid, block, lds,
-                               st, s, w, delay, part, B, R, S, T, rps, total);
-            break;
-        case 3:
-            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, true, G>), grid, block, lds,
-                               st, s, w, delay, part, B, R, S, T, rps, total);
-            break;
-        default:
-            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, true, G>), grid, block, lds,
-                               st, s, w, delay, part, B, R, S, T, rps, total);
+    const bool u8 = reduce_variant() == 3;
+    if (block.x <= 512) {
+        if (u8)
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, true, G, 512>), grid, block,
+                               lds, st, s, w, delay, part, B, R, S, T, rps, total);
+        else
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, true, G, 512>), grid, block,
+                               lds, st, s, w, delay, part, B, R, S, T, rps, total);
+    } else {
+        if (u8)
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, true, G, 1024>), grid, block,
+                               lds, st, s, w, delay, part, B, R, S, T, rps, total);
+        else
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, true, G, 1024>), grid, block,
+                               lds, st, s, w, delay, part, B, R, S, T, rps, total);
     }
 }
 

@@ -98,3 +98,42 @@ def test_ray_sharded_render_world2_gloo():
         assert res["jitter_ok"], rank
         assert res["rel"] < 1e-6, res
         assert res["grad_ok"], rank
+
+
+def _ddp_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from avr_amd.parallel import ddp, shard_range
+
+        torch.manual_seed(0)
+        net = torch.nn.Linear(8, 4, bias=False)
+        model = ddp(net, None)
+        # each rank takes its own pose shard of a batch of 6 (DistributedSampler-like)
+        x = torch.randn(6, 8, generator=torch.Generator().manual_seed(1))
+        a, b = shard_range(6, rank, world)
+        model(x[a:b]).pow(2).sum().backward()
+        q.put((rank, net.weight.grad.clone()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_helper_allreduces_pose_shard_grads_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    ref = torch.nn.Linear(8, 4, bias=False)
+    x = torch.randn(6, 8, generator=torch.Generator().manual_seed(1))
+    ref(x).pow(2).sum().backward()
+    # DDP averages over ranks: mean of the two shard gradients
+    for g in out.values():
+        torch.testing.assert_close(g, ref.weight.grad / 2, rtol=1e-5, atol=1e-6)
