@@ -417,7 +417,8 @@ int launch_rb(const avr_render_params* p, int B, const void* sig, const float* g
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
     // same super-row shape rule as the forward reduction
     int G = 1;
-    while (G < 4 && 2 * G * T <= 512 * VEC && 2 * G <= S) G *= 2;
+    const int max_chunks = (VEC == 8) ? 256 : 512;
+    while (G < 4 && 2 * G * T <= max_chunks * VEC && 2 * G <= S) G *= 2;
     int max_phase = 0;
     for (int s0 = 0; s0 < S && s0 < VEC * G; s0 += G)
         max_phase = max(max_phase, (int)(((int64_t)s0 * T) % VEC));

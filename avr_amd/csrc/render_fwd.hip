@@ -836,9 +836,12 @@ template <int VEC>
 ReduceShape reduce_shape(int S, int T) {
     ReduceShape sh;
     sh.G = 1;
-    // super-rows of up to 512 chunks (G = 2 at config 2: measured 5% faster
-    // than G = 1 in the same process, profiles/r01_sweep_g*.jsonl)
-    while (sh.G < 4 && 2 * sh.G * T <= 512 * VEC && 2 * sh.G <= S) sh.G *= 2;
+    // super-rows of up to 512 chunks for fp32 (G = 2 at config 2: 5% faster
+    // than G = 1 in the same process, profiles/r01_sweep_g*.jsonl) and 256
+    // for 16-bit storage (more w/delay selects per byte: G = 4 measured 20%
+    // slower than G = 2 on config-2 shapes in fp16)
+    const int max_chunks = (VEC == 8) ? 256 : 512;
+    while (sh.G < 4 && 2 * sh.G * T <= max_chunks * VEC && 2 * sh.G <= S) sh.G *= 2;
     if (const char* g = getenv("AVR_REDUCE_G")) {  // tuning override (1, 2 or 4)
         const int v = atoi(g);
         if ((v == 1 || v == 2 || v == 4) && v <= S) sh.G = v;

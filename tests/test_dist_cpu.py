@@ -114,7 +114,7 @@ def _ddp_worker(rank, world, port, q):
         x = torch.randn(6, 8, generator=torch.Generator().manual_seed(1))
         a, b = shard_range(6, rank, world)
         model(x[a:b]).pow(2).sum().backward()
-        q.put((rank, net.weight.grad.clone()))
+        q.put((rank, net.weight.grad.tolist()))  # plain data: the sender exits right after
     finally:
         dist.destroy_process_group()
 
@@ -136,4 +136,4 @@ def test_ddp_helper_allreduces_pose_shard_grads_gloo():
     ref(x).pow(2).sum().backward()
     # DDP averages over ranks: mean of the two shard gradients
     for g in out.values():
-        torch.testing.assert_close(g, ref.weight.grad / 2, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(torch.tensor(g), ref.weight.grad / 2, rtol=1e-5, atol=1e-6)
