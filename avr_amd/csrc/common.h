@@ -43,6 +43,80 @@ __device__ __forceinline__ void store_f(__hip_bfloat16* p, int64_t i, float v) {
 __device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
 
+// 16-byte vectors of signal elements as floats: 4 x fp32 or 8 x fp16/bf16.
+// load() is non-temporal (the signal is streamed once per pass and should
+// not evict the tables and partials from L2/MALL); store() is a plain
+// 16-byte store.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <typename T>
+struct Vec16;
+template <>
+struct Vec16<float> {
+    static constexpr int N = 4;
+    using raw = f32x4;
+    __device__ static void cvt(const raw& v, float* o) {
+        o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
+    }
+    __device__ static raw pack(const float* o) { return raw{o[0], o[1], o[2], o[3]}; }
+};
+template <>
+struct Vec16<__half> {
+    static constexpr int N = 8;
+    using raw = u32x4;
+    __device__ static void cvt(const raw& v, float* o) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t u = v[i];
+            const float2 f = __half22float2(*reinterpret_cast<const __half2*>(&u));
+            o[2 * i] = f.x;
+            o[2 * i + 1] = f.y;
+        }
+    }
+    __device__ static raw pack(const float* o) {
+        raw v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const __half2 h = __floats2half2_rn(o[2 * i], o[2 * i + 1]);
+            v[i] = *reinterpret_cast<const uint32_t*>(&h);
+        }
+        return v;
+    }
+};
+template <>
+struct Vec16<__hip_bfloat16> {
+    static constexpr int N = 8;
+    using raw = u32x4;
+    __device__ static void cvt(const raw& v, float* o) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            o[2 * i] = bf16_lo(v[i]);
+            o[2 * i + 1] = bf16_hi(v[i]);
+        }
+    }
+    __device__ static raw pack(const float* o) {
+        raw v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const __hip_bfloat16 a = __float2bfloat16(o[2 * i]);
+            const __hip_bfloat16 b = __float2bfloat16(o[2 * i + 1]);
+            v[i] = (uint32_t)(*reinterpret_cast<const uint16_t*>(&a)) |
+                   ((uint32_t)(*reinterpret_cast<const uint16_t*>(&b)) << 16);
+        }
+        return v;
+    }
+};
+template <typename T>
+__device__ __forceinline__ void load16_nt(const T* p, float* o) {
+    using V = Vec16<T>;
+    V::cvt(__builtin_nontemporal_load(reinterpret_cast<const typename V::raw*>(p)), o);
+}
+template <typename T>
+__device__ __forceinline__ void store16(T* p, const float* o) {
+    using V = Vec16<T>;
+    *reinterpret_cast<typename V::raw*>(p) = V::pack(o);
+}
+
 // ---------------------------------------------------------------- geometry
 // torch.linspace(a, b, n)[i] on CPU: step = (b-a)/(n-1) in fp32, lower half
 // a + step*i, upper half b - step*(n-1-i), each a single fused rounding.

@@ -26,9 +26,9 @@ constexpr int kBwdThreads = 256;
 constexpr int kFc = 32;  // bins per LDS stage
 
 __global__ __launch_bounds__(kBwdThreads) void dft_phase_bwd_kernel(
-    const float2* __restrict__ gout, const float* __restrict__ pl,
-    const int32_t* __restrict__ shift, const float2* __restrict__ phase,
-    const float2* __restrict__ twg, float* __restrict__ gz, int B, int S, int T) {
+    avr_render_params pp, const float2* __restrict__ gout, const float* __restrict__ pl,
+    const float2* __restrict__ phase, const float2* __restrict__ twg, float* __restrict__ gz, int B,
+    int S, int T) {
     extern __shared__ float2 tw[];         // [T]  (cos, -sin)
     __shared__ float Au[16][kFc + 1];      // U
     __shared__ float Av[16][kFc + 1];      // -V  (pairs with the -sin table entry)
@@ -40,25 +40,36 @@ __global__ __launch_bounds__(kBwdThreads) void dft_phase_bwd_kernel(
     const int tm = (t < T) ? t : 0;
     const int kq = lane >> 4;            // 0..3
     const int fo = kq >> 1, comp = kq & 1;
+    // staging: thread -> (row = tid / 16, cols 2*(tid % 16) + {0,1}) of the 16 x 32 tile
+    const int srow = threadIdx.x >> 4, scol = 2 * (threadIdx.x & 15);
+    const int ss = min(s0 + srow, S - 1);
+    float2 ph_raw[2], g_raw[2];
+    auto issue = [&](int fc) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int f = min(fc + scol + q, F - 1);
+            g_raw[q] = gout[(int64_t)b * F + f];
+            ph_raw[q] = phase[(int64_t)ss * F + f];
+        }
+    };
+    auto commit = [&](int fc) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const bool ok = (s0 + srow) < S && (fc + scol + q) < F;
+            const float2 g = g_raw[q], ph = ph_raw[q];
+            Au[srow][scol + q] = ok ? g.x * ph.x + g.y * ph.y : 0.0f;
+            Av[srow][scol + q] = ok ? -(g.x * ph.y - g.y * ph.x) : 0.0f;
+        }
+    };
+    issue(0);
     stage_table<kBwdThreads>(tw, twg, T);
     floatx4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     const int inc = (int)((2LL * tm) % T);
     for (int fc = 0; fc < F; fc += kFc) {
         __syncthreads();
-        for (int e = threadIdx.x; e < 16 * kFc; e += kBwdThreads) {
-            const int row = e / kFc, col = e % kFc;
-            const int s = s0 + row, f = fc + col;
-            float u = 0.0f, nv = 0.0f;
-            if (s < S && f < F) {
-                const float2 g = gout[(int64_t)b * F + f];
-                const float2 ph = phase[(int64_t)s * F + f];
-                u = g.x * ph.x + g.y * ph.y;
-                nv = -(g.x * ph.y - g.y * ph.x);
-            }
-            Au[row][col] = u;
-            Av[row][col] = nv;
-        }
+        commit(fc);
         __syncthreads();
+        if (fc + kFc < F) issue(fc + kFc);  // next tile's loads fly under the MFMAs
         int idx = (int)(((int64_t)(fc + fo) * tm) % T);
 #pragma unroll 4
         for (int ff = 0; ff < kFc; ff += 2) {
@@ -71,14 +82,24 @@ __global__ __launch_bounds__(kBwdThreads) void dft_phase_bwd_kernel(
             if (idx >= T) idx -= T;
         }
     }
-    // C layout: col t = lane&15, rows s = 4*(lane>>4) + reg
+    // C layout: col t = lane&15, rows s = 4*(lane>>4) + reg.  shift[s]
+    // recomputed (renderer.py:79-80, identical to the table); the 4
+    // path-loss gathers are issued together.
+    float g4[4];
+    int sh4[4];
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+        const int s = min(s0 + 4 * kq + reg, S - 1);
+        const float d = linspace_at(0.0f, 1.0f, S, s) * pp.depth_scale + pp.depth_offset;
+        sh4[reg] = (int)rintf((pp.fs * d) / pp.speed);
+        g4[reg] = pl[sh4[reg] + min(tm, T - 1)];
+    }
     if (t < T) {
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) {
             const int s = s0 + 4 * kq + reg;
             if (s < S) {
-                const int sh = shift[s];
-                const float v = (t < T - 1 - sh) ? acc[reg] * pl[sh + t] : 0.0f;
+                const float v = (t < T - 1 - sh4[reg]) ? acc[reg] * g4[reg] : 0.0f;
                 gz[((int64_t)b * S + s) * T + t] = v;
             }
         }
@@ -86,73 +107,6 @@ __global__ __launch_bounds__(kBwdThreads) void dft_phase_bwd_kernel(
 }
 
 // -------------------------------------------------- ray reduce backward
-// One row (b,r,s) per wavefront: the wave keeps gz[b,s,:] for its lanes'
-// t-chunks in registers and walks the rays of its split; per row it streams
-// x in, writes grad_x = w*[t>=d]*gz, and reduces grad_w with lane shuffles.
-// Boundary chunks (that straddle a neighbouring row) are stored per element.
-template <typename Tin>
-struct V16;
-template <>
-struct V16<float> {
-    static constexpr int N = 4;
-    using raw = float4;
-    __device__ static void load(const float* p, float* o) {
-        float4 v = *reinterpret_cast<const float4*>(p);
-        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
-    }
-    __device__ static void store(float* p, const float* o) {
-        *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
-    }
-};
-template <>
-struct V16<__half> {
-    static constexpr int N = 8;
-    __device__ static void load(const __half* p, float* o) {
-        uint4 v = *reinterpret_cast<const uint4*>(p);
-        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float2 f = __half22float2(*reinterpret_cast<const __half2*>(&u[i]));
-            o[2 * i] = f.x;
-            o[2 * i + 1] = f.y;
-        }
-    }
-    __device__ static void store(__half* p, const float* o) {
-        uint32_t u[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            __half2 h = __floats2half2_rn(o[2 * i], o[2 * i + 1]);
-            u[i] = *reinterpret_cast<uint32_t*>(&h);
-        }
-        *reinterpret_cast<uint4*>(p) = make_uint4(u[0], u[1], u[2], u[3]);
-    }
-};
-
-template <>
-struct V16<__hip_bfloat16> {
-    static constexpr int N = 8;
-    __device__ static void load(const __hip_bfloat16* p, float* o) {
-        uint4 v = *reinterpret_cast<const uint4*>(p);
-        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            o[2 * i] = bf16_lo(u[i]);
-            o[2 * i + 1] = bf16_hi(u[i]);
-        }
-    }
-    __device__ static void store(__hip_bfloat16* p, const float* o) {
-        uint32_t u[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const __hip_bfloat16 a = __float2bfloat16(o[2 * i]);
-            const __hip_bfloat16 b = __float2bfloat16(o[2 * i + 1]);
-            u[i] = (uint32_t)(*reinterpret_cast<const uint16_t*>(&a)) |
-                   ((uint32_t)(*reinterpret_cast<const uint16_t*>(&b)) << 16);
-        }
-        *reinterpret_cast<uint4*>(p) = make_uint4(u[0], u[1], u[2], u[3]);
-    }
-};
-
 constexpr int kMaxRbThreads = 1024;
 constexpr int kMaxRbRays = 4096;  // G * rays per split
 
@@ -162,13 +116,14 @@ constexpr int kMaxRbRays = 4096;  // G * rays per split
 // signal chunk once, writes grad_x = w*[t>=delay]*gz with 16-byte stores
 // (masked scalar stores only where a chunk leaves the super-row) and adds
 // its share of grad_w = sum_t [t>=delay]*gz*x, reduced per ray by a wave
-// shuffle tree and one LDS atomic per wave.
+// shuffle tree and one LDS atomic per wave.  Four rays' loads are issued
+// before any of them is consumed.
 template <typename Tin, bool VECTOR, int CPT, int G, int MAXT>
 __global__ __launch_bounds__(MAXT) void ray_reduce_bwd_kernel(
     const Tin* __restrict__ sig, const float* __restrict__ gz, const float* __restrict__ w,
     const int32_t* __restrict__ delay, Tin* __restrict__ gsig, float* __restrict__ gw, int B,
     int R, int S, int T, int rays_per_split, int64_t total) {
-    constexpr int VEC = VECTOR ? V16<Tin>::N : 1;
+    constexpr int VEC = VECTOR ? Vec16<Tin>::N : 1;
     extern __shared__ float lds_rb[];  // w_l[G][nr], d_l[G][nr], dot_l[G][nr]
     const int nthreads = blockDim.x, lane = threadIdx.x & 63;
     const int split = blockIdx.x, s0 = blockIdx.y * G, b = blockIdx.z;
@@ -220,13 +175,16 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_bwd_kernel(
 
     auto load_chunk = [&](int64_t rowbase, int c, float* x) {
         const int j = threadIdx.x + c * nthreads;
-        const int64_t e0 = rowbase + (int64_t)j * VEC;
-        if (VECTOR && j < nchunks && e0 + VEC <= total) {
-            if constexpr (VECTOR) V16<Tin>::load(sig + e0, x);
-            return;
+        if constexpr (VECTOR) {
+            // S*T % VEC == 0 (host check) and rowbase is VEC-aligned, so a
+            // chunk of the super-row never crosses the end of the tensor;
+            // lanes past the last chunk re-read it (their slots have tk < 0)
+            // instead of branching, keeping the loads of all rays in flight.
+            load16_nt(sig + rowbase + (int64_t)min(j, nchunks - 1) * VEC, x);
+        } else {
+            const int64_t e0 = rowbase + j;
+            x[0] = (j < nchunks && e0 < total) ? load_f(sig, e0) : 0.0f;
         }
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) x[k] = (j < nchunks && e0 + k < total) ? load_f(sig, e0 + k) : 0.0f;
     };
     auto finish = [&](int r, int64_t rowbase, float (*x)[VEC]) {
         float wg[G], dotg[G];
@@ -261,7 +219,7 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_bwd_kernel(
             const int j = threadIdx.x + c * nthreads;
             const int64_t e0 = rowbase + (int64_t)j * VEC;
             if (VECTOR && full[c]) {
-                if constexpr (VECTOR) V16<Tin>::store(gsig + e0, o);
+                if constexpr (VECTOR) store16(gsig + e0, o);
             } else {
 #pragma unroll
                 for (int k = 0; k < VEC; ++k)
@@ -277,17 +235,18 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_bwd_kernel(
         }
     };
 
+    constexpr int U = 4;  // rays in flight per lane
     int r = 0;
-    for (; r + 2 <= nr; r += 2) {
-        float xa[CPT][VEC], xb[CPT][VEC];
-        const int64_t ba = row0 + (int64_t)r * row_stride - phase;
-        const int64_t bb = ba + row_stride;
+    for (; r + U <= nr; r += U) {
+        float x[U][CPT][VEC];
 #pragma unroll
-        for (int c = 0; c < CPT; ++c) load_chunk(ba, c, xa[c]);
+        for (int u = 0; u < U; ++u) {
+            const int64_t bu = row0 + (int64_t)(r + u) * row_stride - phase;
 #pragma unroll
-        for (int c = 0; c < CPT; ++c) load_chunk(bb, c, xb[c]);
-        finish(r, ba, xa);
-        finish(r + 1, bb, xb);
+            for (int c = 0; c < CPT; ++c) load_chunk(bu, c, x[u][c]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) finish(r + u, row0 + (int64_t)(r + u) * row_stride - phase, x[u]);
     }
     for (; r < nr; ++r) {
         float xa[CPT][VEC];
@@ -402,8 +361,12 @@ extern "C" int avr_dft_phase_bwd(const avr_render_params* p, int32_t B, const fl
     AVR_REQUIRE(T >= 2 && T <= 16384, "avr_dft_phase_bwd: T out of range");
     const dim3 grid((T + 63) / 64, (S + 15) / 16, B);
     const size_t lds = (size_t)T * sizeof(float2);
-    hipLaunchKernelGGL(dft_phase_bwd_kernel, grid, dim3(kBwdThreads), lds, as_stream(stream),
-                       reinterpret_cast<const float2*>(grad_out), pl_table, shift,
+    (void)shift;
+    if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)dft_phase_bwd_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(dft_phase_bwd_kernel, grid, dim3(kBwdThreads), lds, as_stream(stream), *p,
+                       reinterpret_cast<const float2*>(grad_out), pl_table,
                        reinterpret_cast<const float2*>(phase),
                        reinterpret_cast<const float2*>(twiddle), gz, (int)B, S, T);
     return check_launch("avr_dft_phase_bwd");
@@ -413,7 +376,7 @@ namespace {
 template <typename Tin, bool VECTOR>
 int launch_rb(const avr_render_params* p, int B, const void* sig, const float* gz, const float* w,
               const int32_t* delay, void* gsig, float* gw, hipStream_t st) {
-    constexpr int VEC = VECTOR ? V16<Tin>::N : 1;
+    constexpr int VEC = VECTOR ? Vec16<Tin>::N : 1;
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
     // same super-row shape rule as the forward reduction
     int G = 1;

@@ -289,47 +289,6 @@ __global__ __launch_bounds__(256) void weights_fwd_kernel(
 // row of one (b,s) column has the same alignment phase, so a lane's register
 // accumulators always see the same t indices.  The per-ray w/delay of the
 // split are gathered into LDS once.
-template <typename Tin>
-struct Vec16;
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-template <>
-struct Vec16<float> {
-    static constexpr int N = 4;
-    using raw = f32x4;
-    __device__ static void cvt(const raw& v, float* o) {
-        o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
-    }
-};
-template <>
-struct Vec16<__half> {
-    static constexpr int N = 8;
-    using raw = u32x4;
-    __device__ static void cvt(const raw& v, float* o) {
-        const uint32_t u[4] = {v[0], v[1], v[2], v[3]};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            __half2 h = *reinterpret_cast<const __half2*>(&u[i]);
-            float2 f = __half22float2(h);
-            o[2 * i] = f.x;
-            o[2 * i + 1] = f.y;
-        }
-    }
-};
-
-template <>
-struct Vec16<__hip_bfloat16> {
-    static constexpr int N = 8;
-    using raw = u32x4;
-    __device__ static void cvt(const raw& v, float* o) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            o[2 * i] = bf16_lo(v[i]);
-            o[2 * i + 1] = bf16_hi(v[i]);
-        }
-    }
-};
-
 constexpr int kMaxReduceThreads = 1024;
 constexpr int kMaxGroupRays = 4096;  // G * rays_per_split (LDS: 32 KiB of w/delay)
 
@@ -389,26 +348,22 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_fwd_kernel(
 
     auto load_chunk = [&](int64_t rowbase, int c, float* x) {
         const int j = threadIdx.x + c * nthreads;
-        if (j >= nchunks) {
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) x[k] = 0.0f;
-            return;
-        }
-        const int64_t e0 = rowbase + (int64_t)j * VEC;  // first element of the chunk
         if constexpr (VECTOR) {
-            if (e0 + VEC <= total) {
-                const auto* vp = reinterpret_cast<const typename Vec16<Tin>::raw*>(sig + e0);
-                typename Vec16<Tin>::raw v;
-                if constexpr (NT)
-                    v = __builtin_nontemporal_load(vp);
-                else
-                    v = *vp;
-                Vec16<Tin>::cvt(v, x);
-                return;
-            }
+            // S*T % VEC == 0 (host check) and rowbase is VEC-aligned: no chunk
+            // crosses the end of the tensor.  Lanes past the last chunk re-read
+            // it (their slots have tk < 0, weight 0) rather than branch.
+            const auto* vp = reinterpret_cast<const typename Vec16<Tin>::raw*>(
+                sig + rowbase + (int64_t)min(j, nchunks - 1) * VEC);
+            typename Vec16<Tin>::raw v;
+            if constexpr (NT)
+                v = __builtin_nontemporal_load(vp);
+            else
+                v = *vp;
+            Vec16<Tin>::cvt(v, x);
+        } else {
+            const int64_t e0 = rowbase + j;
+            x[0] = (j < nchunks && e0 < total) ? load_f(sig, e0) : 0.0f;
         }
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) x[k] = (e0 + k < total) ? load_f(sig, e0 + k) : 0.0f;
     };
     auto accumulate = [&](int r, float (*x)[VEC]) {
         float wg[G];

@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mlp-dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--core-only", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     w = WORKLOADS[args.workload]
@@ -82,6 +83,9 @@ def main():
     alg = w.ray_samples * (3 * T * 4 + 4 * 4)
     res["render_core_alg_GBps"] = alg / t / 1e9
     del attn, sig, rc
+    if args.core_only:
+        print(json.dumps(res))
+        return
 
     # full training step
     mlp_dtype = torch.bfloat16 if args.mlp_dtype == "bf16" else torch.float32
