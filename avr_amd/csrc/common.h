@@ -45,8 +45,8 @@ __device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u 
 
 // 16-byte vectors of signal elements as floats: 4 x fp32 or 8 x fp16/bf16.
 // load() is non-temporal (the signal is streamed once per pass and should
-// not evict the tables and partials from L2/MALL); store() is a plain
-// 16-byte store.
+// not evict the tables and partials from L2/MALL); store16() is a plain
+// 16-byte store, store16_nt() a streaming one.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <typename T>
@@ -115,6 +115,11 @@ template <typename T>
 __device__ __forceinline__ void store16(T* p, const float* o) {
     using V = Vec16<T>;
     *reinterpret_cast<typename V::raw*>(p) = V::pack(o);
+}
+template <typename T>
+__device__ __forceinline__ void store16_nt(T* p, const float* o) {
+    using V = Vec16<T>;
+    __builtin_nontemporal_store(V::pack(o), reinterpret_cast<typename V::raw*>(p));
 }
 
 // ---------------------------------------------------------------- geometry

@@ -118,7 +118,7 @@ constexpr int kMaxRbRays = 4096;  // G * rays per split
 // its share of grad_w = sum_t [t>=delay]*gz*x, reduced per ray by a wave
 // shuffle tree and one LDS atomic per wave.  Four rays' loads are issued
 // before any of them is consumed.
-template <typename Tin, bool VECTOR, int CPT, int G, int MAXT>
+template <typename Tin, bool VECTOR, int CPT, int G, int MAXT, bool NTS>
 __global__ __launch_bounds__(MAXT) void ray_reduce_bwd_kernel(
     const Tin* __restrict__ sig, const float* __restrict__ gz, const float* __restrict__ w,
     const int32_t* __restrict__ delay, Tin* __restrict__ gsig, float* __restrict__ gw, int B,
@@ -219,7 +219,12 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_bwd_kernel(
             const int j = threadIdx.x + c * nthreads;
             const int64_t e0 = rowbase + (int64_t)j * VEC;
             if (VECTOR && full[c]) {
-                if constexpr (VECTOR) store16(gsig + e0, o);
+                if constexpr (VECTOR) {
+                    if constexpr (NTS)
+                        store16_nt(gsig + e0, o);
+                    else
+                        store16(gsig + e0, o);
+                }
             } else {
 #pragma unroll
                 for (int k = 0; k < VEC; ++k)
@@ -390,11 +395,15 @@ int launch_rb(const avr_render_params* p, int B, const void* sig, const float* g
     while ((nch + cpt - 1) / cpt > kMaxRbThreads) ++cpt;
     const int threads = max(64, ((nch + cpt - 1) / cpt + 63) / 64 * 64);
     const int groups = (S + G - 1) / G;
-    // ~8 resident waves per CU, rays per split within the LDS slab
+    // rays per split within the LDS slab, at least 4 per split
     int n = 1;
     const int64_t wps = (int64_t)groups * B * (threads / 64);
+    // no partials in the backward, so splits cost only a gz re-read from L2:
+    // take many (best at the 256-split cap, profiles/r01_tune_bwd_*.jsonl)
+    int64_t waves_target = 262144;
+    if (const char* e = getenv("AVR_RB_WAVES")) waves_target = atoll(e);  // tuning override
     auto rps_of = [&](int k) { return (R + k - 1) / k; };
-    while (n < 64 && (n * wps < 2048 || rps_of(n) * G > kMaxRbRays) && rps_of(2 * n) >= 4) n *= 2;
+    while (n < 256 && (n * wps < waves_target || rps_of(n) * G > kMaxRbRays) && rps_of(2 * n) >= 4) n *= 2;
     const int rps = rps_of(n);
     if (rps * G > kMaxRbRays) return fail(AVR_E_CONFIG, "ray_reduce_bwd: too many rays per split");
     const int64_t total = (int64_t)B * R * S * T;
@@ -402,19 +411,29 @@ int launch_rb(const avr_render_params* p, int B, const void* sig, const float* g
     const size_t lds = (size_t)3 * G * max(rps, 1) * 4;
     const Tin* x = (const Tin*)sig;
     Tin* gx = (Tin*)gsig;
+    const char* nts_env = getenv("AVR_RB_NTS");  // tuning override: 0 = plain stores
+    const bool nts = !(nts_env && atoi(nts_env) == 0);
+#define AVR_RB_L(C, GG, MT, NTS)                                                                   \
+    hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, C, GG, MT, NTS>), grid, dim3(threads),  \
+                       lds, st, x, gz, w, delay, gx, gw, B, R, S, T, rps, total)
 #define AVR_RB(C, GG)                                                                              \
     if (cpt == C && G == GG) {                                                                     \
-        if (threads <= 512)                                                                        \
-            hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, C, GG, 512>), grid, dim3(threads), \
-                               lds, st, x, gz, w, delay, gx, gw, B, R, S, T, rps, total);          \
-        else                                                                                       \
-            hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, C, GG, 1024>), grid,            \
-                               dim3(threads), lds, st, x, gz, w, delay, gx, gw, B, R, S, T, rps,   \
-                               total);                                                             \
+        if (threads <= 512) {                                                                      \
+            if (nts)                                                                               \
+                AVR_RB_L(C, GG, 512, true);                                                        \
+            else                                                                                   \
+                AVR_RB_L(C, GG, 512, false);                                                       \
+        } else {                                                                                   \
+            if (nts)                                                                               \
+                AVR_RB_L(C, GG, 1024, true);                                                       \
+            else                                                                                   \
+                AVR_RB_L(C, GG, 1024, false);                                                      \
+        }                                                                                          \
         return check_launch("avr_ray_reduce_bwd");                                                 \
     }
     AVR_RB(1, 1) AVR_RB(1, 2) AVR_RB(1, 4) AVR_RB(2, 1) AVR_RB(2, 2) AVR_RB(2, 4) AVR_RB(3, 1)
     AVR_RB(4, 1)
+#undef AVR_RB_L
 #undef AVR_RB
     return fail(AVR_E_CONFIG, "ray_reduce_bwd: T too long for this build");
 }

@@ -39,6 +39,7 @@ for s in "$@"; do
     gexp) step g1 200 python tools/tune.py --variants u4nt --nsplit 2,4 --ksplit 8 --rounds 3 \
           && AVR_REDUCE_G=2 step g2 200 python tools/tune.py --variants u4nt --nsplit 1,2,4 --ksplit 8 --rounds 3 \
           && AVR_REDUCE_G=4 step g4 200 python tools/tune.py --variants u4nt --nsplit 1,2 --ksplit 8 --rounds 3 ;;
+    tunebwd) step tunebwd 600 python tools/tune_bwd.py $TUNE_ARGS && step tunebwd2 600 python tools/tune_bwd.py --workload c2_meshrir_1024x256x512 $TUNE_ARGS && step tunebwd5 600 python tools/tune_bwd.py --workload c5_simu_4096x512x2048 $TUNE_ARGS ;;
     profcore) step profcore 600 rocprofv3 --kernel-trace --stats -d $OUT/profcore -o run --output-format csv -- python tools/bench_train.py --core-only --steps 20 ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 50 --warmup 5 --streams 1 ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 3 --streams 1 && step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 3 --streams 1 ;;
