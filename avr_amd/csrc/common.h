@@ -111,6 +111,22 @@ __device__ __forceinline__ void load16_nt(const T* p, float* o) {
     using V = Vec16<T>;
     V::cvt(__builtin_nontemporal_load(reinterpret_cast<const typename V::raw*>(p)), o);
 }
+// Streaming 16-byte load through a buffer resource whose base is the current
+// (wave-uniform) row: a lane whose byte offset is >= nbytes gets zeros and
+// issues no memory traffic.  That masks chunks without control flow, so all
+// loads of an unrolled batch stay in flight together.
+constexpr uint32_t kSkip = 0x80000000u;  // byte offset of a masked lane
+template <typename T>
+__device__ __forceinline__ void load16_masked(const T* row, uint32_t nbytes, uint32_t off,
+                                              float* o) {
+    using V = Vec16<T>;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)row, (short)0, (int)nbytes, 0x00020000);
+    // aux = 2: non-temporal (gfx94x/gfx950 "nt")
+    V::cvt(__builtin_bit_cast(typename V::raw,
+                              __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)off, 0, 2)),
+           o);
+}
 template <typename T>
 __device__ __forceinline__ void store16(T* p, const float* o) {
     using V = Vec16<T>;
@@ -187,6 +203,19 @@ __device__ __forceinline__ void stage_table(float2* __restrict__ dst, const floa
             if (j < n) dst[j] = v[i];
         }
     }
+}
+// receiver-side depth and integer delay of sample s (renderer.py:64-70):
+// d = linspace(0,1,S)[s]*(far-near)+near, shift = round(fs*d/speed).
+// Every kernel recomputes it with the same op sequence as tables_kernel.
+__device__ __forceinline__ float depth_at(const avr_render_params& p, int s) {
+    return linspace_at(0.0f, 1.0f, p.n_samples, s) * p.depth_scale + p.depth_offset;
+}
+__device__ __forceinline__ int receiver_shift(const avr_render_params& p, int s) {
+    return (int)rintf((p.fs * depth_at(p, s)) / p.speed);
+}
+// last+1 sample time kept by the tail mask (renderer.py:72): t < T-1-shift
+__device__ __forceinline__ int tail_limit(const avr_render_params& p, int s) {
+    return p.T - 1 - receiver_shift(p, s);
 }
 // all rays of the sphere (ray generation)
 __host__ __device__ inline int grid_rays(const avr_render_params& p) { return p.n_azi * p.n_ele + 2; }

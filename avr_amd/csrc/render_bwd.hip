@@ -90,8 +90,7 @@ __global__ __launch_bounds__(kBwdThreads) void dft_phase_bwd_kernel(
 #pragma unroll
     for (int reg = 0; reg < 4; ++reg) {
         const int s = min(s0 + 4 * kq + reg, S - 1);
-        const float d = linspace_at(0.0f, 1.0f, S, s) * pp.depth_scale + pp.depth_offset;
-        sh4[reg] = (int)rintf((pp.fs * d) / pp.speed);
+        sh4[reg] = receiver_shift(pp, s);
         g4[reg] = pl[sh4[reg] + min(tm, T - 1)];
     }
     if (t < T) {
@@ -120,7 +119,7 @@ constexpr int kMaxRbRays = 4096;  // G * rays per split
 // before any of them is consumed.
 template <typename Tin, bool VECTOR, int CPT, int G, int MAXT, bool NTS>
 __global__ __launch_bounds__(MAXT) void ray_reduce_bwd_kernel(
-    const Tin* __restrict__ sig, const float* __restrict__ gz, const float* __restrict__ w,
+    avr_render_params pp, const Tin* __restrict__ sig, const float* __restrict__ gz, const float* __restrict__ w,
     const int32_t* __restrict__ delay, Tin* __restrict__ gsig, float* __restrict__ gw, int B,
     int R, int S, int T, int rays_per_split, int64_t total) {
     constexpr int VEC = VECTOR ? Vec16<Tin>::N : 1;
@@ -153,14 +152,22 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_bwd_kernel(
     const int64_t row_stride = (int64_t)S * T;
 
     float gv[CPT][VEC];
-    int tk[CPT][VEC], gk[CPT][VEC];
+    int tk[CPT][VEC];  // t of each slot (-1: outside the super-row)
+    int tm[CPT][VEC];  // t if inside the tail window t < T-1-shift[s], else -1
+    int gk[CPT][VEC];
+    int tmax[CPT][G];  // per chunk and column: largest tm (-1: no live slot)
+    int lim[G];
     bool full[CPT];  // chunk lies inside the super-row: vector store allowed
     const float* gzc = gz + ((int64_t)b * S + s0) * T;  // gz rows of the group are contiguous
+#pragma unroll
+    for (int g = 0; g < G; ++g) lim[g] = tail_limit(pp, min(s0 + g, S - 1));
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
         const int j = threadIdx.x + c * nthreads;
         const int ebase = j * VEC - phase;
         full[c] = j < nchunks && ebase >= 0 && ebase + VEC <= L;
+#pragma unroll
+        for (int g = 0; g < G; ++g) tmax[c][g] = -1;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const int e = ebase + k;
@@ -169,21 +176,36 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_bwd_kernel(
             gk[c][k] = g;
             tk[c][k] = ok ? e - g * T : -1;
             gv[c][k] = ok ? gzc[e] : 0.0f;
+            int l = lim[0];
+#pragma unroll
+            for (int q = 1; q < G; ++q)
+                if (g == q) l = lim[q];
+            tm[c][k] = (tk[c][k] >= 0 && tk[c][k] < l) ? tk[c][k] : -1;
+#pragma unroll
+            for (int q = 0; q < G; ++q)
+                if (g == q) tmax[c][q] = max(tmax[c][q], tm[c][k]);
         }
     }
     __syncthreads();
 
-    auto load_chunk = [&](int64_t rowbase, int c, float* x) {
+    // chunk c of ray r is live if any slot t satisfies delay <= t < T-1-shift;
+    // a dead chunk's signal is not needed (its grad_x is 0, its grad_w term 0)
+    auto live = [&](int r, int c) {
+        bool any = false;
+#pragma unroll
+        for (int g = 0; g < G; ++g) any |= tmax[c][g] >= d_l[g * nr + r];
+        return any;
+    };
+    auto load_chunk = [&](int64_t rowbase, int c, bool need, float* x) {
         const int j = threadIdx.x + c * nthreads;
         if constexpr (VECTOR) {
-            // S*T % VEC == 0 (host check) and rowbase is VEC-aligned, so a
-            // chunk of the super-row never crosses the end of the tensor;
-            // lanes past the last chunk re-read it (their slots have tk < 0)
-            // instead of branching, keeping the loads of all rays in flight.
-            load16_nt(sig + rowbase + (int64_t)min(j, nchunks - 1) * VEC, x);
+            // S*T % VEC == 0 (host check), rowbase VEC-aligned: chunks lie
+            // inside the tensor; dead chunks / spare lanes read zeros for free
+            load16_masked(sig + rowbase, (uint32_t)nchunks * 16u,
+                          need ? (uint32_t)j * 16u : kSkip, x);
         } else {
             const int64_t e0 = rowbase + j;
-            x[0] = (j < nchunks && e0 < total) ? load_f(sig, e0) : 0.0f;
+            x[0] = (need && j < nchunks && e0 < total) ? load_f(sig, e0) : 0.0f;
         }
     };
     auto finish = [&](int r, int64_t rowbase, float (*x)[VEC]) {
@@ -208,8 +230,7 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_bwd_kernel(
                         ws = wg[g];
                         ds = dg[g];
                     }
-                const int t = tk[c][k];
-                const float gm = (t >= 0 && t >= ds) ? gv[c][k] : 0.0f;
+                const float gm = (tm[c][k] >= ds) ? gv[c][k] : 0.0f;
                 o[k] = ws * gm;
                 const float pd = gm * x[c][k];
 #pragma unroll
@@ -244,11 +265,16 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_bwd_kernel(
     int r = 0;
     for (; r + U <= nr; r += U) {
         float x[U][CPT][VEC];
+        bool need[U][CPT];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < CPT; ++c) need[u][c] = live(r + u, c);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t bu = row0 + (int64_t)(r + u) * row_stride - phase;
 #pragma unroll
-            for (int c = 0; c < CPT; ++c) load_chunk(bu, c, x[u][c]);
+            for (int c = 0; c < CPT; ++c) load_chunk(bu, c, need[u][c], x[u][c]);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) finish(r + u, row0 + (int64_t)(r + u) * row_stride - phase, x[u]);
@@ -257,7 +283,7 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_bwd_kernel(
         float xa[CPT][VEC];
         const int64_t ba = row0 + (int64_t)r * row_stride - phase;
 #pragma unroll
-        for (int c = 0; c < CPT; ++c) load_chunk(ba, c, xa[c]);
+        for (int c = 0; c < CPT; ++c) load_chunk(ba, c, live(r, c), xa[c]);
         finish(r, ba, xa);
     }
     __syncthreads();
@@ -415,7 +441,7 @@ int launch_rb(const avr_render_params* p, int B, const void* sig, const float* g
     const bool nts = !(nts_env && atoi(nts_env) == 0);
 #define AVR_RB_L(C, GG, MT, NTS)                                                                   \
     hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, C, GG, MT, NTS>), grid, dim3(threads),  \
-                       lds, st, x, gz, w, delay, gx, gw, B, R, S, T, rps, total)
+                       lds, st, *p, x, gz, w, delay, gx, gw, B, R, S, T, rps, total)
 #define AVR_RB(C, GG)                                                                              \
     if (cpt == C && G == GG) {                                                                     \
         if (threads <= 512) {                                                                      \

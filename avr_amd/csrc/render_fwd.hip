@@ -283,12 +283,16 @@ __global__ __launch_bounds__(256) void weights_fwd_kernel(
 }
 
 // --------------------------------------------- the HBM stream: ray reduce
-// part[k][b][s][t] = sum_{r in split k} w[b,r,s] * [t >= delay[b,r,s]] * x[b,r,s,t]
-// One workgroup per (split, s, b); each row (b,r,s) of T contiguous elements
-// is read once with 16-byte loads.  Because S*T is a multiple of VEC, every
-// row of one (b,s) column has the same alignment phase, so a lane's register
-// accumulators always see the same t indices.  The per-ray w/delay of the
-// split are gathered into LDS once.
+// part[k][b][s][t] = sum_{r in split k} w[b,r,s] * [delay[b,r,s] <= t < T-1-shift[s]] * x[b,r,s,t]
+// i.e. both masks of renderer.py:72-78 (the tail mask is applied again,
+// redundantly, by the DFT stage).  Each row (b,r,s) of T contiguous elements
+// is read at most once with 16-byte loads, and only its LIVE window
+// [delay, T-1-shift) is read at all: a 16-byte chunk whose slots are all
+// masked is never loaded (its product with the mask is zero for any finite
+// signal).  Because S*T is a multiple of VEC, every row of one (b,s) column
+// has the same alignment phase, so a lane's register accumulators always see
+// the same t indices.  The per-ray w/delay of the split are gathered into
+// LDS once.
 constexpr int kMaxReduceThreads = 1024;
 constexpr int kMaxGroupRays = 4096;  // G * rays_per_split (LDS: 32 KiB of w/delay)
 
@@ -299,10 +303,11 @@ constexpr int kMaxGroupRays = 4096;  // G * rays_per_split (LDS: 32 KiB of w/del
 // chosen so a super-row is ~256*VEC elements (short rows: fp16 or small T);
 // the block size is chosen so every lane owns CPT chunks of it.  Lane slots
 // have fixed (g, t) coordinates, so the accumulators need no shuffling.
-template <typename Tin, bool VECTOR, int CPT, int kUnroll, bool NT, int G, int MAXT>
+template <typename Tin, bool VECTOR, int CPT, int kUnroll, int G, int MAXT>
 __global__ __launch_bounds__(MAXT) void ray_reduce_fwd_kernel(
-    const Tin* __restrict__ sig, const float* __restrict__ w, const int32_t* __restrict__ delay,
-    float* __restrict__ part, int B, int R, int S, int T, int rays_per_split, int64_t total) {
+    avr_render_params pp, const Tin* __restrict__ sig, const float* __restrict__ w,
+    const int32_t* __restrict__ delay, float* __restrict__ part, int B, int R, int S, int T,
+    int rays_per_split, int64_t total) {
     constexpr int VEC = VECTOR ? Vec16<Tin>::N : 1;
     extern __shared__ float lds_wd[];  // w_l[G][nr], then d_l[G][nr]
     const int nthreads = blockDim.x;
@@ -333,9 +338,16 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_fwd_kernel(
 
     float acc[CPT][VEC];
     int tk[CPT][VEC];  // t of each slot (-1: outside the super-row)
+    int tm[CPT][VEC];  // t if inside the tail window t < T-1-shift[s], else -1
     int gk[CPT][VEC];  // column of each slot within the group
+    int tmax[CPT][G];  // per chunk and column: largest tm (-1: no live slot)
+    int lim[G];
 #pragma unroll
-    for (int c = 0; c < CPT; ++c)
+    for (int g = 0; g < G; ++g) lim[g] = tail_limit(pp, min(s0 + g, S - 1));
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) tmax[c][g] = -1;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             acc[c][k] = 0.0f;
@@ -344,25 +356,35 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_fwd_kernel(
             const int g = (G == 1) ? 0 : (ok ? e / T : 0);
             gk[c][k] = g;
             tk[c][k] = ok ? e - g * T : -1;
+            int l = lim[0];
+#pragma unroll
+            for (int q = 1; q < G; ++q)
+                if (g == q) l = lim[q];
+            tm[c][k] = (tk[c][k] >= 0 && tk[c][k] < l) ? tk[c][k] : -1;
+#pragma unroll
+            for (int q = 0; q < G; ++q)
+                if (g == q) tmax[c][q] = max(tmax[c][q], tm[c][k]);
         }
+    }
 
-    auto load_chunk = [&](int64_t rowbase, int c, float* x) {
+    // chunk c of ray r is live if any slot t satisfies delay <= t < T-1-shift
+    auto live = [&](int r, int c) {
+        bool any = false;
+#pragma unroll
+        for (int g = 0; g < G; ++g) any |= tmax[c][g] >= d_l[g * nr + r];
+        return any;
+    };
+    auto load_chunk = [&](int64_t rowbase, int c, bool need, float* x) {
         const int j = threadIdx.x + c * nthreads;
         if constexpr (VECTOR) {
-            // S*T % VEC == 0 (host check) and rowbase is VEC-aligned: no chunk
-            // crosses the end of the tensor.  Lanes past the last chunk re-read
-            // it (their slots have tk < 0, weight 0) rather than branch.
-            const auto* vp = reinterpret_cast<const typename Vec16<Tin>::raw*>(
-                sig + rowbase + (int64_t)min(j, nchunks - 1) * VEC);
-            typename Vec16<Tin>::raw v;
-            if constexpr (NT)
-                v = __builtin_nontemporal_load(vp);
-            else
-                v = *vp;
-            Vec16<Tin>::cvt(v, x);
+            // S*T % VEC == 0 (host check) and rowbase is VEC-aligned: the
+            // super-row's chunks lie inside the tensor.  Dead chunks and lanes
+            // past the last chunk read zeros without touching memory.
+            load16_masked(sig + rowbase, (uint32_t)nchunks * 16u,
+                          need ? (uint32_t)j * 16u : kSkip, x);
         } else {
             const int64_t e0 = rowbase + j;
-            x[0] = (j < nchunks && e0 < total) ? load_f(sig, e0) : 0.0f;
+            x[0] = (need && j < nchunks && e0 < total) ? load_f(sig, e0) : 0.0f;
         }
     };
     auto accumulate = [&](int r, float (*x)[VEC]) {
@@ -385,7 +407,7 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_fwd_kernel(
                         ws = wg[g];
                         ds = dg[g];
                     }
-                const float wm = (tk[c][k] >= ds) ? ws : 0.0f;
+                const float wm = (tm[c][k] >= ds) ? ws : 0.0f;
                 acc[c][k] = fmaf(wm, x[c][k], acc[c][k]);
             }
     };
@@ -393,11 +415,16 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_fwd_kernel(
     int r = 0;
     for (; r + kUnroll <= nr; r += kUnroll) {
         float x[kUnroll][CPT][VEC];
+        bool need[kUnroll][CPT];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+            for (int c = 0; c < CPT; ++c) need[u][c] = live(r + u, c);
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) {
             const int64_t rowbase = row0 + (int64_t)(r + u) * row_stride - phase;
 #pragma unroll
-            for (int c = 0; c < CPT; ++c) load_chunk(rowbase, c, x[u][c]);
+            for (int c = 0; c < CPT; ++c) load_chunk(rowbase, c, need[u][c], x[u][c]);
         }
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) accumulate(r + u, x[u]);
@@ -406,7 +433,7 @@ __global__ __launch_bounds__(MAXT) void ray_reduce_fwd_kernel(
         const int64_t rowbase = row0 + (int64_t)r * row_stride - phase;
         float x[CPT][VEC];
 #pragma unroll
-        for (int c = 0; c < CPT; ++c) load_chunk(rowbase, c, x[c]);
+        for (int c = 0; c < CPT; ++c) load_chunk(rowbase, c, live(r, c), x[c]);
         accumulate(r, x);
     }
 #pragma unroll
@@ -460,8 +487,7 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
     for (int i = 0; i < 8; ++i) {
         const int s = stile * 32 + row0 + 4 * i;
         srow[i] = s < S;
-        const float d = linspace_at(0.0f, 1.0f, S, min(s, S - 1)) * pp.depth_scale + pp.depth_offset;
-        sh[i] = (int)rintf((pp.fs * d) / pp.speed);
+        sh[i] = receiver_shift(pp, min(s, S - 1));
     }
     (void)shift;
     const int64_t slab = (int64_t)B * S * T;
@@ -812,27 +838,28 @@ ReduceShape reduce_shape(int S, int T) {
     return sh;
 }
 
-// Variants: rows in flight per lane (4 or 8, non-temporal loads) x launch
+// Variants: rows in flight per lane (4 or 8) x launch
 // bound (512 threads leaves 256 VGPRs per lane, 1024 only 128).
 template <typename Tin, bool VECTOR, int C, int G>
-void launch_reduce_v(dim3 grid, dim3 block, size_t lds, hipStream_t st, const Tin* s, const float* w,
+void launch_reduce_v(dim3 grid, dim3 block, size_t lds, hipStream_t st, const avr_render_params& pp,
+                     const Tin* s, const float* w,
                      const int32_t* delay, float* part, int B, int R, int S, int T, int rps,
                      int64_t total) {
     const bool u8 = reduce_variant() == 3;
     if (block.x <= 512) {
         if (u8)
-            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, true, G, 512>), grid, block,
-                               lds, st, s, w, delay, part, B, R, S, T, rps, total);
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, G, 512>), grid, block,
+                               lds, st, pp, s, w, delay, part, B, R, S, T, rps, total);
         else
-            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, true, G, 512>), grid, block,
-                               lds, st, s, w, delay, part, B, R, S, T, rps, total);
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, G, 512>), grid, block,
+                               lds, st, pp, s, w, delay, part, B, R, S, T, rps, total);
     } else {
         if (u8)
-            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, true, G, 1024>), grid, block,
-                               lds, st, s, w, delay, part, B, R, S, T, rps, total);
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 8, G, 1024>), grid, block,
+                               lds, st, pp, s, w, delay, part, B, R, S, T, rps, total);
         else
-            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, true, G, 1024>), grid, block,
-                               lds, st, s, w, delay, part, B, R, S, T, rps, total);
+            hipLaunchKernelGGL((ray_reduce_fwd_kernel<Tin, VECTOR, C, 4, G, 1024>), grid, block,
+                               lds, st, pp, s, w, delay, part, B, R, S, T, rps, total);
     }
 }
 
@@ -852,7 +879,7 @@ int launch_reduce(const avr_render_params* p, int B, const void* sig, const floa
     const Tin* s = (const Tin*)sig;
 #define AVR_RR(C, GG)                                                                              \
     if (sh.cpt == C && sh.G == GG)                                                                 \
-        return launch_reduce_v<Tin, VECTOR, C, GG>(grid, block, lds, st, s, w, delay, part, B, R, S, \
+        return launch_reduce_v<Tin, VECTOR, C, GG>(grid, block, lds, st, *p, s, w, delay, part, B, R, S, \
                                                    T, rps, total),                                 \
                check_launch("avr_ray_reduce_fwd");
     AVR_RR(1, 1) AVR_RR(1, 2) AVR_RR(1, 4) AVR_RR(2, 1) AVR_RR(2, 2) AVR_RR(2, 4) AVR_RR(3, 1)

@@ -174,7 +174,7 @@ class RenderCore(torch.autograd.Function):
         part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
         timer = KERNEL_TIMER
         if timer is not None:
-            timer.begin(dev, n_split=n_split)
+            timer.begin(dev, n_split=n_split, delay=delay, shift=tables.shift)
         _lib.call("avr_ray_reduce_fwd", pref, B, _ptr(signal), _dtype_code(signal), _ptr(w),
                   _ptr(delay), n_split, _ptr(part), st)
         if timer is not None:

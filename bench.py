@@ -42,20 +42,26 @@ class StubNet(torch.nn.Module):
 
 
 class KernelTimer:
-    """HIP events around the ray-reduction kernel on the stream it runs on."""
+    """HIP events around the ray-reduction kernel on the stream it runs on.
+
+    Also keeps each launch's delay tensor so the live window of every row,
+    [delay, T-1-shift[s]) (the only signal elements the result depends on and
+    the only ones the kernel reads), can be counted afterwards."""
 
     def __init__(self):
         self.pairs = []
+        self.rows = []
         self.n_split = None
         self.enabled = False
 
-    def begin(self, dev, n_split=None):
+    def begin(self, dev, n_split=None, delay=None, shift=None):
         if not self.enabled:
             return
         self.n_split = n_split
         e = torch.cuda.Event(enable_timing=True)
         e.record(torch.cuda.current_stream(dev))
         self.pairs.append([e, None])
+        self.rows.append((delay, shift))
 
     def end(self, dev):
         if not self.enabled:
@@ -67,6 +73,14 @@ class KernelTimer:
     def mean_ms(self):
         ts = [a.elapsed_time(b) for a, b in self.pairs if b is not None]
         return sum(ts) / len(ts) if ts else float("nan")
+
+    def mean_live_elements(self, T):
+        """Average number of live signal elements per launch."""
+        tot = 0.0
+        for delay, shift in self.rows:
+            lim = (T - 1 - shift.long()).clamp(min=0)
+            tot += float((lim.view(1, 1, -1) - delay.long()).clamp(min=0).sum())
+        return tot / max(1, len(self.rows))
 
 
 def pmc_traffic(workload, dtype_name):
@@ -135,6 +149,8 @@ def main():
     ap.add_argument("--workload", default="c2_meshrir_1024x256x512")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--poses", type=int, default=16,
+                    help="distinct synthetic poses cycled over the steps")
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the independent per-pose renders are issued on "
                          "round-robin (1 = strictly serial)")
@@ -157,17 +173,23 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
     attn = (torch.rand(B, R * S, 1, device=dev, generator=gen) * 2).to(dt)
     signal = (torch.randn(B, R * S, T, device=dev, generator=gen) * 0.1).to(dt)
-    rays_o = torch.rand(B, 3, device=dev, generator=gen) * 4 - 2
-    tx = torch.rand(B, 3, device=dev, generator=gen) * 4 - 2
-    dtx = (torch.nn.functional.normalize(torch.randn(B, 3, device=dev, generator=gen), dim=-1)
-           if w.with_dir_tx else None)
+    # a fixed set of listener/source poses, cycled: the live window of each
+    # row (and so the bytes the reduction reads) depends on the geometry
+    P = args.poses
+    rays_o = torch.rand(P, B, 3, device=dev, generator=gen) * 4 - 2
+    tx = torch.rand(P, B, 3, device=dev, generator=gen) * 4 - 2
+    dtx = (torch.nn.functional.normalize(torch.randn(P, B, 3, device=dev, generator=gen), dim=-1)
+           if w.with_dir_tx else [None] * P)
     renderer = AVRRender(StubNet(attn, signal), **w.render)
     timer = KernelTimer()
     rmod.KERNEL_TIMER = timer
+    pose = [0]
 
     def step():
+        i = pose[0] % P
+        pose[0] += 1
         with torch.no_grad():
-            out = renderer(rays_o, tx, dtx)
+            out = renderer(rays_o[i], tx[i], dtx[i])
             return spectrum_to_ir(out)
 
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
@@ -227,7 +249,12 @@ def main():
     k_ms = timer.mean_ms()
     es = 2 if dt == torch.float16 else 4
     n_split = timer.n_split or 1
-    alg_bytes = w.ray_samples * (T * es + 8) + n_split * B * S * T * 4
+    # algorithmic bytes: the live signal elements (each read once), w + delay
+    # (8 B per ray-sample), the fp32 partials written; the dense tensor is
+    # reported beside it
+    live = timer.mean_live_elements(T)
+    alg_bytes = live * es + w.ray_samples * 8 + n_split * B * S * T * 4
+    dense_bytes = w.ray_samples * (T * es + 8) + n_split * B * S * T * 4
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(w.name, "__half" if dt == torch.float16 else "float")
 
@@ -249,7 +276,7 @@ def main():
         "dtype": "f32" if dt == torch.float32 else "f16-storage/f32-math",
         "data": "synthetic (stub network, outputs resident in HBM; seeded torch RNG)",
         "config": {"workload": w.name, "rays": R, "samples": S, "T": T, "freq_bins": w.F,
-                   "poses_per_step": B, "parallelism": f"poses x{world} (no data-path collective)",
+                   "poses_per_step": B, "distinct_poses": P, "parallelism": f"poses x{world} (no data-path collective)",
                    "pipelining": f"{args.streams} HIP streams, consecutive poses round-robin"},
         "roofline": {
             "kernel": "ray_reduce_fwd_kernel",
@@ -261,6 +288,8 @@ def main():
             "traffic": traffic,
             "traffic_source": traffic_src,
             "alg_bytes_per_launch": alg_bytes,
+            "dense_bytes_per_launch": dense_bytes,
+            "live_fraction": live / (w.ray_samples * T),
             "avg_launch_ms": k_ms,
         },
     }

@@ -123,8 +123,11 @@ int avr_weights_fwd(const avr_render_params* p, int32_t B, const void* attn, int
 
 /* ---- a7-a12 (time-domain half): ray reduction --------------------------
  * part[n_split][B][S][T] = sum over the rays of split k of
- *   w[b,r,s] * [t >= delay[b,r,s]] * signal[b,r,s,t]
- * signal [B][R][S][T] (dtype).  The HBM stream of the forward pass. */
+ *   w[b,r,s] * [delay[b,r,s] <= t < T-1-shift[s]] * signal[b,r,s,t]
+ * (both masks of renderer.py:72-78; shift[s] = round(fs*d_s/speed)).
+ * signal [B][R][S][T] (dtype).  The HBM stream of the forward pass; only the
+ * live window [delay, T-1-shift) of each row is read, so non-finite values
+ * outside it do not propagate (the reference multiplies them by 0). */
 int avr_ray_reduce_fwd(const avr_render_params* p, int32_t B, const void* signal,
                        int32_t sig_dtype, const float* w, const int32_t* delay,
                        int32_t n_split, float* part, void* stream);
@@ -159,7 +162,9 @@ int avr_dft_phase_bwd(const avr_render_params* p, int32_t B, const float* grad_o
                       const float* twiddle, float* gz, void* stream);
 
 /* gz, signal, w, delay -> grad_signal[B][R][S][T] (sig dtype) and
- * grad_w[B][R][S] = sum_t [t>=delay] gz[b,s,t] * signal[b,r,s,t]. */
+ * grad_w[B][R][S] = sum_t m gz[b,s,t] * signal[b,r,s,t], where
+ * m = [delay[b,r,s] <= t < T-1-shift[s]] as in avr_ray_reduce_fwd;
+ * grad_signal = w * m * gz.  Reads only the live window of the signal. */
 int avr_ray_reduce_bwd(const avr_render_params* p, int32_t B, const void* signal,
                        int32_t sig_dtype, const float* gz, const float* w,
                        const int32_t* delay, void* grad_signal, float* grad_w, void* stream);
