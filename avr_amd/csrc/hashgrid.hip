@@ -118,17 +118,22 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(int64_t N, int L,
     store_pair(out, q, acc);
 }
 
-// Backward: scatter-add of w_corner * dL/dy into the tables.  One thread per
-// point for ONE level (blockIdx.y), so a wavefront holds 64 consecutive
-// points of one level.  Consecutive points are often identical or share a
-// cell (tx and dir_tx are constant over a pose, view over a ray, coarse
-// levels are shared by neighbouring samples), and float atomics to one
-// address serialise at the memory side (MI355X_MICROARCH.md, Global float
-// atomics, 'contention').  So each corner's contributions are first summed
-// over runs of equal table index inside the wavefront (head-flag segmented
-// scan, 6 shuffle steps) and only the last lane of each run issues the
-// atomic: a pose-constant input costs one atomic per corner per wavefront
-// instead of 64.
+// Backward: scatter-add of w_corner * dL/dy into the tables.
+//
+// Float atomics execute at the memory side and cost one request per 64-B
+// segment a wave-instruction touches (MI355X_MICROARCH.md, Global float
+// atomics: 64 lanes in 64 different rows are ~17x slower than 64 contiguous
+// dwords).  So a lane owns ONE dword: (point, corner k, feature f), 16 lanes
+// per point, lane order (k, f) with the x-corner bit next to the feature
+// bit.  The 4 dwords of an x-neighbour pair are adjacent in the table (dense
+// levels: consecutive entries; hashed levels: x enters the hash with prime 1,
+// so x and x+1 usually differ only in the low bits of the entry), so one
+// wave-instruction (4 points x 16 dwords) touches ~4 segments per point
+// instead of 16 requests per point for a lane-per-point layout.
+//
+// Points of a wave that hit the same dword (consecutive samples of a ray in
+// one coarse cell) are first summed over runs of equal addresses across the
+// 4 points (head flags at lane stride 16) and only the last one adds.
 template <typename Tg>
 __global__ __launch_bounds__(256) void hashgrid_bwd_kernel(int64_t N, int L,
                                                            const float* __restrict__ x,
@@ -136,54 +141,45 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_kernel(int64_t N, int L,
                                                            LevelTable lt,
                                                            float* __restrict__ gparams) {
     const int l = blockIdx.y;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
+    const int slot = threadIdx.x & 15;
+    const int k = slot >> 1, f = slot & 1;
+    const int64_t i = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
     const bool live = i < N;
     const int64_t ic = live ? i : N - 1;
     const float xi[3] = {x[ic * 3 + 0], x[ic * 3 + 1], x[ic * 3 + 2]};
+    const float g = live ? load_f(gout, ic * (2 * L) + 2 * l + f) : 0.0f;
     const Corner c = locate(xi, lt.scale[l]);
     const uint32_t size = (uint32_t)(lt.offset[l + 1] - lt.offset[l]);
     const uint32_t res = lt.res[l];
-    float* table = gparams + 2 * lt.offset[l];
-    float2 g = load_pair(gout, ic * L + l);
-    if (!live) g = make_float2(0.0f, 0.0f);
+    float wgt = 1.0f;
+    uint32_t gg[3];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        float wgt = 1.0f;
-        uint32_t gg[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            if (k & (1 << d)) {
-                wgt *= c.pos[d];
-                gg[d] = c.grid[d] + 1;
-            } else {
-                wgt *= 1.0f - c.pos[d];
-                gg[d] = c.grid[d];
-            }
-        }
-        const uint32_t e = grid_index(size, res, gg[0], gg[1], gg[2]);
-        float vx = wgt * g.x, vy = wgt * g.y;
-        // runs of equal e: head flags -> start lane of this lane's run
-        const uint32_t prev = __shfl_up(e, 1, 64);
-        const bool head = lane == 0 || prev != e;
-        const unsigned long long heads = __ballot(head);
-        const unsigned long long upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
-        const int start = 63 - __clzll(heads & upto);
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const float ox = __shfl_up(vx, off, 64);
-            const float oy = __shfl_up(vy, off, 64);
-            if (lane - off >= start) {
-                vx += ox;
-                vy += oy;
-            }
-        }
-        const bool tail = lane == 63 || ((heads >> (lane + 1)) & 1ull);
-        if (tail && (vx != 0.0f || vy != 0.0f)) {
-            atomicAdd(table + 2 * (int64_t)e, vx);
-            atomicAdd(table + 2 * (int64_t)e + 1, vy);
+    for (int d = 0; d < 3; ++d) {
+        if (k & (1 << d)) {
+            wgt *= c.pos[d];
+            gg[d] = c.grid[d] + 1;
+        } else {
+            wgt *= 1.0f - c.pos[d];
+            gg[d] = c.grid[d];
         }
     }
+    const uint32_t e = 2u * grid_index(size, res, gg[0], gg[1], gg[2]) + (uint32_t)f;
+    float v = wgt * g;
+    // runs of equal e over the wave's 4 points (same slot: lanes 16 apart)
+    const int p = lane >> 4;
+    const uint32_t prev = __shfl_up(e, 16, 64);
+    const bool head = p == 0 || prev != e;
+    const unsigned long long heads = __ballot(head);
+    int start = p;
+    while (!((heads >> (16 * start + slot)) & 1ull)) --start;  // <= 3 steps
+#pragma unroll
+    for (int off = 16; off < 64; off <<= 1) {
+        const float o = __shfl_up(v, off, 64);
+        if (lane - off >= 16 * start + slot) v += o;
+    }
+    const bool tail = p == 3 || ((heads >> (lane + 16)) & 1ull);
+    if (tail && v != 0.0f) atomicAdd(gparams + 2 * lt.offset[l] + e, v);
 }
 
 int make_table(int L, const int64_t* off, const float* scale, const int32_t* res, LevelTable* lt) {
@@ -240,7 +236,7 @@ extern "C" int avr_hashgrid_bwd(int64_t N, int32_t n_levels, const float* x, con
     if (N == 0) return 0;
     LevelTable lt;
     if (int e = make_table(n_levels, level_offset, level_scale, level_res, &lt)) return e;
-    const dim3 grid((unsigned)((N + 255) / 256), (unsigned)n_levels);
+    const dim3 grid((unsigned)((N + 15) / 16), (unsigned)n_levels);  // 16 lanes per point
     hipStream_t st = as_stream(stream);
     if (grad_dtype == AVR_DTYPE_F32)
         hipLaunchKernelGGL(hashgrid_bwd_kernel<float>, grid, dim3(256), 0, st, N, (int)n_levels, x,

@@ -1,0 +1,218 @@
+// Weight gradient of the networks' bias-free linear layers (a6), bf16 MFMA.
+//
+//   dW[m][k] = sum_n gy[n][m] * x[n][k]      gy [N][M], x [N][K] bf16, dW fp32
+//
+// The reference trains its MLPs inside tcnn (model.py:21-31, 117-121,
+// 176-180); here they are PyTorch GEMMs, and the one shape hipBLASLt serves
+// badly is exactly this one: N = B*R*S = 1e5..1e6 rows reduced into a small
+// (<= 1600 x 512) output, i.e. a few dozen output tiles for 256 CUs
+// (0.15 PFLOP/s measured, tools/mm_probe.py), and batching it as split-K
+// costs ~1 ms of host time per call once several shapes alternate.
+//
+// Split-K MFMA kernel: a 256-thread workgroup owns a 128 x 128 tile of dW and
+// a range of n; four waves each compute 64 x 64 with v_mfma_f32_32x32x16_bf16.
+// Both operands are stored n-major (the reduction index is the ROW), so the
+// 32-row slabs are staged row-major in LDS (16-byte coalesced loads, the next
+// slab's loads in flight under the current slab's MFMAs) and read back with
+// ds_read_b64_tr_b16, the CDNA4 transposing LDS read, which hands each lane
+// 4 consecutive rows of one column.  The image is XOR-swizzled per 16-byte
+// chunk (cdna_hip_programming.md T10 image (b)) so those reads are
+// conflict-free.  fp32 partials per n-range are summed in a fixed order by a
+// second kernel (deterministic).
+#include "common.h"
+
+using namespace avr;
+
+namespace {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+constexpr int kTile = 128;   // dW tile edge (both m and k)
+constexpr int kSlab = 32;    // rows of n per LDS slab
+constexpr int kImg = kSlab * kTile * 2;  // bytes of one operand image (8 KiB)
+
+// byte offset of 16-byte chunk `ch` (0..15) of image row `row` (0..31)
+__device__ __forceinline__ int img_off(int row, int ch) {
+    return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ s16x4 tr_read(const char* lds_base, int byte_off) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(lds_base + byte_off));
+}
+
+__global__ __launch_bounds__(256) void linear_wgrad_kernel(int64_t N, int M, int K, int64_t rows_per_split,
+                                                            const __hip_bfloat16* __restrict__ gy,
+                                                            const __hip_bfloat16* __restrict__ x,
+                                                            float* __restrict__ partial) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * kImg];  // [A image][B image]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int m0 = blockIdx.y * kTile, k0 = blockIdx.x * kTile;
+    const int split = blockIdx.z;
+    const int64_t n_begin = (int64_t)split * rows_per_split;
+    const int64_t n_end = min(N, n_begin + rows_per_split);
+
+    // staging: thread -> chunks q = tid + 256u (u = 0, 1): row q/16, chunk q%16
+    u32x4v ra[2], rb[2];
+    int srow[2], sch[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int q = tid + 256 * u;
+        srow[u] = q >> 4;
+        sch[u] = q & 15;
+    }
+    // columns past M / K are clamped to a valid chunk: they only feed dW rows
+    // / columns that are never stored
+    const int64_t acol0 = min(m0 + 8 * sch[0], M - 8), acol1 = min(m0 + 8 * sch[1], M - 8);
+    const int64_t bcol0 = min(k0 + 8 * sch[0], K - 8), bcol1 = min(k0 + 8 * sch[1], K - 8);
+    auto issue = [&](int64_t n0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int64_t n = min(n0 + srow[u], n_end - 1);
+            const int64_t ac = u ? acol1 : acol0, bc = u ? bcol1 : bcol0;
+            ra[u] = *reinterpret_cast<const u32x4v*>(gy + n * M + ac);
+            rb[u] = *reinterpret_cast<const u32x4v*>(x + n * K + bc);
+        }
+    };
+    auto commit = [&](int64_t n0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            // rows past the split's end contribute zero
+            const bool ok = n0 + srow[u] < n_end;
+            const u32x4v z = {0u, 0u, 0u, 0u};
+            const int off = img_off(srow[u], sch[u]);
+            *reinterpret_cast<u32x4v*>(lds + off) = ok ? ra[u] : z;
+            *reinterpret_cast<u32x4v*>(lds + kImg + off) = ok ? rb[u] : z;
+        }
+    };
+
+    // transposed-read addresses: lane = 16g + 4q + p; group g takes columns
+    // 16(g&1) .. +15 of a 32-column block and rows 8(g>>1) .. +7 of a 16-row
+    // half-slab; lane 4q+p points at row r0+q, columns c0+4p .. c0+4p+3
+    const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+    const int wm = wave & 1, wk = wave >> 1;
+    auto tr_addr = [&](int colblock, int kh, int second) {
+        const int c0 = colblock + 16 * (g & 1);       // element column of the group
+        const int row = 16 * kh + 8 * (g >> 1) + 4 * second + qq;
+        return img_off(row, (c0 >> 3) + (pp >> 1)) + 8 * (pp & 1);
+    };
+    int aoff[2][2][2], boff[2][2][2];  // [block][kh][second]
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+            for (int sc = 0; sc < 2; ++sc) {
+                aoff[blk][kh][sc] = tr_addr(64 * wm + 32 * blk, kh, sc);
+                boff[blk][kh][sc] = tr_addr(64 * wk + 32 * blk, kh, sc) + kImg;
+            }
+
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+    if (n_begin < n_end) issue(n_begin);
+    for (int64_t n0 = n_begin; n0 < n_end; n0 += kSlab) {
+        __syncthreads();
+        commit(n0);
+        __syncthreads();
+        if (n0 + kSlab < n_end) issue(n0 + kSlab);  // next slab under the MFMAs
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+            bf16x8 av[2], bv[2];
+#pragma unroll
+            for (int blk = 0; blk < 2; ++blk) {
+                const s16x4 a0 = tr_read(lds, aoff[blk][kh][0]), a1 = tr_read(lds, aoff[blk][kh][1]);
+                const s16x4 b0 = tr_read(lds, boff[blk][kh][0]), b1 = tr_read(lds, boff[blk][kh][1]);
+                const s16x8 a = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+                const s16x8 b = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+                av[blk] = __builtin_bit_cast(bf16x8, a);
+                bv[blk] = __builtin_bit_cast(bf16x8, b);
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    // D layout: row (reg&3) + 8*(reg>>2) + 4*(lane>>5), column lane&31
+    float* out = partial + (int64_t)split * M * K;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int k = k0 + 64 * wk + 32 * j + (lane & 31);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + 64 * wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+                if (m < M && k < K) out[(int64_t)m * K + k] = acc[i][j][r];
+            }
+        }
+}
+
+// dW = sum over splits of the partials, in split order (deterministic).
+// 4 consecutive outputs per thread (16-byte loads), 8 splits' loads in flight.
+__global__ __launch_bounds__(256) void wgrad_finalize_kernel(int64_t MK, int splits,
+                                                              const float* __restrict__ partial,
+                                                              float* __restrict__ out) {
+    const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (i >= MK) return;  // MK % 8 == 0 (M, K multiples of 8)
+    f32x4 s = {0.0f, 0.0f, 0.0f, 0.0f};
+    int k = 0;
+    for (; k + 8 <= splits; k += 8) {
+        f32x4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            v[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(partial + (int64_t)(k + u) * MK + i));
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; k < splits; ++k) s += *reinterpret_cast<const f32x4*>(partial + (int64_t)k * MK + i);
+    *reinterpret_cast<f32x4*>(out + i) = s;
+}
+
+int wgrad_splits(int64_t N, int M, int K) {
+    const int tiles = ((M + kTile - 1) / kTile) * ((K + kTile - 1) / kTile);
+    int splits = (512 + tiles - 1) / tiles;  // ~2 workgroups per CU
+    const int64_t max_by_rows = N / 256 > 1 ? N / 256 : 1;  // >= 8 slabs per split
+    return (int)(splits < max_by_rows ? splits : max_by_rows);
+}
+
+}  // namespace
+
+extern "C" int avr_linear_wgrad_splits(int64_t N, int32_t M, int32_t K, int32_t* splits) {
+    AVR_REQUIRE(N >= 1 && M >= 8 && K >= 8 && splits, "avr_linear_wgrad_splits: bad args");
+    *splits = wgrad_splits(N, M, K);
+    return 0;
+}
+
+extern "C" int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* grad_y, const void* x,
+                                float* workspace, int32_t splits, float* grad_w, void* stream) {
+    AVR_REQUIRE(N >= 1 && M >= 8 && K >= 8 && grad_y && x && workspace && grad_w && splits >= 1,
+                "avr_linear_wgrad: bad args");
+    AVR_REQUIRE(M % 8 == 0 && K % 8 == 0, "avr_linear_wgrad: M and K must be multiples of 8");
+    AVR_REQUIRE(reinterpret_cast<uintptr_t>(grad_y) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(x) % 16 == 0,
+                "avr_linear_wgrad: operands must be 16-byte aligned");
+    int64_t rows = (N + splits - 1) / splits;
+    rows = (rows + kSlab - 1) / kSlab * kSlab;
+    const int used = (int)((N + rows - 1) / rows);
+    hipStream_t st = as_stream(stream);
+    const dim3 grid((K + kTile - 1) / kTile, (M + kTile - 1) / kTile, used);
+    hipLaunchKernelGGL(linear_wgrad_kernel, grid, dim3(256), 0, st, N, (int)M, (int)K, rows,
+                       (const __hip_bfloat16*)grad_y, (const __hip_bfloat16*)x, workspace);
+    if (int e = check_launch("avr_linear_wgrad")) return e;
+    const int64_t MK = (int64_t)M * K;
+    hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)((MK / 4 + 255) / 256)), dim3(256), 0, st,
+                       MK, used, workspace, grad_w);
+    return check_launch("avr_linear_wgrad_finalize");
+}

@@ -905,7 +905,7 @@ extern "C" int avr_reduce_splits(const avr_render_params* p, int32_t B, int32_t 
     // or ~16 (fp16: twice the VALU work per byte) resident waves per CU, and
     // a split's w/delay within the 32 KiB LDS slab.  Sweeps:
     // profiles/r01_sweep_*.jsonl.
-    const int64_t waves_target = (vec == 8) ? 4096 : 2048;
+    const int64_t waves_target = (vec == 8) ? 4096 : 1536;
     const int64_t waves_per_split = (int64_t)groups * B * (sh.threads / 64);
     int n = 1;
     auto rps = [&](int k) { return (R + k - 1) / k; };

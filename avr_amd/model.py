@@ -18,6 +18,82 @@ import torch.nn.functional as F
 from .encoding import HashGridEncoding
 
 
+import os
+
+_WGRAD_ROWS = 4096  # rows per split of the weight-gradient GEMM
+# split only the large weights: every distinct batched-GEMM shape in a step
+# costs ~1 ms of host time in hipBLASLt's solution lookup once more than a
+# few alternate (tools/mm_probe.py --interleave)
+_WGRAD_MIN = int(os.environ.get("AVR_WGRAD_MIN", str(512 * 512)))
+
+
+def _wgrad_hip(gy, x):
+    """dW = gy^T x on the HIP split-K MFMA kernel (bf16 operands, fp32 out)."""
+    import ctypes
+
+    from . import _lib
+
+    N, M = gy.shape
+    K = x.size(1)
+    sp = ctypes.c_int32(0)
+    _lib.call("avr_linear_wgrad_splits", N, M, K, ctypes.byref(sp))
+    ws = torch.empty(sp.value * M * K, dtype=torch.float32, device=gy.device)
+    out = torch.empty(M, K, dtype=torch.float32, device=gy.device)
+    _lib.call("avr_linear_wgrad", N, M, K, ctypes.c_void_p(gy.data_ptr()),
+              ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(ws.data_ptr()), sp.value,
+              ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(torch.cuda.current_stream(gy.device).cuda_stream))
+    return out
+
+
+def _hip_wgrad_ok(gy, x):
+    return (gy.is_cuda and gy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16
+            and gy.size(1) % 8 == 0 and x.size(1) % 8 == 0 and gy.size(1) >= 8 and x.size(1) >= 8
+            and gy.is_contiguous() and x.is_contiguous()
+            and gy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
+
+
+def _wgrad(gy, x):
+    """dW = gy^T x for gy [N, out], x [N, in] with N >> out, in.
+
+    A single GEMM with a K dimension of N = B*R*S (1e5..1e6) and a 512x512
+    output has only a few dozen output tiles, far too few for 256 CUs (it
+    measured 0.14 PFLOP/s).  Split K into chunks of _WGRAD_ROWS rows,
+    batch them (one output tile set per chunk) and sum the fp32 partials."""
+    if _hip_wgrad_ok(gy, x):
+        return _wgrad_hip(gy, x)
+    N = gy.size(0)
+    k = N // _WGRAD_ROWS
+    if k < 2 or gy.size(1) * x.size(1) < _WGRAD_MIN:
+        return (gy.t() @ x).float()
+    m = k * _WGRAD_ROWS
+    a = gy[:m].view(k, _WGRAD_ROWS, -1).transpose(1, 2)
+    b = x[:m].view(k, _WGRAD_ROWS, -1)
+    part = torch.bmm(a, b)
+    gw = part.sum(0, dtype=torch.float32)
+    if m < N:
+        gw += (gy[m:].t() @ x[m:]).float()
+    return gw
+
+
+class _Linear(torch.autograd.Function):
+    """y = x W^T with W kept in fp32 (master) and cast to the GEMM dtype;
+    the weight gradient uses the split-K GEMM above and is returned in fp32."""
+
+    @staticmethod
+    def forward(ctx, x, w_master, dtype):
+        w = w_master.to(dtype)
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = gy @ w if ctx.needs_input_grad[0] else None
+        gw = _wgrad(gy, x) if ctx.needs_input_grad[1] else None
+        return gx, gw, None
+
+
 class MLP(nn.Module):
     """tcnn.Network(n_in, n_out, {n_neurons, n_hidden_layers, activation ReLU,
     output_activation None}) without biases."""
@@ -34,12 +110,59 @@ class MLP(nn.Module):
         self.n_output_dims = n_out
 
     def forward(self, x):
-        x = x.to(self.dtype)
+        x = x.to(self.dtype).contiguous()
         for i, lin in enumerate(self.layers):
-            x = F.linear(x, lin.weight.to(self.dtype))
+            x = _Linear.apply(x, lin.weight, self.dtype)
             if i + 1 < len(self.layers):
                 x = F.relu(x)
         return x
+
+
+class _Broadcast(torch.autograd.Function):
+    """e [G, E] -> [B, R, S, E] broadcast over each group's rows; the backward
+    sums the group's row gradients in fp32 (autograd's own expand backward
+    would sum them in the feature dtype, fp16 for AVRModel's grids)."""
+
+    @staticmethod
+    def forward(ctx, e, view_shape, shape):
+        ctx.view_shape = view_shape
+        return e.view(view_shape).expand(shape).contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        dims = tuple(i for i, n in enumerate(ctx.view_shape) if n == 1)
+        gs = g.sum(dim=dims, keepdim=True, dtype=torch.float32)
+        return gs.to(g.dtype).view(-1, g.size(-1)), None, None
+
+
+def _grouped(enc, x, layout, per):
+    """Encode rows that repeat over a known group and broadcast the result.
+
+    x is the full [B*R*S, 3] network input.  With the renderer's layout
+    (B, R, S), `per="ray"` rows are constant over the S samples of a ray
+    (the view direction) and `per="pose"` rows over all R*S samples of a
+    pose (tx position / orientation): the grid is evaluated once per group
+    (bit-identical features) and expanded, so its backward scatters one
+    summed gradient per group instead of R*S contended atomics.  Returns a
+    [B, R, S, E] tensor."""
+    if layout is None:
+        return enc(x)
+    B, R, S = layout
+    if per == "sample":
+        return enc(x).view(B, R, S, -1)
+    if per == "ray":
+        e = enc(x.view(B, R, S, 3)[:, :, 0].reshape(B * R, 3))
+        return _Broadcast.apply(e, (B, R, 1, e.size(-1)), (B, R, S, e.size(-1)))
+    e = enc(x.view(B, R * S, 3)[:, 0].contiguous())
+    return _Broadcast.apply(e, (B, 1, 1, e.size(-1)), (B, R, S, e.size(-1)))
+
+
+def _cat_features(parts, layout):
+    """Concatenate per-sample features ([N, E] or [B, R, S, E] views) into
+    one contiguous [N, sum E] MLP input."""
+    if layout is None:
+        return torch.cat(parts, -1)
+    return torch.cat(parts, -1).view(-1, sum(p.size(-1) for p in parts))
 
 
 class AVRModel(nn.Module):
@@ -58,17 +181,22 @@ class AVRModel(nn.Module):
         sig_in = 128 + self._dir_encoding.n_output_dims + self._tx_encoding.n_output_dims
         self._model_signal = MLP(sig_in, self.signal_output_dim, cfg["signal_network"], mlp_dtype)
 
-    def forward(self, pts, view, tx, ch_idx=None):
+    # AVRRender passes ray_layout=(B, R, S) to networks that declare this
+    accepts_ray_layout = True
+
+    def forward(self, pts, view, tx, ch_idx=None, ray_layout=None):
         if ch_idx is not None:
             raise NotImplementedError("channel-embedding variants are not provided")
         bs, n = pts.size(0), pts.size(1)
+        L = ray_layout
         pos_enc = self._pos_encoding((pts.reshape(-1, 3) + 1) / 2)
         sigma_feat = self._model_encoder_sigma(pos_enc)
         attn = self._model_decoder_sigma(F.relu(sigma_feat))
-        dir_enc = self._dir_encoding((view.reshape(-1, 3) + 1) / 2)
-        tx_enc = self._tx_encoding((tx.reshape(-1, 3) + 1) / 2)
+        dir_enc = _grouped(self._dir_encoding, (view.reshape(-1, 3) + 1) / 2, L, "ray")
+        tx_enc = _grouped(self._tx_encoding, (tx.reshape(-1, 3) + 1) / 2, L, "pose")
         dt = sigma_feat.dtype
-        base = torch.cat([sigma_feat, dir_enc.to(dt), tx_enc.to(dt)], dim=-1)
+        sf = sigma_feat if L is None else sigma_feat.view(*L, -1)
+        base = _cat_features([sf, dir_enc.to(dt), tx_enc.to(dt)], L)
         signal = self._model_signal(base)
         attn = torch.abs(F.leaky_relu(attn)).view(bs, n, 1)
         return attn, signal.view(bs, n, self.signal_output_dim)
@@ -96,19 +224,26 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
                  + self._pos_signal_encoding.n_output_dims + self._tx_pos_signal_encoding.n_output_dims)
         self._model_signal = MLP(n_sig, self.signal_output_dim, cfg["signal_network"], mlp_dtype)
 
-    def forward(self, pts, view, tx, tx_view):
+    accepts_ray_layout = True
+
+    def forward(self, pts, view, tx, tx_view, ray_layout=None):
         bs, n = pts.size(0), pts.size(1)
+        L = ray_layout
         pts = (pts.reshape(-1, 3) + 1) / 2
         view = (view.reshape(-1, 3) + 1) / 2
         tx = (tx.reshape(-1, 3) + 1) / 2
         tx_view = (tx_view.reshape(-1, 3) + 1) / 2
-        pos_e = self._pos_encoding(pts)
-        txp_e = self._tx_pos_encoding(tx)
-        feat = self._model_encoder_sigma(torch.cat([pos_e, txp_e], -1))
+        pos_e = _grouped(self._pos_encoding, pts, L, "sample")
+        txp_e = _grouped(self._tx_pos_encoding, tx, L, "pose")
+        feat = self._model_encoder_sigma(_cat_features([pos_e, txp_e], L))
         attn = self._model_decoder_sigma(F.relu(feat))
         dt = feat.dtype
-        parts = [F.relu(feat), self._dir_encoding(view).to(dt), self._tx_dir_encoding(tx_view).to(dt),
-                 self._pos_signal_encoding(pts).to(dt), self._tx_pos_signal_encoding(tx).to(dt)]
-        signal = self._model_signal(torch.cat(parts, -1))
+        rf = F.relu(feat)
+        parts = [rf if L is None else rf.view(*L, -1),
+                 _grouped(self._dir_encoding, view, L, "ray").to(dt),
+                 _grouped(self._tx_dir_encoding, tx_view, L, "pose").to(dt),
+                 _grouped(self._pos_signal_encoding, pts, L, "sample").to(dt),
+                 _grouped(self._tx_pos_signal_encoding, tx, L, "pose").to(dt)]
+        signal = self._model_signal(_cat_features(parts, L))
         attn = torch.abs(F.leaky_relu(attn, negative_slope=self.leaky_relu)).view(bs, n, 1)
         return attn, signal.reshape(bs, n, self.signal_output_dim)

@@ -358,6 +358,10 @@ class AVRRender(nn.Module):
         """Render [B, F, 2] (real, imag) spectra; see renderer.py:31-124."""
         pts, view, tx, dtx, geom = self.sample(rays_o, position_tx, direction_tx)
         kw = {} if ch_idx is None else {"ch_idx": ch_idx}
+        if getattr(self.network_fn, "accepts_ray_layout", False):
+            # our own networks: tell them which inputs repeat over samples /
+            # rays so they encode each distinct row once (same values)
+            kw["ray_layout"] = (geom["B"], geom["n_rays"], int(self.n_samples))
         if dtx is not None:
             attn, signal = self.network_fn(pts, view, tx, dtx, **kw)
         else:

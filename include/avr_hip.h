@@ -189,6 +189,16 @@ int avr_hashgrid_bwd(int64_t N, int32_t n_levels, const float* x, const void* gr
                      int32_t grad_dtype, const int64_t* level_offset, const float* level_scale,
                      const int32_t* level_res, float* grad_params, void* stream);
 
+/* ---- a6: weight gradient of the networks' bias-free linear layers -------
+ * grad_w[M][K] (fp32) = sum_n grad_y[n][M] * x[n][K], both operands bf16,
+ * row-major, 16-byte aligned, M and K multiples of 8.  Replaces the wgrad
+ * GEMM tcnn runs inside its MLP backward (model.py:21-31, 176-180 through
+ * avr_runner.py:190).  Split-K over n: `workspace` holds splits*M*K fp32
+ * partials (splits from avr_linear_wgrad_splits), summed deterministically. */
+int avr_linear_wgrad_splits(int64_t N, int32_t M, int32_t K, int32_t* splits);
+int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* grad_y, const void* x,
+                     float* workspace, int32_t splits, float* grad_w, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

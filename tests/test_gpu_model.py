@@ -48,3 +48,60 @@ def test_meshrir_model_training_step():
     model = AVRModel(cfg).to(DEV)
     out = _step(model, w, None)
     assert out.shape == (1, 512, 2)
+
+
+@pytest.mark.parametrize("cls", ["AVRModel", "AVRModel_complex"])
+def test_ray_layout_grouped_encoding_matches_flat(cls):
+    """With ray_layout the per-ray / per-pose inputs are encoded once per group;
+    the network output must be bit-identical to the flat call and the
+    parameter gradients equal up to fp32 summation order."""
+    w = WORKLOADS["c1_meshrir_plumbing"]
+    B, R, S = 2, w.n_rays, w.n_samples
+    if cls == "AVRModel":
+        model = AVRModel(dict(MESHRIR_MODEL, signal_output_dim=254)).to(DEV)
+    else:
+        model = AVRModel_complex(dict(RAF_MODEL, signal_output_dim=254)).to(DEV)
+    r = AVRRender(model, **w.render)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    ro = torch.rand(B, 3, device=DEV, generator=g) * 2 - 1
+    tx = torch.rand(B, 3, device=DEV, generator=g) * 2 - 1
+    dtx = torch.nn.functional.normalize(torch.randn(B, 3, device=DEV, generator=g), dim=-1)
+    torch.manual_seed(0)
+    pts, view, txs, dts, geom = r.sample(ro, tx, dtx if cls != "AVRModel" else None)
+    args = (pts, view, txs) if cls == "AVRModel" else (pts, view, txs, dts)
+    outs, grads = [], []
+    for layout in (None, (B, R, S)):
+        model.zero_grad(set_to_none=True)
+        attn, sig = model(*args, ray_layout=layout)
+        (attn.float().sum() + (sig.float() * 1e-2).sum()).backward()
+        outs.append((attn.detach(), sig.detach()))
+        grads.append({n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None})
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert grads[0].keys() == grads[1].keys()
+    # fp16 feature grids (AVRModel): the group's summed gradient is rounded
+    # to fp16 once (the flat path adds the fp16 row gradients in fp32)
+    rtol = 2e-4 if cls == "AVRModel_complex" else 2e-3
+    for n in grads[0]:
+        a, b = grads[1][n], grads[0][n]
+        err = float((a - b).norm() / b.norm().clamp_min(1e-30))
+        assert err < rtol, (n, err)
+
+
+@pytest.mark.parametrize("N,M,K", [(83200, 512, 512), (83200, 1600, 512), (5003, 512, 336),
+                                   (300, 128, 80), (33, 8, 16), (147712, 256, 128)])
+def test_linear_wgrad_kernel_matches_fp32(N, M, K):
+    """avr_linear_wgrad (split-K bf16 MFMA) against an fp32 GEMM of the same
+    bf16 operands (products are exact in fp32; only the summation order
+    differs)."""
+    from avr_amd.model import _hip_wgrad_ok, _wgrad_hip
+
+    g = torch.Generator(device=DEV).manual_seed(N + M + K)
+    gy = torch.randn(N, M, device=DEV, generator=g).to(torch.bfloat16)
+    x = torch.randn(N, K, device=DEV, generator=g).to(torch.bfloat16)
+    assert _hip_wgrad_ok(gy, x)
+    out = _wgrad_hip(gy, x)
+    ref = gy.double().t() @ x.double()
+    err = float((out.double() - ref).norm() / ref.norm())
+    assert err < 5e-5, err
+    # deterministic
+    assert torch.equal(out, _wgrad_hip(gy, x))

@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mlp-dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--core-only", action="store_true")
+    ap.add_argument("--profile", action="store_true", help="torch.profiler table of a few steps")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     w = WORKLOADS[args.workload]
@@ -104,6 +105,14 @@ def main():
         opt.step()
 
     t = timeit(train_step, args.steps, args.warmup)
+    if args.profile:
+        from torch.profiler import ProfilerActivity, profile
+
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            for _ in range(3):
+                train_step()
+            torch.cuda.synchronize()
+        print(prof.key_averages().table(sort_by="cpu_time_total", row_limit=40), file=sys.stderr)
     res["train_step_ms"] = t * 1e3
     res["train_ray_samples_per_s"] = w.ray_samples / t
     res["mlp_dtype"] = args.mlp_dtype

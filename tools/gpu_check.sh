@@ -35,12 +35,16 @@ for s in "$@"; do
             && step exp_c5_S128 300 python tools/tune.py --workload c5_simu_4096x512x2048 --S 128 --variants u4nt,u4 --nsplit 4,8 --ksplit 8 --rounds 2 --steps 5 \
             && step exp_c5_fp32 300 python tools/tune.py --workload c5_simu_4096x512x2048 --S 128 --dtype float32 --variants u4nt --nsplit 2,4,8 --ksplit 8 --rounds 2 --steps 5 ;;
     train) step train_c3 600 python tools/bench_train.py && step train_c4 600 python tools/bench_train.py --workload c4_raf_empty_b4_per_gpu ;;
+    wgrad) for v in 1 262144 500000 819200 100000000; do AVR_WGRAD_MIN=$v step wgrad_$v 300 python tools/bench_train.py --steps 10 || exit 1; done ;;
+    torchprof) step torchprof 600 python tools/bench_train.py --steps 5 --profile ;;
     proftrain) step proftrain 600 rocprofv3 --kernel-trace --stats -d $OUT/proftrain -o run --output-format csv -- python tools/bench_train.py --steps 5 --warmup 2 ;;
     gexp) step g1 200 python tools/tune.py --variants u4nt --nsplit 2,4 --ksplit 8 --rounds 3 \
           && AVR_REDUCE_G=2 step g2 200 python tools/tune.py --variants u4nt --nsplit 1,2,4 --ksplit 8 --rounds 3 \
           && AVR_REDUCE_G=4 step g4 200 python tools/tune.py --variants u4nt --nsplit 1,2 --ksplit 8 --rounds 3 ;;
     tunebwd) step tunebwd 600 python tools/tune_bwd.py $TUNE_ARGS && step tunebwd2 600 python tools/tune_bwd.py --workload c2_meshrir_1024x256x512 $TUNE_ARGS && step tunebwd5 600 python tools/tune_bwd.py --workload c5_simu_4096x512x2048 $TUNE_ARGS ;;
     profcore) step profcore 600 rocprofv3 --kernel-trace --stats -d $OUT/profcore -o run --output-format csv -- python tools/bench_train.py --core-only --steps 20 ;;
+    prof5) step prof5 600 rocprofv3 --kernel-trace --stats -d $OUT/prof5 -o run --output-format csv -- python bench.py --workload c5_simu_4096x512x2048 --no-cpu-baseline --steps 10 --warmup 2 --streams 1 --poses 4 ;;
+    benchall) for wl in c1_meshrir_plumbing c3_raf_furnished_b4 c4_raf_empty_b4_per_gpu c5_simu_4096x512x2048; do step bench_$wl 300 python bench.py --workload $wl --no-cpu-baseline --steps 50 || exit 1; done ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 50 --warmup 5 --streams 1 ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 3 --streams 1 && step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 3 --streams 1 ;;
   esac
