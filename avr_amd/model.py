@@ -109,13 +109,20 @@ class MLP(nn.Module):
         self.dtype = dtype
         self.n_output_dims = n_out
 
-    def forward(self, x):
+    def hidden(self, x):
+        """All layers but the last (each followed by ReLU): the features the
+        output layer is applied to."""
         x = x.to(self.dtype).contiguous()
-        for i, lin in enumerate(self.layers):
-            x = _Linear.apply(x, lin.weight, self.dtype)
-            if i + 1 < len(self.layers):
-                x = F.relu(x)
+        for lin in self.layers[:-1]:
+            x = F.relu(_Linear.apply(x, lin.weight, self.dtype))
         return x
+
+    def last(self, h):
+        """The bias-free output layer (output_activation None)."""
+        return _Linear.apply(h.contiguous(), self.layers[-1].weight, self.dtype)
+
+    def forward(self, x):
+        return self.last(self.hidden(x))
 
 
 class _Broadcast(torch.autograd.Function):
@@ -183,8 +190,12 @@ class AVRModel(nn.Module):
 
     # AVRRender passes ray_layout=(B, R, S) to networks that declare this
     accepts_ray_layout = True
+    # ... and folds the signal network's last layer into the render
+    # (forward_fused / finish_signal) for networks that declare this
+    supports_fused_head = True
 
-    def forward(self, pts, view, tx, ch_idx=None, ray_layout=None):
+    def _trunk(self, pts, view, tx, ch_idx, ray_layout):
+        """Everything up to the signal network's input: (attn, features)."""
         if ch_idx is not None:
             raise NotImplementedError("channel-embedding variants are not provided")
         bs, n = pts.size(0), pts.size(1)
@@ -197,9 +208,24 @@ class AVRModel(nn.Module):
         dt = sigma_feat.dtype
         sf = sigma_feat if L is None else sigma_feat.view(*L, -1)
         base = _cat_features([sf, dir_enc.to(dt), tx_enc.to(dt)], L)
-        signal = self._model_signal(base)
         attn = torch.abs(F.leaky_relu(attn)).view(bs, n, 1)
-        return attn, signal.view(bs, n, self.signal_output_dim)
+        return attn, base
+
+    def forward(self, pts, view, tx, ch_idx=None, ray_layout=None):
+        attn, base = self._trunk(pts, view, tx, ch_idx, ray_layout)
+        signal = self._model_signal(base)
+        return attn, signal.view(pts.size(0), pts.size(1), self.signal_output_dim)
+
+    def forward_fused(self, pts, view, tx, ch_idx=None, ray_layout=None):
+        """(attn, h, W, dtype) with signal = h @ W^T left to the renderer."""
+        attn, base = self._trunk(pts, view, tx, ch_idx, ray_layout)
+        h = self._model_signal.hidden(base)
+        return (attn, h.view(pts.size(0), pts.size(1), -1), self._model_signal.layers[-1].weight,
+                self._model_signal.dtype)
+
+    def finish_signal(self, h):
+        """The output layer forward_fused left out: [B, N, K] -> [B, N, T]."""
+        return self._model_signal.last(h.reshape(-1, h.size(-1))).view(h.size(0), h.size(1), -1)
 
 
 class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
@@ -225,8 +251,22 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
         self._model_signal = MLP(n_sig, self.signal_output_dim, cfg["signal_network"], mlp_dtype)
 
     accepts_ray_layout = True
+    supports_fused_head = True
 
     def forward(self, pts, view, tx, tx_view, ray_layout=None):
+        attn, base = self._trunk(pts, view, tx, tx_view, ray_layout)
+        signal = self._model_signal(base)
+        return attn, signal.reshape(pts.size(0), pts.size(1), self.signal_output_dim)
+
+    def forward_fused(self, pts, view, tx, tx_view, ray_layout=None):
+        attn, base = self._trunk(pts, view, tx, tx_view, ray_layout)
+        h = self._model_signal.hidden(base)
+        return (attn, h.view(pts.size(0), pts.size(1), -1), self._model_signal.layers[-1].weight,
+                self._model_signal.dtype)
+
+    finish_signal = AVRModel.finish_signal
+
+    def _trunk(self, pts, view, tx, tx_view, ray_layout):
         bs, n = pts.size(0), pts.size(1)
         L = ray_layout
         pts = (pts.reshape(-1, 3) + 1) / 2
@@ -244,6 +284,5 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
                  _grouped(self._tx_dir_encoding, tx_view, L, "pose").to(dt),
                  _grouped(self._pos_signal_encoding, pts, L, "sample").to(dt),
                  _grouped(self._tx_pos_signal_encoding, tx, L, "pose").to(dt)]
-        signal = self._model_signal(_cat_features(parts, L))
         attn = torch.abs(F.leaky_relu(attn, negative_slope=self.leaky_relu)).view(bs, n, 1)
-        return attn, signal.reshape(bs, n, self.signal_output_dim)
+        return attn, _cat_features(parts, L)

@@ -18,6 +18,7 @@ and `signal` outputs through `RenderCore`.  There is no CPU fallback.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 import threading
@@ -150,26 +151,65 @@ def pick_k_split(B, S, T):
 # --------------------------------------------------------------------------
 # autograd core: (attn, signal) -> spectrum
 # --------------------------------------------------------------------------
+def _weights(p, attn, rays_o, position_tx, dirs, tables, st):
+    """avr_weights_fwd: compositing weights w and source delays [B, R, S]."""
+    B = attn.size(0)
+    R, S = p.n_rays, p.n_samples
+    dev = attn.device
+    w = torch.empty(B, R, S, dtype=torch.float32, device=dev)
+    delay = torch.empty(B, R, S, dtype=torch.int32, device=dev)
+    _lib.call("avr_weights_fwd", ctypes_ref(p), B, _ptr(attn), _dtype_code(attn), _ptr(rays_o),
+              _ptr(position_tx), _ptr(dirs), _ptr(tables.d_vals), _ptr(w), _ptr(delay), st)
+    return w, delay
+
+
+def _spectrum(p, tables, part, n_split, B, dev, st):
+    """Partials [n_split, B, S, T] -> DFT + phase -> [B, F, 2]."""
+    S, T = p.n_samples, p.T
+    F = T // 2 + 1
+    k_split = pick_k_split(B, S, T)
+    P = math.ceil(S / 32) * k_split
+    spart = torch.empty(B, P, F, 2, dtype=torch.float32, device=dev)
+    _lib.call("avr_dft_phase_fwd", ctypes_ref(p), B, _ptr(part), n_split, _ptr(tables.pl),
+              _ptr(tables.shift), _ptr(tables.phase), _ptr(tables.twiddle), k_split,
+              _ptr(spart), st)
+    out = torch.empty(B, F, 2, dtype=torch.float32, device=dev)
+    _lib.call("avr_spectrum_finalize", B, P, F, _ptr(spart), _ptr(out), st)
+    return out
+
+
+def _grad_z(p, tables, grad_out, B, dev, st):
+    """avr_dft_phase_bwd: dL/dz [B, S, T] (path loss and tail mask included)."""
+    g = grad_out.contiguous().float()
+    gz = torch.empty(B, p.n_samples, p.T, dtype=torch.float32, device=dev)
+    _lib.call("avr_dft_phase_bwd", ctypes_ref(p), B, _ptr(g), _ptr(tables.pl), _ptr(tables.shift),
+              _ptr(tables.phase), _ptr(tables.twiddle), _ptr(gz), st)
+    return gz
+
+
+def _grad_attn(p, tables, attn, grad_w, st):
+    grad_attn = torch.empty_like(attn)
+    _lib.call("avr_weights_bwd", ctypes_ref(p), attn.size(0), _ptr(attn), _dtype_code(attn),
+              _ptr(tables.d_vals), _ptr(grad_w), _ptr(grad_attn), st)
+    return grad_attn
+
+
 class RenderCore(torch.autograd.Function):
     """Everything after the network call (renderer.py:75-121) as HIP kernels.
 
-    Inputs: attn [B, R*S] and signal [B, R*S, T] (fp32 or fp16, contiguous),
-    plus the pose geometry.  Output [B, F, 2] fp32.  Gradients flow to attn
-    and signal (poses are constants, as in the reference).
+    Inputs: attn [B, R*S] and signal [B, R*S, T] (fp32, fp16 or bf16,
+    contiguous), plus the pose geometry.  Output [B, F, 2] fp32.  Gradients
+    flow to attn and signal (poses are constants, as in the reference).
     """
 
     @staticmethod
     def forward(ctx, attn, signal, p, tables, rays_o, position_tx, dirs):
         dev = signal.device
         B = signal.size(0)
-        R, S, T = p.n_rays, p.n_samples, p.T
-        F = T // 2 + 1
+        S, T = p.n_samples, p.T
         st = _stream(dev)
         pref = ctypes_ref(p)
-        w = torch.empty(B, R, S, dtype=torch.float32, device=dev)
-        delay = torch.empty(B, R, S, dtype=torch.int32, device=dev)
-        _lib.call("avr_weights_fwd", pref, B, _ptr(attn), _dtype_code(attn), _ptr(rays_o),
-                  _ptr(position_tx), _ptr(dirs), _ptr(tables.d_vals), _ptr(w), _ptr(delay), st)
+        w, delay = _weights(p, attn, rays_o, position_tx, dirs, tables, st)
         n_split = reduce_splits(p, B, _dtype_code(signal))
         part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
         timer = KERNEL_TIMER
@@ -179,14 +219,7 @@ class RenderCore(torch.autograd.Function):
                   _ptr(delay), n_split, _ptr(part), st)
         if timer is not None:
             timer.end(dev)
-        k_split = pick_k_split(B, S, T)
-        P = math.ceil(S / 32) * k_split
-        spart = torch.empty(B, P, F, 2, dtype=torch.float32, device=dev)
-        _lib.call("avr_dft_phase_fwd", pref, B, _ptr(part), n_split, _ptr(tables.pl),
-                  _ptr(tables.shift), _ptr(tables.phase), _ptr(tables.twiddle), k_split,
-                  _ptr(spart), st)
-        out = torch.empty(B, F, 2, dtype=torch.float32, device=dev)
-        _lib.call("avr_spectrum_finalize", B, P, F, _ptr(spart), _ptr(out), st)
+        out = _spectrum(p, tables, part, n_split, B, dev, st)
         ctx.p, ctx.tables = p, tables
         ctx.save_for_backward(attn, signal, w, delay)
         return out
@@ -197,24 +230,72 @@ class RenderCore(torch.autograd.Function):
         p, tables = ctx.p, ctx.tables
         dev = signal.device
         B = signal.size(0)
+        R, S = p.n_rays, p.n_samples
+        st = _stream(dev)
+        gz = _grad_z(p, tables, grad_out, B, dev, st)
+        grad_signal = torch.empty_like(signal)
+        grad_w = torch.empty(B, R, S, dtype=torch.float32, device=dev)
+        _lib.call("avr_ray_reduce_bwd", ctypes_ref(p), B, _ptr(signal), _dtype_code(signal),
+                  _ptr(gz), _ptr(w), _ptr(delay), _ptr(grad_signal), _ptr(grad_w), st)
+        grad_attn = _grad_attn(p, tables, attn, grad_w, st) if ctx.needs_input_grad[0] else None
+        return (grad_attn, grad_signal if ctx.needs_input_grad[1] else None,
+                None, None, None, None, None)
+
+
+class FusedHeadCore(torch.autograd.Function):
+    """Render core with the signal network's last linear layer folded in
+    (kernels in csrc/head.hip).
+
+    Inputs: attn [B, R*S], the last hidden activation h [B, R*S, K] and the
+    layer's fp32 master weight [T, K] (cast to `dtype`, fp32 or bf16, as the
+    unfused layer would).  Equal to RenderCore on signal = h @ W^T, without
+    the [B, R*S, T] tensor, the R*S*K*T GEMM or their backward; gradients to
+    attn, h and the weight.
+    """
+
+    @staticmethod
+    def forward(ctx, attn, h, w_master, dtype, p, tables, rays_o, position_tx, dirs):
+        dev = h.device
+        B, K = h.size(0), h.size(-1)
+        S, T = p.n_samples, p.T
+        st = _stream(dev)
+        pref = ctypes_ref(p)
+        W = w_master.to(dtype).contiguous()
+        code = _dtype_code(h)
+        w, delay = _weights(p, attn, rays_o, position_tx, dirs, tables, st)
+        ns = ctypes.c_int32(0)
+        _lib.call("avr_head_splits", pref, B, K, code, ctypes.byref(ns))
+        n_split = ns.value
+        part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
+        _lib.call("avr_head_fwd", pref, B, K, _ptr(h), _ptr(W), code, _ptr(w), _ptr(delay),
+                  n_split, _ptr(part), st)
+        out = _spectrum(p, tables, part, n_split, B, dev, st)
+        ctx.p, ctx.tables = p, tables
+        ctx.save_for_backward(attn, h, W, w, delay)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        attn, h, W, w, delay = ctx.saved_tensors
+        p, tables = ctx.p, ctx.tables
+        dev = h.device
+        B, K = h.size(0), h.size(-1)
         R, S, T = p.n_rays, p.n_samples, p.T
         st = _stream(dev)
         pref = ctypes_ref(p)
-        g = grad_out.contiguous().float()
-        gz = torch.empty(B, S, T, dtype=torch.float32, device=dev)
-        _lib.call("avr_dft_phase_bwd", pref, B, _ptr(g), _ptr(tables.pl), _ptr(tables.shift),
-                  _ptr(tables.phase), _ptr(tables.twiddle), _ptr(gz), st)
-        grad_signal = torch.empty_like(signal)
+        code = _dtype_code(h)
+        gz = _grad_z(p, tables, grad_out, B, dev, st)
+        nbytes = ctypes.c_int64(0)
+        _lib.call("avr_head_bwd_workspace", pref, B, K, code, ctypes.byref(nbytes))
+        ws = torch.empty(max(1, nbytes.value // 4), dtype=torch.float32, device=dev)
+        grad_h = torch.empty_like(h)
         grad_w = torch.empty(B, R, S, dtype=torch.float32, device=dev)
-        _lib.call("avr_ray_reduce_bwd", pref, B, _ptr(signal), _dtype_code(signal), _ptr(gz),
-                  _ptr(w), _ptr(delay), _ptr(grad_signal), _ptr(grad_w), st)
-        grad_attn = None
-        if ctx.needs_input_grad[0]:
-            grad_attn = torch.empty_like(attn)
-            _lib.call("avr_weights_bwd", pref, B, _ptr(attn), _dtype_code(attn),
-                      _ptr(tables.d_vals), _ptr(grad_w), _ptr(grad_attn), st)
-        return (grad_attn, grad_signal if ctx.needs_input_grad[1] else None,
-                None, None, None, None, None)
+        grad_W = torch.empty(T, K, dtype=torch.float32, device=dev)
+        _lib.call("avr_head_bwd", pref, B, K, _ptr(h), _ptr(W), code, _ptr(w), _ptr(delay), _ptr(gz),
+                  _ptr(grad_h), _ptr(grad_w), _ptr(grad_W), _ptr(ws), nbytes.value, st)
+        grad_attn = _grad_attn(p, tables, attn, grad_w, st) if ctx.needs_input_grad[0] else None
+        return (grad_attn, grad_h if ctx.needs_input_grad[1] else None,
+                grad_W if ctx.needs_input_grad[2] else None, None, None, None, None, None, None)
 
 
 # --------------------------------------------------------------------------
@@ -270,6 +351,9 @@ class AVRRender(nn.Module):
             setattr(self, k, kwargs[k])
         self._cfg = {k: kwargs[k] for k in _RENDER_KEYS}
         self.ray_range = None  # (r0, r1) when rays are sharded over GPUs
+        # fold the signal network's last layer into the render when the
+        # network offers it (avr_amd.model networks; FusedHeadCore)
+        self.fused_head = bool(kwargs.get("fused_head", True))
 
     # -- stages, exposed for tests and for callers that bring their own network
     def _device(self, rays_o):
@@ -354,6 +438,40 @@ class AVRRender(nn.Module):
             return RenderCore.apply(attn, signal, p, tables, geom["rays_o"], geom["position_tx"],
                                     geom["dirs"])
 
+    def _head_supported(self, geom, h, weight, dtype):
+        """Whether the fused-head kernels take this shape (T <= 4096, <= 4096
+        rays per shard, the LDS budget, fp32/bf16); otherwise the network
+        applies its last layer and the plain path renders."""
+        if dtype not in (torch.float32, torch.bfloat16):
+            return False
+        p = render_params(self._cfg, weight.size(0), n_rays=geom["n_rays"])
+        code = DTYPE_BF16 if dtype == torch.bfloat16 else DTYPE_F32
+        n = ctypes.c_int32(0)
+        return _lib.load().avr_head_splits(ctypes_ref(p), geom["B"], h.size(-1), code,
+                                           ctypes.byref(n)) == 0
+
+    def render_from_hidden(self, attn, h, weight, dtype, geom):
+        """Render core with the signal head fused (FusedHeadCore): `h` is the
+        signal network's last hidden activation [B, R*S, K], `weight` its
+        last layer's weight [T, K] (signal = h @ weight^T)."""
+        dev, B = geom["device"], geom["B"]
+        S = int(self.n_samples)
+        attn = attn.to(dev).reshape(B, -1)
+        if attn.dtype not in (torch.float32, torch.float16, torch.bfloat16):
+            attn = attn.float()
+        attn = attn.contiguous()
+        K, T = h.size(-1), weight.size(0)
+        h = h.to(dev, dtype).reshape(B, -1, K).contiguous()
+        R = geom["n_rays"]
+        if attn.size(1) != R * S or h.size(1) != R * S:
+            raise ValueError(f"network output has {h.size(1)} ray-samples, expected {R}x{S}={R * S}")
+        p = render_params(self._cfg, T, n_rays=R)
+        with torch.cuda.device(dev):
+            tables = get_tables(p, dev)
+            check_config(p, tables)
+            return FusedHeadCore.apply(attn, h, weight, dtype, p, tables, geom["rays_o"],
+                                       geom["position_tx"], geom["dirs"])
+
     def forward(self, rays_o, position_tx, direction_tx=None, ch_idx=None):
         """Render [B, F, 2] (real, imag) spectra; see renderer.py:31-124."""
         pts, view, tx, dtx, geom = self.sample(rays_o, position_tx, direction_tx)
@@ -362,6 +480,13 @@ class AVRRender(nn.Module):
             # our own networks: tell them which inputs repeat over samples /
             # rays so they encode each distinct row once (same values)
             kw["ray_layout"] = (geom["B"], geom["n_rays"], int(self.n_samples))
+        net_in = (pts, view, tx) if dtx is None else (pts, view, tx, dtx)
+        if self.fused_head and getattr(self.network_fn, "supports_fused_head", False):
+            attn, h, weight, dtype = self.network_fn.forward_fused(*net_in, **kw)
+            if self._head_supported(geom, h, weight, dtype):
+                return self.render_from_hidden(attn, h, weight, dtype, geom)
+            signal = self.network_fn.finish_signal(h)
+            return self.render_from_network_output(attn, signal, geom)
         if dtx is not None:
             attn, signal = self.network_fn(pts, view, tx, dtx, **kw)
         else:

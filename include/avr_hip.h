@@ -199,6 +199,30 @@ int avr_linear_wgrad_splits(int64_t N, int32_t M, int32_t K, int32_t* splits);
 int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* grad_y, const void* x,
                      float* workspace, int32_t splits, float* grad_w, void* stream);
 
+/* ---- §8f rank 1: fused signal head -------------------------------------
+ * The signal network's last bias-free linear layer (model.py:176-180,
+ * output_activation None) folded into the ray reduction:
+ *   zpart[n][B][S][T], summed over n = avr_ray_reduce_fwd's `part` for
+ *   signal[b,r,s,t] = sum_k h[b,r,s,k] * W[t,k]
+ * without materialising the signal.  h [B][R][S][K] (post-activation hidden
+ * features) and W [T][K] are fp32 or bf16 (dtype), 16-byte aligned.  n_split
+ * (a power of two <= 16, for avr_dft_phase_fwd) comes from avr_head_splits.
+ * T <= 4096 and <= 4096 rays per shard. */
+int avr_head_splits(const avr_render_params* p, int32_t B, int32_t K, int32_t dtype,
+                    int32_t* n_split);
+int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* W,
+                 int32_t dtype, const float* w, const int32_t* delay, int32_t n_split,
+                 float* zpart, void* stream);
+/* Backward: gz [B][S][T] (avr_dft_phase_bwd) -> grad_h [B][R][S][K] (dtype),
+ * grad_w [B][R][S] fp32 (to avr_weights_bwd) and grad_W [T][K] fp32.
+ * `workspace` holds avr_head_bwd_workspace() bytes of fp32 partials. */
+int avr_head_bwd_workspace(const avr_render_params* p, int32_t B, int32_t K, int32_t dtype,
+                           int64_t* bytes);
+int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* W,
+                 int32_t dtype, const float* w, const int32_t* delay, const float* gz,
+                 void* grad_h, float* grad_w, float* grad_W, float* workspace,
+                 int64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mlp-dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--core-only", action="store_true")
+    ap.add_argument("--no-fused", action="store_true", help="materialise the signal (no fused head)")
     ap.add_argument("--profile", action="store_true", help="torch.profiler table of a few steps")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -92,7 +93,7 @@ def main():
     mlp_dtype = torch.bfloat16 if args.mlp_dtype == "bf16" else torch.float32
     cfg = dict(RAF_MODEL, signal_output_dim=T)
     model = AVRModel_complex(cfg, mlp_dtype=mlp_dtype).to(dev)
-    r = AVRRender(model, **w.render).to(dev)
+    r = AVRRender(model, fused_head=not args.no_fused, **w.render).to(dev)
     opt = torch.optim.Adam(r.parameters(), lr=2e-4)
     target = torch.randn(B, T // 2 + 1, 2, device=dev, generator=g)
 
@@ -116,6 +117,7 @@ def main():
     res["train_step_ms"] = t * 1e3
     res["train_ray_samples_per_s"] = w.ray_samples / t
     res["mlp_dtype"] = args.mlp_dtype
+    res["fused_head"] = not args.no_fused
     print(json.dumps(res))
 
 

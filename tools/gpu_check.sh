@@ -35,6 +35,7 @@ for s in "$@"; do
             && step exp_c5_S128 300 python tools/tune.py --workload c5_simu_4096x512x2048 --S 128 --variants u4nt,u4 --nsplit 4,8 --ksplit 8 --rounds 2 --steps 5 \
             && step exp_c5_fp32 300 python tools/tune.py --workload c5_simu_4096x512x2048 --S 128 --dtype float32 --variants u4nt --nsplit 2,4,8 --ksplit 8 --rounds 2 --steps 5 ;;
     train) step train_c3 600 python tools/bench_train.py && step train_c4 600 python tools/bench_train.py --workload c4_raf_empty_b4_per_gpu ;;
+    trainu) step trainu_c3 600 python tools/bench_train.py --no-fused && step trainu_c4 600 python tools/bench_train.py --workload c4_raf_empty_b4_per_gpu --no-fused ;;
     wgrad) for v in 1 262144 500000 819200 100000000; do AVR_WGRAD_MIN=$v step wgrad_$v 300 python tools/bench_train.py --steps 10 || exit 1; done ;;
     torchprof) step torchprof 600 python tools/bench_train.py --steps 5 --profile ;;
     proftrain) step proftrain 600 rocprofv3 --kernel-trace --stats -d $OUT/proftrain -o run --output-format csv -- python tools/bench_train.py --steps 5 --warmup 2 ;;
