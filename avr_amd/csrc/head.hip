@@ -33,39 +33,43 @@ namespace {
 
 constexpr int kThreads = 256;
 
-// KB consecutive elements of a row as floats (16-byte aligned when KB*es >= 16)
+// Barrier for LDS-only communication: waits for this thread's LDS traffic but
+// leaves its global loads in flight (__syncthreads would drain them), so the
+// next block's operands stream in while the current block is scanned.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt/expcnt untouched (gfx9 encoding)
+    __builtin_amdgcn_s_barrier();
+}
+
+// KB consecutive elements of a row, held raw (packed) in registers until used
 template <typename Th, int KB>
-__device__ __forceinline__ void load_block(const Th* p, float* o) {
-    if constexpr (sizeof(Th) == 2) {
-        static_assert(KB % 4 == 0, "KB");
-        if constexpr (KB >= 8) {
+struct Raw {
+    static constexpr int NB = KB * (int)sizeof(Th);  // 8..64 bytes
+    static constexpr int ND = NB / 4;
+    uint32_t d[ND];
+    __device__ __forceinline__ void load(const Th* p) {
+        if constexpr (NB % 16 == 0) {
 #pragma unroll
-            for (int c = 0; c < KB / 8; ++c) {
+            for (int c = 0; c < NB / 16; ++c) {
                 const u32x4 v = reinterpret_cast<const u32x4*>(p)[c];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    o[8 * c + 2 * i] = bf16_lo(v[i]);
-                    o[8 * c + 2 * i + 1] = bf16_hi(v[i]);
-                }
+                d[4 * c] = v[0];
+                d[4 * c + 1] = v[1];
+                d[4 * c + 2] = v[2];
+                d[4 * c + 3] = v[3];
             }
         } else {
             const uint2 v = *reinterpret_cast<const uint2*>(p);
-            o[0] = bf16_lo(v.x);
-            o[1] = bf16_hi(v.x);
-            o[2] = bf16_lo(v.y);
-            o[3] = bf16_hi(v.y);
-        }
-    } else {
-#pragma unroll
-        for (int c = 0; c < KB / 4; ++c) {
-            const f32x4 v = reinterpret_cast<const f32x4*>(p)[c];
-            o[4 * c] = v[0];
-            o[4 * c + 1] = v[1];
-            o[4 * c + 2] = v[2];
-            o[4 * c + 3] = v[3];
+            d[0] = v.x;
+            d[1] = v.y;
         }
     }
-}
+    __device__ __forceinline__ float operator[](int k) const {
+        if constexpr (sizeof(Th) == 2)
+            return (k & 1) ? bf16_hi(d[k >> 1]) : bf16_lo(d[k >> 1]);
+        else
+            return __uint_as_float(d[k]);
+    }
+};
 
 template <typename Th, int KB>
 __device__ __forceinline__ void store_block(Th* p, const float* v) {
@@ -142,106 +146,290 @@ __device__ __forceinline__ void scan_rows(float* A, int T) {
     }
 }
 
-constexpr int kRB = 4;  // rays per thread per batch: their global loads are issued together
+// The RPT rays a thread owns (r = tid + 256*u) and their w / delay
+template <int RPT>
+struct Rays {
+    float w[RPT];
+    int d[RPT];
+    __device__ __forceinline__ void load(const float* __restrict__ wp, const int32_t* __restrict__ dp,
+                                         int b, int s, int R, int S) {
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) {
+            const int r = threadIdx.x + kThreads * u;
+            const int64_t i = ((int64_t)b * R + min(r, R - 1)) * S + s;
+            w[u] = wp[i];
+            d[u] = r < R ? dp[i] : 0x7fffffff;  // spare slots are never live
+        }
+    }
+};
 
-// w / delay of the rays of column (b, s) into LDS
-__device__ __forceinline__ void stage_rays(const float* __restrict__ w, const int32_t* __restrict__ delay,
-                                           int b, int s, int R, int S, float* wl, int* dl) {
-    for (int rb = 0; rb < R; rb += kThreads * kRB) {
-        float wv[kRB];
-        int dv[kRB];
+template <typename Th, int KB, int RPT>
+__device__ __forceinline__ void load_rows(Raw<Th, KB> (&v)[RPT], const Th* __restrict__ h, int64_t hrow0,
+                                          int64_t hstride, int k0, int R) {
 #pragma unroll
-        for (int u = 0; u < kRB; ++u) {
-            const int rc = min(rb + (int)threadIdx.x + kThreads * u, R - 1);
-            const int64_t i = ((int64_t)b * R + rc) * S + s;
-            wv[u] = w[i];
-            dv[u] = delay[i];
-        }
+    for (int u = 0; u < RPT; ++u)
+        v[u].load(h + hrow0 + (int64_t)min((int)threadIdx.x + kThreads * u, R - 1) * hstride + k0);
+}
+
+template <typename Th, int KB, int NT>
+__device__ __forceinline__ void load_wrows(Raw<Th, KB> (&v)[NT], const Th* __restrict__ W, int K, int k0,
+                                           int T) {
 #pragma unroll
-        for (int u = 0; u < kRB; ++u) {
-            const int r = rb + threadIdx.x + kThreads * u;
-            if (r < R) {
-                wl[r] = wv[u];
-                dl[r] = dv[u];
-            }
-        }
+    for (int i = 0; i < NT; ++i) v[i].load(W + (int64_t)min((int)threadIdx.x + kThreads * i, T - 1) * K + k0);
+}
+
+// Runs of equal keys over the lanes of a wavefront (consecutive rays have
+// slowly changing delays): the run's first lane, last lane and whether this
+// lane ends its run.
+struct Run {
+    int first, last;
+    bool tail;
+};
+__device__ __forceinline__ Run lane_run(int key) {
+    const int lane = threadIdx.x & 63;
+    const int prev = __shfl_up(key, 1, 64);
+    const bool head = lane == 0 || prev != key;
+    const unsigned long long heads = __ballot(head);
+    const unsigned long long upto = (lane == 63) ? ~0ull : ((2ull << lane) - 1);
+    Run r;
+    r.first = 63 - __clzll(heads & upto);
+    const unsigned long long later = heads & ~upto;
+    r.last = later ? (__ffsll((long long)later) - 2) : 63;
+    r.tail = r.last == lane;
+    return r;
+}
+
+// In-place exclusive prefix sum of cnt[0..T) (ints): contiguous segments per
+// thread, segment totals scanned through the wavefronts and 4 LDS slots.
+__device__ __forceinline__ void block_exclusive_scan(int* cnt, int T, int* wtot) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int seg = (T + kThreads - 1) / kThreads;
+    const int lo = threadIdx.x * seg, hi = min(T, lo + seg);
+    int tot = 0;
+    for (int t = lo; t < hi; ++t) tot += cnt[t];
+    int x = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wtot[wave] = x;
+    lds_barrier();
+    int off = x - tot;  // exact for ints
+    for (int w = 0; w < wave; ++w) off += wtot[w];
+    for (int t = lo; t < hi; ++t) {
+        const int c = cnt[t];
+        cnt[t] = off;
+        off += c;
     }
 }
 
-// A[k][t] = sum_{r: d_r = t < lim} w_r h[r, k0+k]  (LDS float atomics), then
-// the inclusive prefix over t.  The kRB rays of a thread are loaded together.
-template <typename Th, int KB>
-__device__ __forceinline__ void build_prefix(const Th* __restrict__ h, int64_t hrow0, int64_t hstride,
-                                             int k0, int R, int lim, const float* wl, const int* dl,
-                                             float* A, int T) {
-    for (int i = threadIdx.x; i < KB * T; i += kThreads) A[i] = 0.0f;
-    __syncthreads();
-    for (int rb = 0; rb < R; rb += kThreads * kRB) {
-        float v[kRB][KB];
+// Rays of column (b, s) with a non-empty window (d < lim), counting-sorted
+// by delay into LDS: perm[p] = ray, ws[p] = its weight, and afterwards
+// cnt[t] = number of those rays with delay <= t.  Returns that number.
+template <int RPT>
+__device__ __forceinline__ int sort_rays(const Rays<RPT>& rays, int lim, int T, int* cnt, int* perm,
+                                         float* ws, int* wtot) {
+    const int lane = threadIdx.x & 63;
+    for (int t = threadIdx.x; t < T; t += kThreads) cnt[t] = 0;
+    lds_barrier();
 #pragma unroll
-        for (int u = 0; u < kRB; ++u) {
-            const int rc = min(rb + (int)threadIdx.x + kThreads * u, R - 1);
-            load_block<Th, KB>(h + hrow0 + (int64_t)rc * hstride + k0, v[u]);
-        }
+    for (int u = 0; u < RPT; ++u) {
+        const int d = rays.d[u];
+        const bool live = d < lim;
+        const Run run = lane_run(live ? d : -1);
+        if (run.tail && live) atomicAdd(&cnt[d], run.last - run.first + 1);
+    }
+    lds_barrier();
+    block_exclusive_scan(cnt, T, wtot);
+    lds_barrier();
 #pragma unroll
-        for (int u = 0; u < kRB; ++u) {
-            const int r = rb + threadIdx.x + kThreads * u;
-            if (r < R) {
-                const int d = dl[r];
-                if (d < lim) {
-                    const float wr = wl[r];
-#pragma unroll
-                    for (int k = 0; k < KB; ++k) atomicAdd(&A[k * T + d], wr * v[u][k]);
-                }
-            }
+    for (int u = 0; u < RPT; ++u) {
+        const int d = rays.d[u];
+        const bool live = d < lim;
+        const Run run = lane_run(live ? d : -1);
+        int base = 0;
+        if (run.tail && live) base = atomicAdd(&cnt[d], run.last - run.first + 1);
+        base = __shfl(base, run.last, 64);
+        if (live) {
+            const int pos = base + lane - run.first;
+            perm[pos] = threadIdx.x + kThreads * u;
+            ws[pos] = rays.w[u];
         }
     }
-    __syncthreads();
-    scan_rows<KB, false>(A, T);
-    __syncthreads();
+    lds_barrier();
+    return T > 0 ? cnt[T - 1] : 0;
 }
 
-constexpr int kMaxTPer = 16;  // T <= 4096: t slots per thread NT in {4, 8, 16}
+// C[k][p] (row stride R+1) = sum of w h[k] over the first p sorted rays,
+// i.e. P[k][t] = C[k][cnt[t]].  Thread j owns sorted positions
+// j*spt .. j*spt+spt-1; its h rows (hv, already loaded) are summed locally,
+// the per-thread totals scanned across the block.
+template <typename Th, int KB, int RPT>
+__device__ __forceinline__ void build_cumsum(float* C, int R, int n, int spt, const float (&wr)[RPT],
+                                             const Raw<Th, KB> (&hv)[RPT], float* wtotf) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int p0 = threadIdx.x * spt;
+    float pre[RPT][KB];
+    float run[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) run[k] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+            run[k] = fmaf(wr[u], hv[u][k], run[k]);
+            pre[u][k] = run[k];
+        }
+    }
+    // exclusive scan of run[k] over the 256 threads
+    float off[KB];
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+        float x = run[k];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const float y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        float ex = __shfl_up(x, 1, 64);
+        if (lane == 0) ex = 0.0f;
+        off[k] = ex;
+        if (lane == 63) wtotf[wave * KB + k] = x;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+        float o = 0.0f;
+        for (int w = 0; w < wave; ++w) o += wtotf[w * KB + k];
+        off[k] += o;
+    }
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int k = 0; k < KB; ++k) C[k * (R + 1)] = 0.0f;
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int p = p0 + u;
+        if (u < spt && p < n)
+#pragma unroll
+            for (int k = 0; k < KB; ++k) C[k * (R + 1) + p + 1] = off[k] + pre[u][k];
+    }
+}
+
+// The sorted positions a thread owns (p = tid*spt + u, u < spt): the ray and
+// its weight (0 for positions past n), from the avr_head_sort tables.
+template <int RPT>
+struct Owned {
+    int ray[RPT];
+    float w[RPT];
+    int n, spt;
+    __device__ __forceinline__ void load(const int* __restrict__ perm, const float* __restrict__ ws,
+                                         const int* __restrict__ cnt, int T) {
+        n = cnt[T - 1];
+        spt = (n + kThreads - 1) / kThreads;  // <= RPT
+#pragma unroll
+        for (int u = 0; u < RPT; ++u) {
+            const int p = threadIdx.x * spt + u;
+            const bool ok = u < spt && p < n;
+            ray[u] = ok ? perm[p] : 0;
+            w[u] = ok ? ws[p] : 0.0f;
+        }
+    }
+};
+
+template <typename Th, int KB, int RPT>
+__device__ __forceinline__ void load_sorted_rows(Raw<Th, KB> (&v)[RPT], const Th* __restrict__ h, int64_t hrow0,
+                                                 int64_t hstride, int k0, const Owned<RPT>& own) {
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) v[u].load(h + hrow0 + (int64_t)own.ray[u] * hstride + k0);
+}
+
+// LDS of the cumulative-sum kernels: C[KB][R+1] | wave totals
+__host__ __device__ constexpr size_t cumsum_lds_bytes(int R, int KB) {
+    return 4 * ((size_t)KB * (R + 1) + 4 * (size_t)KB);
+}
+
+// Counting sort of the rays of every column (b, s) by delay (rays with an
+// empty window, d >= lim, dropped): perm / ws [B][S][R] and
+// cnt[B][S][T] = number of kept rays with delay <= t.  Shared by the forward
+// feature groups and by both backward kernels.
+template <int RPT>
+__global__ __launch_bounds__(kThreads) void head_sort_kernel(avr_render_params pp, int R,
+                                                             const float* __restrict__ w,
+                                                             const int32_t* __restrict__ delay,
+                                                             int* __restrict__ perm_out,
+                                                             float* __restrict__ ws_out,
+                                                             int* __restrict__ cnt_out) {
+    extern __shared__ float lds_f[];
+    const int T = pp.T, S = pp.n_samples;
+    const int s = blockIdx.x, b = blockIdx.y;
+    int* cnt = reinterpret_cast<int*>(lds_f);
+    int* perm = cnt + T;
+    float* ws = reinterpret_cast<float*>(perm + R);
+    int* wtot = reinterpret_cast<int*>(ws + R);
+    Rays<RPT> rays;
+    rays.load(w, delay, b, s, R, S);
+    const int n = sort_rays<RPT>(rays, tail_limit(pp, s), T, cnt, perm, ws, wtot);
+    const int64_t col = (int64_t)b * S + s;
+    for (int p = threadIdx.x; p < R; p += kThreads) {
+        perm_out[col * R + p] = p < n ? perm[p] : 0;
+        ws_out[col * R + p] = p < n ? ws[p] : 0.0f;
+    }
+    for (int t = threadIdx.x; t < T; t += kThreads) cnt_out[col * T + t] = cnt[t];
+}
 
 // ------------------------------------------------------------------ forward
-template <typename Th, int KB, int NT>
+// Per (feature group, s, b): rays counting-sorted by delay once; per feature
+// block, cumulative sums over the sorted rays (no float atomics), then
+// z[t] += sum_k W[t,k] C[k][cnt[t]].  The next block's h rows and W rows are
+// loaded as soon as the current ones are consumed (LDS-only barriers keep
+// them in flight).
+template <typename Th, int KB, int NT, int RPT>
 __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp, int B, int R, int K,
                                                             int KG, const Th* __restrict__ h,
                                                             const Th* __restrict__ W,
-                                                            const float* __restrict__ w,
-                                                            const int32_t* __restrict__ delay,
-                                                            float* __restrict__ zpart) {
-    extern __shared__ float lds_h[];
+                                                            const int* __restrict__ perm,
+                                                            const float* __restrict__ ws,
+                                                            const int* __restrict__ cnt,
+                                                            float* __restrict__ zpart, int dbg) {
+    extern __shared__ float lds_f[];
     const int T = pp.T, S = pp.n_samples;
     const int kg = blockIdx.x, s = blockIdx.y, b = blockIdx.z;
-    float* A = lds_h;                        // [KB][T]
-    float* wl = lds_h + KB * T;              // [R]
-    int* dl = reinterpret_cast<int*>(wl + R);
+    float* C = lds_f;                  // [KB][R+1]
+    float* wtotf = C + KB * (R + 1);   // [4][KB]
     const int lim = tail_limit(pp, s);
-    stage_rays(w, delay, b, s, R, S, wl, dl);
+    const int64_t col = (int64_t)b * S + s;
+    const int64_t hrow0 = ((int64_t)b * R * S + s) * K;
+    const int64_t hstride = (int64_t)S * K;
+    const int kbeg = kg * KG, kend = kbeg + KG;
+    Raw<Th, KB> wt[NT];
+    load_wrows<Th, KB, NT>(wt, W, K, kbeg, T);
+    Owned<RPT> own;
+    own.load(perm + col * R, ws + col * R, cnt + col * T, T);
+    int ct[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) ct[i] = cnt[col * T + min((int)threadIdx.x + kThreads * i, T - 1)];
+    Raw<Th, KB> hv[RPT];
+    load_sorted_rows<Th, KB, RPT>(hv, h, hrow0, hstride, kbeg, own);
     float zacc[NT];
 #pragma unroll
     for (int i = 0; i < NT; ++i) zacc[i] = 0.0f;
-    const int64_t hrow0 = ((int64_t)b * R * S + s) * K;
-    const int64_t hstride = (int64_t)S * K;
-    for (int k0 = kg * KG; k0 < (kg + 1) * KG; k0 += KB) {
-        // this block's W rows, in flight while the prefix is built
-        float wt[NT][KB];
-#pragma unroll
-        for (int i = 0; i < NT; ++i)
-            load_block<Th, KB>(W + (int64_t)min((int)threadIdx.x + kThreads * i, T - 1) * K + k0, wt[i]);
-        __syncthreads();
-        build_prefix<Th, KB>(h, hrow0, hstride, k0, R, lim, wl, dl, A, T);
+    for (int k0 = kbeg; k0 < kend; k0 += KB) {
+        if (!(dbg & 1)) build_cumsum<Th, KB, RPT>(C, R, own.n, own.spt, own.w, hv, wtotf);
+        if (k0 + KB < kend) load_sorted_rows<Th, KB, RPT>(hv, h, hrow0, hstride, k0 + KB, own);
+        lds_barrier();
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
             const int t = threadIdx.x + kThreads * i;
-            if (t < lim) {
+            if (t < lim && !(dbg & 4)) {
                 float a = zacc[i];
 #pragma unroll
-                for (int k = 0; k < KB; ++k) a = fmaf(wt[i][k], A[k * T + t], a);
+                for (int k = 0; k < KB; ++k) a = fmaf(wt[i][k], C[k * (R + 1) + ct[i]], a);
                 zacc[i] = a;
             }
         }
+        if (k0 + KB < kend) load_wrows<Th, KB, NT>(wt, W, K, k0 + KB, T);
+        lds_barrier();  // C and wtotf are rewritten by the next block
     }
     float* out = zpart + (((int64_t)kg * B + b) * S + s) * T;
 #pragma unroll
@@ -252,7 +440,7 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp
 }
 
 // ------------------------------------------------- backward: dL/dh, dL/dw
-template <typename Th, int KB, int NT>
+template <typename Th, int KB, int NT, int RPT>
 __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params pp, int B, int R, int K,
                                                               int KG, const Th* __restrict__ h,
                                                               const Th* __restrict__ W,
@@ -261,16 +449,15 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
                                                               const float* __restrict__ gz,
                                                               Th* __restrict__ grad_h,
                                                               float* __restrict__ gw_part) {
-    extern __shared__ float lds_h[];
+    extern __shared__ float Q[];  // [KB][T]
     const int T = pp.T, S = pp.n_samples;
     const int kg = blockIdx.x, s = blockIdx.y, b = blockIdx.z;
-    float* Q = lds_h;                        // [KB][T]
-    float* wl = lds_h + KB * T;              // [R]
-    int* dl = reinterpret_cast<int*>(wl + R);
-    float* gwl = wl + 2 * R;                 // [R] dL/dw partial (each ray owned by one thread)
     const int lim = tail_limit(pp, s);
-    stage_rays(w, delay, b, s, R, S, wl, dl);
-    for (int r = threadIdx.x; r < R; r += kThreads) gwl[r] = 0.0f;
+    const int64_t hrow0 = ((int64_t)b * R * S + s) * K;
+    const int64_t hstride = (int64_t)S * K;
+    const int kbeg = kg * KG, kend = kbeg + KG;
+    Rays<RPT> rays;
+    rays.load(w, delay, b, s, R, S);
     const float* gzr = gz + ((int64_t)b * S + s) * T;
     float g[NT];
 #pragma unroll
@@ -279,14 +466,14 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
         const float v = gzr[min(t, T - 1)];
         g[i] = t < lim ? v : 0.0f;
     }
-    const int64_t hrow0 = ((int64_t)b * R * S + s) * K;
-    const int64_t hstride = (int64_t)S * K;
-    for (int k0 = kg * KG; k0 < (kg + 1) * KG; k0 += KB) {
-        float wt[NT][KB];
+    Raw<Th, KB> hv[RPT], wt[NT];
+    load_wrows<Th, KB, NT>(wt, W, K, kbeg, T);
+    load_rows<Th, KB, RPT>(hv, h, hrow0, hstride, kbeg, R);
+    float gw[RPT];
 #pragma unroll
-        for (int i = 0; i < NT; ++i)
-            load_block<Th, KB>(W + (int64_t)min((int)threadIdx.x + kThreads * i, T - 1) * K + k0, wt[i]);
-        __syncthreads();
+    for (int u = 0; u < RPT; ++u) gw[u] = 0.0f;
+    for (int k0 = kbeg; k0 < kend; k0 += KB) {
+        lds_barrier();
         // u[k][t] = gz[t] W[t][k], then the suffix sum over t
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
@@ -295,87 +482,105 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
 #pragma unroll
                 for (int k = 0; k < KB; ++k) Q[k * T + t] = g[i] * wt[i][k];
         }
-        __syncthreads();
+        if (k0 + KB < kend) load_wrows<Th, KB, NT>(wt, W, K, k0 + KB, T);
+        lds_barrier();
         scan_rows<KB, true>(Q, T);
-        __syncthreads();
-        for (int rb = 0; rb < R; rb += kThreads * kRB) {
-            float hv[kRB][KB];
+        lds_barrier();
 #pragma unroll
-            for (int u = 0; u < kRB; ++u) {
-                const int rc = min(rb + (int)threadIdx.x + kThreads * u, R - 1);
-                load_block<Th, KB>(h + hrow0 + (int64_t)rc * hstride + k0, hv[u]);
-            }
+        for (int u = 0; u < RPT; ++u) {
+            const int r = threadIdx.x + kThreads * u;
+            if (r < R) {
+                const int d = rays.d[u];
+                float gh[KB];
+                if (d < lim) {
+                    const float wr = rays.w[u];
+                    float acc = gw[u];
 #pragma unroll
-            for (int u = 0; u < kRB; ++u) {
-                const int r = rb + threadIdx.x + kThreads * u;
-                if (r < R) {
-                    const int d = dl[r];
-                    float gh[KB];
-                    if (d < lim) {
-                        const float wr = wl[r];
-                        float acc = 0.0f;
-#pragma unroll
-                        for (int k = 0; k < KB; ++k) {
-                            const float q = Q[k * T + d];
-                            gh[k] = wr * q;
-                            acc = fmaf(hv[u][k], q, acc);
-                        }
-                        gwl[r] += acc;
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < KB; ++k) gh[k] = 0.0f;
+                    for (int k = 0; k < KB; ++k) {
+                        const float q = Q[k * T + d];
+                        gh[k] = wr * q;
+                        acc = fmaf(hv[u][k], q, acc);
                     }
-                    store_block<Th, KB>(grad_h + hrow0 + (int64_t)r * hstride + k0, gh);
+                    gw[u] = acc;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < KB; ++k) gh[k] = 0.0f;
                 }
+                store_block<Th, KB>(grad_h + hrow0 + (int64_t)r * hstride + k0, gh);
             }
         }
+        if (k0 + KB < kend) load_rows<Th, KB, RPT>(hv, h, hrow0, hstride, k0 + KB, R);
     }
-    __syncthreads();
-    for (int r = threadIdx.x; r < R; r += kThreads)
-        gw_part[(((int64_t)kg * B + b) * R + r) * S + s] = gwl[r];
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int r = threadIdx.x + kThreads * u;
+        if (r < R) gw_part[(((int64_t)kg * B + b) * R + r) * S + s] = gw[u];
+    }
 }
 
 // ---------------------------------------------------- backward: dL/dW
 // One workgroup per (feature block, sample group, b): for each of its
-// samples, rebuild P (as the forward) and accumulate gz[t] * P[k][t] in
-// registers; one [T][KB] partial per workgroup.
-template <typename Th, int KB, int NT>
+// samples, sort the rays, build the cumulative sums C (as the forward) and
+// accumulate gz[t] C[k][cnt[t]] in registers; one [T][KB] partial per
+// workgroup.  The next sample's rays and gz are loaded during the current one.
+template <typename Th, int KB, int NT, int RPT>
 __global__ __launch_bounds__(kThreads) void head_bwd_w_kernel(avr_render_params pp, int B, int R, int K,
                                                               int s_per_group,
                                                               const Th* __restrict__ h,
-                                                              const float* __restrict__ w,
-                                                              const int32_t* __restrict__ delay,
+                                                              const int* __restrict__ perm,
+                                                              const float* __restrict__ ws,
+                                                              const int* __restrict__ cnt,
                                                               const float* __restrict__ gz,
                                                               float* __restrict__ gW_part) {
-    extern __shared__ float lds_h[];
+    extern __shared__ float lds_f[];
     const int T = pp.T, S = pp.n_samples;
     const int kb = blockIdx.x, sg = blockIdx.y, b = blockIdx.z;
     const int k0 = kb * KB;
-    float* A = lds_h;
-    float* wl = lds_h + KB * T;
-    int* dl = reinterpret_cast<int*>(wl + R);
+    float* C = lds_f;
+    float* wtotf = C + KB * (R + 1);
+    const int64_t hstride = (int64_t)S * K;
     float acc[NT][KB];
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll
         for (int k = 0; k < KB; ++k) acc[i][k] = 0.0f;
     const int s_lo = sg * s_per_group, s_hi = min(S, s_lo + s_per_group);
+    Owned<RPT> own;
+    Raw<Th, KB> hv[RPT];
+    float g[NT];
+    int ct[NT];
+    auto prefetch = [&](int s) {
+        const int64_t col = (int64_t)b * S + s;
+        own.load(perm + col * R, ws + col * R, cnt + col * T, T);
+        load_sorted_rows<Th, KB, RPT>(hv, h, ((int64_t)b * R * S + s) * K, hstride, k0, own);
+        const float* gzr = gz + col * T;
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            const int tc = min((int)threadIdx.x + kThreads * i, T - 1);
+            g[i] = gzr[tc];
+            ct[i] = cnt[col * T + tc];
+        }
+    };
+    if (s_lo < s_hi) prefetch(s_lo);
     for (int s = s_lo; s < s_hi; ++s) {
         const int lim = tail_limit(pp, s);
-        const float* gzr = gz + ((int64_t)b * S + s) * T;
-        float g[NT];
+        lds_barrier();  // the previous sample is done with C
+        build_cumsum<Th, KB, RPT>(C, R, own.n, own.spt, own.w, hv, wtotf);
+        float gc[NT];
+        int cc[NT];
 #pragma unroll
-        for (int i = 0; i < NT; ++i) g[i] = gzr[min((int)threadIdx.x + kThreads * i, T - 1)];
-        __syncthreads();
-        stage_rays(w, delay, b, s, R, S, wl, dl);
-        __syncthreads();
-        build_prefix<Th, KB>(h, ((int64_t)b * R * S + s) * K, (int64_t)S * K, k0, R, lim, wl, dl, A, T);
+        for (int i = 0; i < NT; ++i) {
+            gc[i] = g[i];
+            cc[i] = ct[i];
+        }
+        if (s + 1 < s_hi) prefetch(s + 1);
+        lds_barrier();
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
             const int t = threadIdx.x + kThreads * i;
             if (t < lim) {
 #pragma unroll
-                for (int k = 0; k < KB; ++k) acc[i][k] = fmaf(g[i], A[k * T + t], acc[i][k]);
+                for (int k = 0; k < KB; ++k) acc[i][k] = fmaf(gc[i], C[k * (R + 1) + cc[i]], acc[i][k]);
             }
         }
     }
@@ -408,34 +613,41 @@ __global__ __launch_bounds__(256) void sum_parts_kernel(int64_t n, int parts, co
 
 // ----------------------------------------------------------- launch shapes
 struct HeadShape {
-    int nt;      // t slots per thread (4, 8 or 16)
-    int kb;      // features per LDS block (4, 8 or 16)
-    int n_kg;    // feature groups = DFT partials (power of two <= 16)
-    int kg;      // features per group
-    size_t lds;  // bytes
+    int rpt;            // rays per thread (4, 8 or 16)
+    int nt;             // t slots per thread (4, 8 or 16)
+    int kb;             // features per block (4, 8 or 16)
+    int n_kg;           // forward feature groups = DFT partials (power of two <= 16)
+    int kg;             // features per group
+    size_t lds_q;       // head_bwd_h: Q[kb][T]
+    size_t lds_c;       // head_fwd / head_bwd_w: C[kb][R+1]
+    size_t lds_sort;    // head_sort: cnt[T], perm[R], ws[R]
 };
 
 int head_shape(const avr_render_params& p, int B, int R, int K, int es, HeadShape* hs) {
     const int T = p.T, S = p.n_samples;
-    if (T > kThreads * kMaxTPer) return fail(AVR_E_CONFIG, "fused head: T > 4096 not supported");
+    if (T > kThreads * 16) return fail(AVR_E_CONFIG, "fused head: T > 4096 not supported");
     if (R > kThreads * 16) return fail(AVR_E_CONFIG, "fused head: more than 4096 rays per shard");
-    const size_t ray_bytes = (size_t)R * 12;  // w, delay (+ dL/dw in the backward)
-    int kb = 16;
-    // two workgroups per CU when the block fits 80 KiB; 16-byte row loads
     const int nt = T <= 1024 ? 4 : (T <= 2048 ? 8 : 16);
-    while (kb > 4 && ((size_t)kb * T * 4 + ray_bytes > 80 * 1024 || kb * nt > 64)) kb /= 2;
-    if ((size_t)kb * T * 4 + ray_bytes > 150 * 1024)
+    // feature block: prefetched W rows in registers (kb*nt <= 64), and the
+    // backward's Q[kb][T] in <= 80 KiB of LDS (two workgroups per CU)
+    int kb = 16;
+    while (kb > 4 && ((size_t)kb * T * 4 > 80 * 1024 || kb * nt > 64)) kb /= 2;
+    const size_t lds_sort = 4 * ((size_t)T + 2 * (size_t)R + 4);
+    if ((size_t)kb * T * 4 > 150 * 1024 || cumsum_lds_bytes(R, kb) > 150 * 1024 || lds_sort > 150 * 1024)
         return fail(AVR_E_CONFIG, "fused head: T x rays too large for LDS");
     if (K % kb != 0 || (kb * es) % 8 != 0)
         return fail(AVR_E_CONFIG, "fused head: hidden width must be a multiple of the feature block");
     int n = 1;
     const int64_t cols = (int64_t)B * S;
     while (n < 16 && cols * n < 1024 && (K / (2 * n)) % kb == 0 && K % (2 * n) == 0) n *= 2;
+    hs->rpt = R <= 4 * kThreads ? 4 : (R <= 8 * kThreads ? 8 : 16);
     hs->nt = nt;
     hs->kb = kb;
     hs->n_kg = n;
     hs->kg = K / n;
-    hs->lds = (size_t)kb * T * 4 + ray_bytes;
+    hs->lds_q = (size_t)kb * T * 4;
+    hs->lds_c = cumsum_lds_bytes(R, kb);
+    hs->lds_sort = lds_sort;
     return 0;
 }
 
@@ -454,6 +666,15 @@ int head_check(const avr_render_params* p, int B, int K, const void* h, const vo
     return 0;
 }
 
+// dW workgroups: (feature block, sample group, b), ~1024 of them
+void dw_groups(const HeadShape& hs, int B, int S, int K, int* n_sg, int* s_per) {
+    const int nkb = K / hs.kb;
+    int n = 1;
+    while (n < S && (int64_t)nkb * n * B < 1024) n *= 2;
+    *s_per = (S + n - 1) / n;
+    *n_sg = (S + *s_per - 1) / *s_per;
+}
+
 }  // namespace
 
 extern "C" int avr_head_splits(const avr_render_params* p, int32_t B, int32_t K, int32_t dtype,
@@ -466,85 +687,120 @@ extern "C" int avr_head_splits(const avr_render_params* p, int32_t B, int32_t K,
     return 0;
 }
 
+extern "C" int avr_head_sort(const avr_render_params* p, int32_t B, const float* w, const int32_t* delay,
+                             int32_t* perm, float* ws, int32_t* cnt, void* stream) {
+    AVR_REQUIRE(p && B >= 1 && w && delay && perm && ws && cnt, "avr_head_sort: bad args");
+    const int R = n_rays(*p);
+    HeadShape hs;
+    if (int e = head_shape(*p, B, R, 16, 4, &hs)) return e;
+    hipStream_t st = as_stream(stream);
+    const dim3 grid(p->n_samples, B);
+    auto go = [&](auto kern) {
+        allow_lds(kern, hs.lds_sort);
+        hipLaunchKernelGGL(kern, grid, dim3(kThreads), hs.lds_sort, st, *p, R, w, delay, perm, ws, cnt);
+    };
+    if (hs.rpt == 4)
+        go(head_sort_kernel<4>);
+    else if (hs.rpt == 8)
+        go(head_sort_kernel<8>);
+    else
+        go(head_sort_kernel<16>);
+    return check_launch("avr_head_sort");
+}
+
 extern "C" int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, const void* h,
-                            const void* W, int32_t dtype, const float* w, const int32_t* delay,
-                            int32_t n_split, float* zpart, void* stream) {
+                            const void* W, int32_t dtype, const int32_t* perm, const float* ws,
+                            const int32_t* cnt, int32_t n_split, float* zpart, void* stream) {
     if (int e = head_check(p, B, K, h, W, dtype)) return e;
-    AVR_REQUIRE(w && delay && zpart, "avr_head_fwd: bad args");
+    AVR_REQUIRE(perm && ws && cnt && zpart, "avr_head_fwd: bad args");
     const int R = n_rays(*p);
     HeadShape hs;
     if (int e = head_shape(*p, B, R, K, dtype == AVR_DTYPE_BF16 ? 2 : 4, &hs)) return e;
     AVR_REQUIRE(n_split == hs.n_kg, "avr_head_fwd: n_split must come from avr_head_splits");
     const dim3 grid(hs.n_kg, p->n_samples, B);
     hipStream_t st = as_stream(stream);
+    const char* dbg_env = getenv("AVR_HEAD_DBG");  // profiling only: skip phases
+    const int dbg = dbg_env ? atoi(dbg_env) : 0;
     auto go = [&](auto kern, auto hp, auto wp) {
-        allow_lds(kern, hs.lds);
-        hipLaunchKernelGGL(kern, grid, dim3(kThreads), hs.lds, st, *p, (int)B, R, (int)K, hs.kg, hp, wp, w,
-                           delay, zpart);
+        allow_lds(kern, hs.lds_c);
+        hipLaunchKernelGGL(kern, grid, dim3(kThreads), hs.lds_c, st, *p, (int)B, R, (int)K, hs.kg, hp, wp,
+                           perm, ws, cnt, zpart, dbg);
     };
-#define AVR_HF(TH, KBV, NTV)                                                                       \
-    if (hs.kb == KBV && hs.nt == NTV) go(head_fwd_kernel<TH, KBV, NTV>, (const TH*)h, (const TH*)W);
+#define AVR_HF(TH, KBV, NTV, RP)                                                                   \
+    if (hs.kb == KBV && hs.nt == NTV && hs.rpt == RP)                                              \
+        go(head_fwd_kernel<TH, KBV, NTV, RP>, (const TH*)h, (const TH*)W);
+#define AVR_HF_R(TH, KBV, NTV) AVR_HF(TH, KBV, NTV, 4) AVR_HF(TH, KBV, NTV, 8) AVR_HF(TH, KBV, NTV, 16)
 #define AVR_HF_ALL(TH)                                                                             \
-    AVR_HF(TH, 4, 4) AVR_HF(TH, 4, 8) AVR_HF(TH, 4, 16) AVR_HF(TH, 8, 4) AVR_HF(TH, 8, 8)          \
-    AVR_HF(TH, 16, 4)
+    AVR_HF_R(TH, 4, 4) AVR_HF_R(TH, 4, 8) AVR_HF_R(TH, 4, 16) AVR_HF_R(TH, 8, 4) AVR_HF_R(TH, 8, 8) \
+    AVR_HF_R(TH, 16, 4)
     if (dtype == AVR_DTYPE_BF16) {
         AVR_HF_ALL(__hip_bfloat16)
     } else {
         AVR_HF_ALL(float)
     }
+#undef AVR_HF_R
 #undef AVR_HF_ALL
 #undef AVR_HF
     return check_launch("avr_head_fwd");
 }
 
-extern "C" int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, const void* h,
-                            const void* W, int32_t dtype, const float* w, const int32_t* delay,
-                            const float* gz, void* grad_h, float* grad_w, float* grad_W,
-                            float* workspace, int64_t workspace_bytes, void* stream) {
-    if (int e = head_check(p, B, K, h, W, dtype)) return e;
-    AVR_REQUIRE(w && delay && gz && grad_h && grad_w && grad_W && workspace, "avr_head_bwd: bad args");
+extern "C" int avr_head_bwd_workspace(const avr_render_params* p, int32_t B, int32_t K, int32_t dtype,
+                                      int64_t* bytes) {
+    AVR_REQUIRE(p && bytes, "avr_head_bwd_workspace: bad args");
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
     HeadShape hs;
     if (int e = head_shape(*p, B, R, K, dtype == AVR_DTYPE_BF16 ? 2 : 4, &hs)) return e;
-    // dW: (feature block, sample group, b) workgroups, ~1024 of them
-    const int nkb = K / hs.kb;
-    int n_sg = 1;
-    while (n_sg < S && (int64_t)nkb * n_sg * B < 1024) n_sg *= 2;
-    const int s_per = (S + n_sg - 1) / n_sg;
-    n_sg = (S + s_per - 1) / s_per;
-    int64_t need = 0;
-    AVR_REQUIRE(workspace_bytes >= 0, "avr_head_bwd: bad workspace size");
+    int n_sg, s_per;
+    dw_groups(hs, B, S, K, &n_sg, &s_per);
+    *bytes = ((int64_t)hs.n_kg * B * R * S + (int64_t)B * n_sg * T * K) * 4;
+    return 0;
+}
+
+extern "C" int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, const void* h,
+                            const void* W, int32_t dtype, const float* w, const int32_t* delay,
+                            const int32_t* perm, const float* ws, const int32_t* cnt, const float* gz,
+                            void* grad_h, float* grad_w, float* grad_W, float* workspace,
+                            int64_t workspace_bytes, void* stream) {
+    if (int e = head_check(p, B, K, h, W, dtype)) return e;
+    AVR_REQUIRE(w && delay && perm && ws && cnt && gz && grad_h && grad_w && grad_W && workspace,
+                "avr_head_bwd: bad args");
+    const int R = n_rays(*p), S = p->n_samples, T = p->T;
+    HeadShape hs;
+    if (int e = head_shape(*p, B, R, K, dtype == AVR_DTYPE_BF16 ? 2 : 4, &hs)) return e;
+    int n_sg, s_per;
+    dw_groups(hs, B, S, K, &n_sg, &s_per);
     const int64_t gw_elems = (int64_t)hs.n_kg * B * R * S;
     const int64_t gW_elems = (int64_t)B * n_sg * T * K;
-    need = (gw_elems + gW_elems) * 4;
-    if (workspace_bytes < need) return fail(AVR_E_ARG, "avr_head_bwd: workspace too small");
+    if (workspace_bytes < (gw_elems + gW_elems) * 4)
+        return fail(AVR_E_ARG, "avr_head_bwd: workspace too small");
     float* gw_part = workspace;
     float* gW_part = workspace + gw_elems;
     hipStream_t st = as_stream(stream);
     auto go_h = [&](auto kern, auto hp, auto wp, auto gp) {
-        const size_t lds_h = hs.lds + (size_t)R * 4;  // + the per-ray dL/dw accumulators
-        allow_lds(kern, lds_h);
-        hipLaunchKernelGGL(kern, dim3(hs.n_kg, S, B), dim3(kThreads), lds_h, st, *p, (int)B, R, (int)K,
+        allow_lds(kern, hs.lds_q);
+        hipLaunchKernelGGL(kern, dim3(hs.n_kg, S, B), dim3(kThreads), hs.lds_q, st, *p, (int)B, R, (int)K,
                            hs.kg, hp, wp, w, delay, gz, gp, gw_part);
     };
     auto go_w = [&](auto kern, auto hp) {
-        allow_lds(kern, hs.lds);
-        hipLaunchKernelGGL(kern, dim3(nkb, n_sg, B), dim3(kThreads), hs.lds, st, *p, (int)B, R, (int)K,
-                           s_per, hp, w, delay, gz, gW_part);
+        allow_lds(kern, hs.lds_c);
+        hipLaunchKernelGGL(kern, dim3(K / hs.kb, n_sg, B), dim3(kThreads), hs.lds_c, st, *p, (int)B, R,
+                           (int)K, s_per, hp, perm, ws, cnt, gz, gW_part);
     };
-#define AVR_HB(TH, KBV, NTV)                                                                       \
-    if (hs.kb == KBV && hs.nt == NTV) {                                                            \
-        go_h(head_bwd_h_kernel<TH, KBV, NTV>, (const TH*)h, (const TH*)W, (TH*)grad_h);            \
-        go_w(head_bwd_w_kernel<TH, KBV, NTV>, (const TH*)h);                                       \
+#define AVR_HB(TH, KBV, NTV, RP)                                                                   \
+    if (hs.kb == KBV && hs.nt == NTV && hs.rpt == RP) {                                            \
+        go_h(head_bwd_h_kernel<TH, KBV, NTV, RP>, (const TH*)h, (const TH*)W, (TH*)grad_h);        \
+        go_w(head_bwd_w_kernel<TH, KBV, NTV, RP>, (const TH*)h);                                   \
     }
+#define AVR_HB_R(TH, KBV, NTV) AVR_HB(TH, KBV, NTV, 4) AVR_HB(TH, KBV, NTV, 8) AVR_HB(TH, KBV, NTV, 16)
 #define AVR_HB_ALL(TH)                                                                             \
-    AVR_HB(TH, 4, 4) AVR_HB(TH, 4, 8) AVR_HB(TH, 4, 16) AVR_HB(TH, 8, 4) AVR_HB(TH, 8, 8)          \
-    AVR_HB(TH, 16, 4)
+    AVR_HB_R(TH, 4, 4) AVR_HB_R(TH, 4, 8) AVR_HB_R(TH, 4, 16) AVR_HB_R(TH, 8, 4) AVR_HB_R(TH, 8, 8) \
+    AVR_HB_R(TH, 16, 4)
     if (dtype == AVR_DTYPE_BF16) {
         AVR_HB_ALL(__hip_bfloat16)
     } else {
         AVR_HB_ALL(float)
     }
+#undef AVR_HB_R
 #undef AVR_HB_ALL
 #undef AVR_HB
     if (int e = check_launch("avr_head_bwd")) return e;
@@ -554,19 +810,4 @@ extern "C" int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, co
     hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)((n2 + 255) / 256)), dim3(256), 0, st, n2,
                        (int)(B * n_sg), gW_part, grad_W);
     return check_launch("avr_head_bwd_sum");
-}
-
-extern "C" int avr_head_bwd_workspace(const avr_render_params* p, int32_t B, int32_t K, int32_t dtype,
-                                      int64_t* bytes) {
-    AVR_REQUIRE(p && bytes, "avr_head_bwd_workspace: bad args");
-    const int R = n_rays(*p), S = p->n_samples, T = p->T;
-    HeadShape hs;
-    if (int e = head_shape(*p, B, R, K, dtype == AVR_DTYPE_BF16 ? 2 : 4, &hs)) return e;
-    const int nkb = K / hs.kb;
-    int n_sg = 1;
-    while (n_sg < S && (int64_t)nkb * n_sg * B < 1024) n_sg *= 2;
-    const int s_per = (S + n_sg - 1) / n_sg;
-    n_sg = (S + s_per - 1) / s_per;
-    *bytes = ((int64_t)hs.n_kg * B * R * S + (int64_t)B * n_sg * T * K) * 4;
-    return 0;
 }

@@ -263,20 +263,25 @@ class FusedHeadCore(torch.autograd.Function):
         W = w_master.to(dtype).contiguous()
         code = _dtype_code(h)
         w, delay = _weights(p, attn, rays_o, position_tx, dirs, tables, st)
+        R = p.n_rays
+        perm = torch.empty(B, S, R, dtype=torch.int32, device=dev)
+        ws = torch.empty(B, S, R, dtype=torch.float32, device=dev)
+        cnt = torch.empty(B, S, T, dtype=torch.int32, device=dev)
+        _lib.call("avr_head_sort", pref, B, _ptr(w), _ptr(delay), _ptr(perm), _ptr(ws), _ptr(cnt), st)
         ns = ctypes.c_int32(0)
         _lib.call("avr_head_splits", pref, B, K, code, ctypes.byref(ns))
         n_split = ns.value
         part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
-        _lib.call("avr_head_fwd", pref, B, K, _ptr(h), _ptr(W), code, _ptr(w), _ptr(delay),
+        _lib.call("avr_head_fwd", pref, B, K, _ptr(h), _ptr(W), code, _ptr(perm), _ptr(ws), _ptr(cnt),
                   n_split, _ptr(part), st)
         out = _spectrum(p, tables, part, n_split, B, dev, st)
         ctx.p, ctx.tables = p, tables
-        ctx.save_for_backward(attn, h, W, w, delay)
+        ctx.save_for_backward(attn, h, W, w, delay, perm, ws, cnt)
         return out
 
     @staticmethod
     def backward(ctx, grad_out):
-        attn, h, W, w, delay = ctx.saved_tensors
+        attn, h, W, w, delay, perm, ws, cnt = ctx.saved_tensors
         p, tables = ctx.p, ctx.tables
         dev = h.device
         B, K = h.size(0), h.size(-1)
@@ -287,12 +292,13 @@ class FusedHeadCore(torch.autograd.Function):
         gz = _grad_z(p, tables, grad_out, B, dev, st)
         nbytes = ctypes.c_int64(0)
         _lib.call("avr_head_bwd_workspace", pref, B, K, code, ctypes.byref(nbytes))
-        ws = torch.empty(max(1, nbytes.value // 4), dtype=torch.float32, device=dev)
+        work = torch.empty(max(1, nbytes.value // 4), dtype=torch.float32, device=dev)
         grad_h = torch.empty_like(h)
         grad_w = torch.empty(B, R, S, dtype=torch.float32, device=dev)
         grad_W = torch.empty(T, K, dtype=torch.float32, device=dev)
-        _lib.call("avr_head_bwd", pref, B, K, _ptr(h), _ptr(W), code, _ptr(w), _ptr(delay), _ptr(gz),
-                  _ptr(grad_h), _ptr(grad_w), _ptr(grad_W), _ptr(ws), nbytes.value, st)
+        _lib.call("avr_head_bwd", pref, B, K, _ptr(h), _ptr(W), code, _ptr(w), _ptr(delay), _ptr(perm),
+                  _ptr(ws), _ptr(cnt), _ptr(gz), _ptr(grad_h), _ptr(grad_w), _ptr(grad_W),
+                  _ptr(work), nbytes.value, st)
         grad_attn = _grad_attn(p, tables, attn, grad_w, st) if ctx.needs_input_grad[0] else None
         return (grad_attn, grad_h if ctx.needs_input_grad[1] else None,
                 grad_W if ctx.needs_input_grad[2] else None, None, None, None, None, None, None)

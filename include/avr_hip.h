@@ -210,18 +210,24 @@ int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* grad_y, const 
  * T <= 4096 and <= 4096 rays per shard. */
 int avr_head_splits(const avr_render_params* p, int32_t B, int32_t K, int32_t dtype,
                     int32_t* n_split);
+/* Counting sort of each column's rays by delay (rays with d >= T-1-shift
+ * dropped): perm, ws [B][S][R] (ray index, weight) and cnt [B][S][T] (number
+ * of kept rays with delay <= t).  Input to avr_head_fwd and avr_head_bwd. */
+int avr_head_sort(const avr_render_params* p, int32_t B, const float* w, const int32_t* delay,
+                  int32_t* perm, float* ws, int32_t* cnt, void* stream);
 int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* W,
-                 int32_t dtype, const float* w, const int32_t* delay, int32_t n_split,
-                 float* zpart, void* stream);
+                 int32_t dtype, const int32_t* perm, const float* ws, const int32_t* cnt,
+                 int32_t n_split, float* zpart, void* stream);
 /* Backward: gz [B][S][T] (avr_dft_phase_bwd) -> grad_h [B][R][S][K] (dtype),
  * grad_w [B][R][S] fp32 (to avr_weights_bwd) and grad_W [T][K] fp32.
  * `workspace` holds avr_head_bwd_workspace() bytes of fp32 partials. */
 int avr_head_bwd_workspace(const avr_render_params* p, int32_t B, int32_t K, int32_t dtype,
                            int64_t* bytes);
 int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* W,
-                 int32_t dtype, const float* w, const int32_t* delay, const float* gz,
-                 void* grad_h, float* grad_w, float* grad_W, float* workspace,
-                 int64_t workspace_bytes, void* stream);
+                 int32_t dtype, const float* w, const int32_t* delay, const int32_t* perm,
+                 const float* ws, const int32_t* cnt, const float* gz, void* grad_h,
+                 float* grad_w, float* grad_W, float* workspace, int64_t workspace_bytes,
+                 void* stream);
 
 #ifdef __cplusplus
 }
