@@ -159,25 +159,25 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(int64_t N, int M, int
         }
 }
 
-// dW = sum over splits of the partials, in split order (deterministic).
-// 4 consecutive outputs per thread (16-byte loads), 8 splits' loads in flight.
+// dW = sum over splits of the partials.  One wavefront per 4 consecutive
+// outputs: its lanes stride over the splits (16-byte loads), then a fixed
+// shuffle tree combines them (deterministic, and no long serial chains when
+// a small layer is split many ways).
 __global__ __launch_bounds__(256) void wgrad_finalize_kernel(int64_t MK, int splits,
                                                               const float* __restrict__ partial,
                                                               float* __restrict__ out) {
-    const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-    if (i >= MK) return;  // MK % 8 == 0 (M, K multiples of 8)
+    const int lane = threadIdx.x & 63;
+    const int64_t i = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
+    if (i >= MK) return;  // wave-uniform; MK % 8 == 0
     f32x4 s = {0.0f, 0.0f, 0.0f, 0.0f};
-    int k = 0;
-    for (; k + 8 <= splits; k += 8) {
-        f32x4 v[8];
+    for (int k = lane; k < splits; k += 64)
+        s += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(partial + (int64_t)k * MK + i));
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            v[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(partial + (int64_t)(k + u) * MK + i));
+    for (int off = 32; off > 0; off >>= 1) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) s += v[u];
+        for (int c = 0; c < 4; ++c) s[c] += __shfl_xor(s[c], off, 64);
     }
-    for (; k < splits; ++k) s += *reinterpret_cast<const f32x4*>(partial + (int64_t)k * MK + i);
-    *reinterpret_cast<f32x4*>(out + i) = s;
+    if (lane == 0) *reinterpret_cast<f32x4*>(out + i) = s;
 }
 
 int wgrad_splits(int64_t N, int M, int K) {
@@ -212,7 +212,7 @@ extern "C" int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* gra
                        (const __hip_bfloat16*)grad_y, (const __hip_bfloat16*)x, workspace);
     if (int e = check_launch("avr_linear_wgrad")) return e;
     const int64_t MK = (int64_t)M * K;
-    hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)((MK / 4 + 255) / 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)((MK / 4 + 3) / 4)), dim3(256), 0, st,
                        MK, used, workspace, grad_w);
     return check_launch("avr_linear_wgrad_finalize");
 }

@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--mlp-dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--core-only", action="store_true")
     ap.add_argument("--no-fused", action="store_true", help="materialise the signal (no fused head)")
+    ap.add_argument("--foreach-adam", action="store_true", help="torch's default (foreach) Adam")
     ap.add_argument("--profile", action="store_true", help="torch.profiler table of a few steps")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -94,7 +95,9 @@ def main():
     cfg = dict(RAF_MODEL, signal_output_dim=T)
     model = AVRModel_complex(cfg, mlp_dtype=mlp_dtype).to(dev)
     r = AVRRender(model, fused_head=not args.no_fused, **w.render).to(dev)
-    opt = torch.optim.Adam(r.parameters(), lr=2e-4)
+    # same update as the reference's torch.optim.Adam (avr_runner.py), as one
+    # fused multi-tensor kernel instead of foreach chains
+    opt = torch.optim.Adam(r.parameters(), lr=2e-4, fused=not args.foreach_adam)
     target = torch.randn(B, T // 2 + 1, 2, device=dev, generator=g)
 
     def train_step():
@@ -118,6 +121,7 @@ def main():
     res["train_ray_samples_per_s"] = w.ray_samples / t
     res["mlp_dtype"] = args.mlp_dtype
     res["fused_head"] = not args.no_fused
+    res["adam"] = "foreach" if args.foreach_adam else "fused"
     print(json.dumps(res))
 
 
