@@ -37,6 +37,8 @@ for s in "$@"; do
     train) step train_c3 600 python tools/bench_train.py && step train_c4 600 python tools/bench_train.py --workload c4_raf_empty_b4_per_gpu ;;
     trainu) step trainu_c3 600 python tools/bench_train.py --no-fused && step trainu_c4 600 python tools/bench_train.py --workload c4_raf_empty_b4_per_gpu --no-fused ;;
     wgrad) for v in 1 262144 500000 819200 100000000; do AVR_WGRAD_MIN=$v step wgrad_$v 300 python tools/bench_train.py --steps 10 || exit 1; done ;;
+    infer) step infer_bf16 600 python tools/bench_infer.py && step infer_fp32 600 python tools/bench_infer.py --mlp-dtype fp32 ;;
+    profinfer) step profinfer 600 rocprofv3 --kernel-trace --stats -d $OUT/profinfer -o run --output-format csv -- python tools/bench_infer.py --steps 5 --warmup 2 ;;
     torchprof) step torchprof 600 python tools/bench_train.py --steps 5 --profile ;;
     proftrain) step proftrain 600 rocprofv3 --kernel-trace --stats -d $OUT/proftrain -o run --output-format csv -- python tools/bench_train.py --steps 5 --warmup 2 ;;
     gexp) step g1 200 python tools/tune.py --variants u4nt --nsplit 2,4 --ksplit 8 --rounds 3 \
