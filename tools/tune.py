@@ -62,7 +62,7 @@ def main():
     tx = torch.rand(B, 3, device=dev, generator=g) * 4 - 2
     dtx = torch.nn.functional.normalize(torch.randn(B, 3, device=dev, generator=g), dim=-1) if w.with_dir_tx else None
     r = AVRRender(StubNet(attn, sig), **w.render)
-    timer = KernelTimer()
+    timer = KernelTimer(args.steps)
     rmod.KERNEL_TIMER = timer
     combos = list(itertools.product(args.variants.split(","), [int(x) for x in args.nsplit.split(",")],
                                     [int(x) for x in args.ksplit.split(",")]))
@@ -81,7 +81,8 @@ def main():
                 for _ in range(3):
                     spectrum_to_ir(r(ro, tx, dtx))
                 torch.cuda.synchronize()
-                timer.pairs.clear()
+                timer.used = 0
+                timer.rows.clear()
                 timer.enabled = True
                 t0 = time.perf_counter()
                 for _ in range(args.steps):
