@@ -26,6 +26,11 @@ int check_launch(const char* what);
         if (!(cond)) return ::avr::fail(AVR_E_ARG, msg); \
     } while (0)
 
+// irfft of B spectra [B][F][2] -> [B][2(F-1)], and of a second batch
+// (spec2 -> ir2, may be null) in the same launch (render_fwd.hip).
+int launch_irfft(int B, int F, const float* spec, const float* spec2, const float* tw, float* ir,
+                 float* ir2, void* stream);
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ---------------------------------------------------------------- dtypes

@@ -622,15 +622,23 @@ __global__ __launch_bounds__(256) void spectrum_finalize_kernel(int B, int P, in
 // Block = 32 output samples x 8 bin-slices; each thread walks bins
 // k = 1 + slice + 8j with four independent index chains (ILP over the LDS
 // latency), then the 8 slices are combined in LDS in a fixed order.
-__global__ __launch_bounds__(256) void irfft_kernel(int F, const float2* __restrict__ spec,
+// Rows b >= B1 come from (spec2, ir2): the criterion transforms the
+// predicted and measured spectra in one launch.
+__global__ __launch_bounds__(256) void irfft_kernel(int F, int B1, const float2* __restrict__ spec,
+                                                    const float2* __restrict__ spec2,
                                                     const float2* __restrict__ twg,
-                                                    float* __restrict__ ir) {
+                                                    float* __restrict__ ir, float* __restrict__ ir2) {
     extern __shared__ float2 lds[];
     __shared__ float red[8][33];
     const int n = 2 * (F - 1);
     float2* X = lds;       // [F]
     float2* tw = lds + F;  // [n]
-    const int b = blockIdx.y;
+    int b = blockIdx.y;
+    if (b >= B1) {
+        b -= B1;
+        spec = spec2;
+        ir = ir2;
+    }
     stage_table<256>(X, spec + (int64_t)b * F, F);
     stage_table<256>(tw, twg, n);
     __syncthreads();
@@ -987,14 +995,23 @@ extern "C" int avr_spectrum_finalize(int32_t B, int32_t P, int32_t F, const floa
     return check_launch("avr_spectrum_finalize");
 }
 
-extern "C" int avr_irfft(int32_t B, int32_t F, const float* spec, const float* tw, float* ir,
-                         void* stream) {
+namespace avr {
+int launch_irfft(int B, int F, const float* spec, const float* spec2, const float* tw, float* ir,
+                 float* ir2, void* stream) {
     AVR_REQUIRE(B >= 1 && F >= 2 && spec && tw && ir, "avr_irfft: bad args");
     const int n = 2 * (F - 1);
     AVR_REQUIRE(n <= 16384, "avr_irfft: n too large");
     const size_t lds = (size_t)(F + n) * sizeof(float2);
-    hipLaunchKernelGGL(irfft_kernel, dim3((n + 31) / 32, B), dim3(256), lds, as_stream(stream),
-                       (int)F, reinterpret_cast<const float2*>(spec),
-                       reinterpret_cast<const float2*>(tw), ir);
+    const int rows = spec2 ? 2 * B : B;
+    hipLaunchKernelGGL(irfft_kernel, dim3((n + 31) / 32, rows), dim3(256), lds, as_stream(stream),
+                       (int)F, (int)B, reinterpret_cast<const float2*>(spec),
+                       reinterpret_cast<const float2*>(spec2 ? spec2 : spec),
+                       reinterpret_cast<const float2*>(tw), ir, ir2 ? ir2 : ir);
     return check_launch("avr_irfft");
+}
+}  // namespace avr
+
+extern "C" int avr_irfft(int32_t B, int32_t F, const float* spec, const float* tw, float* ir,
+                         void* stream) {
+    return avr::launch_irfft(B, F, spec, nullptr, tw, ir, nullptr, stream);
 }

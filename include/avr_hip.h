@@ -229,6 +229,35 @@ int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, const void* h
                  float* grad_w, float* grad_W, float* workspace, int64_t workspace_bytes,
                  void* stream);
 
+/* ---- §8f rank 2: training criterion (utils/criterion.py:69-98) ---------
+ * pred, ori: spectra [B][F][2] fp32 (the renderer's output and the measured
+ * spectrum); IR length n = 2(F-1) must exceed 256 (torch.stft reflect pad of
+ * the 512-point resolution) and be <= 12288; B <= 256.
+ * weights[6] (HOST) = spec, amplitude, angle, time, energy, multistft loss
+ * weights (criterion.py:11-16).  wtab[avr_criterion_window_len()] = the
+ * hann windows torch.hann_window(300), (150), (75), (30) then 256 ones,
+ * concatenated; tw512 = avr_ir_twiddle(512); irtw = avr_ir_twiddle(n).
+ * Forward writes pred_time, ori_time [B][n] (irfft of each,
+ * criterion.py:71-72) and losses[8] = spec, amplitude, angle, time, energy
+ * and multi-STFT losses, weighted as the reference returns them
+ * (criterion.py:85-98), then two zeros (the DAS terms, criterion.py:101-102).  The workspace (avr_criterion_workspace bytes) holds
+ * the STFT bins and statistics the backward reuses: pass the same one.
+ * Backward: grad_losses[6] (DEVICE) = upstream grads of the six losses,
+ * grad_pred_time [B][n] (DEVICE, may be NULL) = upstream grad of pred_time;
+ * writes grad_pred [B][F][2] = dL/dRe, dL/dIm of pred. */
+int avr_criterion_window_len(void);
+int avr_criterion_workspace(int32_t B, int32_t F, int64_t* bytes);
+int avr_criterion_fwd(int32_t B, int32_t F, const float* weights, const float* pred,
+                      const float* ori, const float* wtab, const float* tw512, const float* irtw,
+                      float* pred_time, float* ori_time, float* losses, void* workspace,
+                      int64_t workspace_bytes, void* stream);
+int avr_criterion_bwd(int32_t B, int32_t F, const float* weights, const float* pred,
+                      const float* ori, const float* pred_time, const float* ori_time,
+                      const float* grad_losses,
+                      const float* grad_pred_time, const float* wtab, const float* tw512,
+                      const float* irtw, void* workspace, int64_t workspace_bytes,
+                      float* grad_pred, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

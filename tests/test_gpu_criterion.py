@@ -1,0 +1,148 @@
+"""GPU: the training criterion (csrc/criterion.hip)
+against the CPU restatement of utils/criterion.py:69-98 in
+oracle/criterion_oracle.py (auraloss MR-STFT restated; "parity unpinned"
+against the running reference, whose auraloss import is absent here).
+
+Tolerances: each loss within 1e-4 relative of the fp32 oracle (the DFT is a
+direct sum, torch's is an FFT); gradients w.r.t. the predicted spectrum
+within 1e-3 relative (L2) of the fp32 oracle's autograd."""
+import numpy as np
+import pytest
+import torch
+
+from avr_amd.criterion import Criterion
+from oracle import criterion_oracle as co
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+MESHRIR_W = dict(spec_loss_weight=1, amplitude_loss_weight=0.5, angle_loss_weight=0.5,
+                 time_loss_weight=100, energy_loss_weight=5, multistft_loss_weight=1)
+RAF_W = dict(spec_loss_weight=1, amplitude_loss_weight=1, angle_loss_weight=1,
+             time_loss_weight=20, energy_loss_weight=3, multistft_loss_weight=2)
+RENDER = dict(fs=16000, speed=346.8)
+
+
+def _spectra(B, F, seed, noise=0.3):
+    """A decaying-noise IR's spectrum (ori) and a perturbed copy (pred)."""
+    rng = np.random.default_rng(seed)
+    n = 2 * (F - 1)
+    t = np.arange(n)
+    ir = rng.standard_normal((B, n)) * np.exp(-t / (0.15 * n)) * 0.05
+    ori = torch.fft.rfft(torch.from_numpy(ir).float())
+    pert = torch.from_numpy(rng.standard_normal((B, F)) + 1j * rng.standard_normal((B, F)))
+    pred = ori + noise * ori.abs().mean() * pert.to(torch.complex64)
+    return pred.to(torch.complex64), ori.to(torch.complex64)
+
+
+def _rel(a, b):
+    a, b = a.detach().double(), b.detach().double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _oracle(pred, ori, weights, upstream):
+    p = pred.clone().requires_grad_(True)
+    out = co.criterion(p, ori, weights)
+    total = sum(u * x for u, x in zip(upstream, out[:6]))
+    total.backward()
+    return [x.detach() for x in out], p.grad
+
+
+CASES = [
+    # name, B, F, weights, seed
+    ("meshrir_c2", 2, 512, MESHRIR_W, 0),
+    ("raf_c3", 4, 801, RAF_W, 1),
+    ("raf_c4", 4, 801, MESHRIR_W, 2),
+    ("simu_long", 1, 2048, RAF_W, 3),
+    ("min_len", 3, 130, RAF_W, 4),  # n = 258: smallest IR the 512-point STFT accepts
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_criterion_matches_oracle(case):
+    name, B, F, weights, seed = case
+    pred, ori = _spectra(B, F, seed)
+    upstream = [1.0, 0.7, 1.3, 0.5, 2.0, 1.1]
+    ref, ref_grad = _oracle(pred, ori, weights, upstream)
+
+    crit = Criterion(weights, RENDER)
+    p = pred.to(DEV).requires_grad_(True)
+    out = crit(p, ori.to(DEV))
+    assert len(out) == 10
+    for i in range(6):
+        a, b = float(out[i]), float(ref[i])
+        assert abs(a - b) <= 1e-4 * abs(b) + 1e-7, (name, i, a, b)
+    assert float(out[6]) == 0.0 and float(out[7]) == 0.0
+    assert _rel(out[8].cpu(), ref[6]) < 1e-5  # ori_time
+    assert _rel(out[9].cpu(), ref[7]) < 1e-5  # pred_time
+    total = sum(u * x for u, x in zip(upstream, out[:6]))
+    total.backward()
+    torch.cuda.synchronize()
+    err = _rel(p.grad.cpu(), ref_grad)
+    assert err < 1e-3, (name, err)
+
+
+def test_criterion_term_by_term_gradients():
+    """Each loss term's gradient alone (the others' upstream grads zero)."""
+    B, F = 2, 801
+    pred, ori = _spectra(B, F, 7)
+    crit = Criterion(RAF_W, RENDER)
+    for term in range(6):
+        upstream = [0.0] * 6
+        upstream[term] = 1.0
+        _, ref_grad = _oracle(pred, ori, RAF_W, upstream)
+        p = pred.to(DEV).requires_grad_(True)
+        out = crit(p, ori.to(DEV))
+        out[term].backward()
+        err = _rel(p.grad.cpu(), ref_grad)
+        assert err < 1e-3, (term, err)
+
+
+def test_criterion_pred_time_gradient_and_training_sum():
+    """The training loop sums all eight losses (avr_runner.py:187); a loss on
+    the returned pred_time also backpropagates through the irfft."""
+    B, F = 2, 512
+    pred, ori = _spectra(B, F, 9)
+    p_ref = pred.clone().requires_grad_(True)
+    r = co.criterion(p_ref, ori, MESHRIR_W)
+    (sum(r[:6]) + (r[7] ** 2).sum()).backward()
+    crit = Criterion(MESHRIR_W, RENDER)
+    p = pred.to(DEV).requires_grad_(True)
+    out = crit(p, ori.to(DEV))
+    total = out[0] + out[1] + out[2] + out[3] + out[4] + out[5] + out[6] + out[7]
+    (total + (out[9] ** 2).sum()).backward()
+    assert _rel(p.grad.cpu(), p_ref.grad) < 1e-3
+
+
+def test_criterion_identical_spectra():
+    """pred == ori: every loss is zero and the gradient is finite (zero
+    norms take the reference's zero-gradient convention)."""
+    _, ori = _spectra(2, 512, 11)
+    crit = Criterion(MESHRIR_W, RENDER)
+    p = ori.to(DEV).requires_grad_(True)
+    out = crit(p, ori.to(DEV))
+    for i in range(6):
+        assert abs(float(out[i])) < 1e-6, (i, float(out[i]))
+    sum(out[:6]).backward()
+    assert torch.isfinite(torch.view_as_real(p.grad)).all()
+
+
+def test_criterion_real_view_input_and_render_output_path():
+    """[B, F, 2] real input (the renderer's output layout) gives the same
+    losses as the complex view the training loop builds."""
+    pred, ori = _spectra(2, 801, 12)
+    crit = Criterion(RAF_W, RENDER)
+    a = crit(pred.to(DEV), ori.to(DEV))
+    out = torch.view_as_real(pred).to(DEV).requires_grad_(True)
+    b = crit(out[..., 0] + 1j * out[..., 1], ori.to(DEV))
+    for i in range(6):
+        assert float(a[i]) == float(b[i])
+    sum(b[:6]).backward()
+    assert out.grad is not None and torch.isfinite(out.grad).all()
+
+
+def test_criterion_rejects_short_ir():
+    pred, ori = _spectra(1, 128, 0)  # n = 254 <= 256: torch.stft reflect pad fails
+    crit = Criterion(RAF_W, RENDER)
+    with pytest.raises(RuntimeError, match="Padding size"):
+        crit(pred.to(DEV), ori.to(DEV))
