@@ -179,7 +179,7 @@ class Criterion(nn.Module):
         spec, amp, angle, time, energy, mr, das_reg, das_ce, ori_time, pred_time = out
         if self.das_reg_loss_weight > 0 or self.das_ce_loss_weight > 0:
             from .das import das_losses
-            das_reg, das_ce = das_losses(pred, ori, self.fs, self.sound_speed,
+            das_reg, das_ce = das_losses(pred_time, ori_time, self.fs, self.sound_speed,
                                          self.das_reg_loss_weight, self.das_ce_loss_weight,
                                          self.beta)
         return (spec, amp, angle, time, energy, mr, das_reg, das_ce, ori_time, pred_time)

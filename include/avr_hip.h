@@ -258,6 +258,21 @@ int avr_criterion_bwd(int32_t B, int32_t F, const float* weights, const float* p
                       const float* irtw, void* workspace, int64_t workspace_bytes,
                       float* grad_pred, void* stream);
 
+/* DAS direction terms (criterion.py:35-67, 100-122) for 8 channels:
+ * pred_time, ori_time [8][n]; steer [360][8][257][2] = the reference's
+ * steering vectors exp(-i 2 pi delay freq) and angles [360] (radians), both
+ * built by the host with the reference's torch ops; tw512 = avr_ir_twiddle(512).
+ * Forward writes losses[2] = das_reg * w_reg, das_ce * w_ce (0 for a zero
+ * weight).  Backward: grad_losses[2] (DEVICE) -> grad_pred_time [8][n]
+ * (overwritten).  Same workspace for both. */
+int avr_das_workspace(int64_t* bytes);
+int avr_das_fwd(int32_t n, const float* pred_time, const float* ori_time, const float* steer,
+                const float* angles, const float* tw512, float beta, float w_reg, float w_ce,
+                float* losses, void* workspace, int64_t workspace_bytes, void* stream);
+int avr_das_bwd(int32_t n, const float* steer, const float* angles, const float* tw512, float beta,
+                float w_reg, float w_ce, const float* grad_losses, void* workspace,
+                int64_t workspace_bytes, float* grad_pred_time, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -146,3 +146,34 @@ def test_criterion_rejects_short_ir():
     crit = Criterion(RAF_W, RENDER)
     with pytest.raises(RuntimeError, match="Padding size"):
         crit(pred.to(DEV), ori.to(DEV))
+
+
+DAS_W = dict(RAF_W, das_reg_loss_weight=1.0, das_ce_loss_weight=1.0, beta=100.0)
+DAS_RENDER = dict(fs=16000, speed=343.0)
+
+
+@pytest.mark.parametrize("F,seed", [(801, 20), (257, 21)])
+def test_das_terms_match_oracle(F, seed):
+    """8-channel DAS regression / cross-entropy terms (criterion.py:100-122),
+    forward and the gradient of the whole loss including them."""
+    pred, ori = _spectra(8, F, seed, noise=0.5)
+    p_ref = pred.clone().requires_grad_(True)
+    r = co.criterion(p_ref, ori, DAS_W)
+    reg, ce = co.das_losses(p_ref, ori, DAS_RENDER["fs"], DAS_RENDER["speed"], 1.0, 1.0, 100.0)
+    (sum(r[:6]) + reg + ce).backward()
+
+    crit = Criterion(DAS_W, DAS_RENDER)
+    p = pred.to(DEV).requires_grad_(True)
+    out = crit(p, ori.to(DEV))
+    assert abs(float(out[6]) - float(reg)) <= 1e-3 * abs(float(reg)) + 1e-5, (float(out[6]), float(reg))
+    assert abs(float(out[7]) - float(ce)) <= 1e-4 * abs(float(ce)) + 1e-6, (float(out[7]), float(ce))
+    sum(out[:8]).backward()
+    err = _rel(p.grad.cpu(), p_ref.grad)
+    assert err < 2e-3, err
+
+
+def test_das_needs_eight_channels():
+    pred, ori = _spectra(4, 801, 0)
+    crit = Criterion(DAS_W, DAS_RENDER)
+    with pytest.raises(AssertionError, match="Expected 8 microphones"):
+        crit(pred.to(DEV), ori.to(DEV))
