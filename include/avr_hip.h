@@ -273,6 +273,14 @@ int avr_das_bwd(int32_t n, const float* steer, const float* angles, const float*
                 float w_reg, float w_ce, const float* grad_losses, void* workspace,
                 int64_t workspace_bytes, float* grad_pred_time, void* stream);
 
+/* ---- training-loop gradient post-processing (avr_runner.py:190-196) -----
+ * For each of n_tensors fp32 gradients (HOST arrays of device pointers and
+ * element counts): g = isfinite(g * coef) ? g * coef : 0, where coef is a
+ * DEVICE scalar (clip_grad_norm_'s clamped coefficient; NULL = 1).  One
+ * launch per 32 tensors. */
+int avr_scale_sanitize(int32_t n_tensors, float* const* ptrs, const int64_t* sizes,
+                       const float* coef, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -3,9 +3,13 @@
 Two numbers, both fwd+bwd:
   * render core only: stub network outputs resident in HBM, grads to attn and
     signal (the hot path's backward, SURVEY.md §8 a14);
-  * full step: AVRModel_complex (6 HIP hash grids + PyTorch MLPs) ->
-    renderer -> L1 spectrum loss -> backward -> grad clip -> Adam
-    (avr_runner.py:181-200 without the auraloss criterion).
+  * full step (avr_amd.training.TrainStep, avr_runner.py:160-200):
+    AVRModel_complex (6 HIP hash grids + MLPs) -> renderer -> the reference
+    criterion on the GPU (HIP: spectral, time, energy-decay, multi-resolution
+    STFT) -> backward -> clip_grad_norm_ + NaN/Inf zeroing (one HIP launch)
+    -> Adam -> CosineAnnealingLR.  `--loss l1` swaps the criterion for a
+    plain L1 on the spectrum (the round-1 stand-in, for comparison);
+    `--nan-check` adds the reference's per-step host sync on the energy loss.
 
     python tools/bench_train.py [--workload c3_raf_furnished_b4] [--steps 20] [--mlp-dtype bf16]
 """
@@ -24,6 +28,7 @@ sys.path.insert(0, ROOT)
 
 from avr_amd import AVRRender  # noqa: E402
 from avr_amd.model import AVRModel_complex  # noqa: E402
+from avr_amd.training import TrainStep  # noqa: E402
 from avr_amd.workloads import RAF_MODEL, WORKLOADS  # noqa: E402
 
 
@@ -57,6 +62,8 @@ def main():
     ap.add_argument("--no-fused", action="store_true", help="materialise the signal (no fused head)")
     ap.add_argument("--foreach-adam", action="store_true", help="torch's default (foreach) Adam")
     ap.add_argument("--profile", action="store_true", help="torch.profiler table of a few steps")
+    ap.add_argument("--loss", default="criterion", choices=["criterion", "l1"])
+    ap.add_argument("--nan-check", action="store_true", help="reference's per-step isnan().item()")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     w = WORKLOADS[args.workload]
@@ -95,12 +102,24 @@ def main():
     cfg = dict(RAF_MODEL, signal_output_dim=T)
     model = AVRModel_complex(cfg, mlp_dtype=mlp_dtype).to(dev)
     r = AVRRender(model, fused_head=not args.no_fused, **w.render).to(dev)
-    # same update as the reference's torch.optim.Adam (avr_runner.py), as one
-    # fused multi-tensor kernel instead of foreach chains
-    opt = torch.optim.Adam(r.parameters(), lr=2e-4, fused=not args.foreach_adam)
-    target = torch.randn(B, T // 2 + 1, 2, device=dev, generator=g)
+    # RAF training config (config_files/avr_raf_*.yml:24-40); the same Adam as
+    # the reference's torch.optim.Adam, as one fused multi-tensor kernel
+    train_cfg = dict(lr=2e-4, weight_decay=0, T_max=300000, eta_min=8e-5,
+                     spec_loss_weight=1, amplitude_loss_weight=1, angle_loss_weight=1,
+                     time_loss_weight=20, energy_loss_weight=3, multistft_loss_weight=2)
+    ts = TrainStep(r, train_cfg, w.render, fused_adam=not args.foreach_adam,
+                   nan_check=args.nan_check)
+    # measured-IR-like target spectrum: decaying noise
+    tt = torch.arange(T, device=dev)
+    ir = torch.randn(B, T, device=dev, generator=g) * torch.exp(-tt / (0.15 * T)) * 0.05
+    target_c = torch.fft.rfft(ir)
+    target = torch.view_as_real(target_c).contiguous()
+    opt = ts.optimizer
 
     def train_step():
+        if args.loss == "criterion":
+            ts(target_c, ro, tx, dtx)
+            return
         out = r(ro, tx, dtx)
         loss = (out - target).abs().mean()
         opt.zero_grad(set_to_none=True)
@@ -122,6 +141,8 @@ def main():
     res["mlp_dtype"] = args.mlp_dtype
     res["fused_head"] = not args.no_fused
     res["adam"] = "foreach" if args.foreach_adam else "fused"
+    res["loss"] = args.loss
+    res["nan_check"] = args.nan_check
     print(json.dumps(res))
 
 
