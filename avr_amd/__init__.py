@@ -12,6 +12,7 @@ from .renderer import (  # noqa: F401
     ray_directions,
     spectrum_to_ir,
 )
+from .criterion import Criterion  # noqa: F401
 from . import workloads  # noqa: F401
 
 __version__ = "0.1.0"
