@@ -94,6 +94,45 @@ class _Linear(torch.autograd.Function):
         return gx, gw, None
 
 
+_ZERO_BIAS: dict = {}
+
+
+def _zero_bias(n, dtype, device):
+    key = (n, dtype, device)
+    z = _ZERO_BIAS.get(key)
+    if z is None:
+        z = torch.zeros(n, dtype=dtype, device=device)
+        _ZERO_BIAS[key] = z
+    return z
+
+
+class _LinearReLU(torch.autograd.Function):
+    """y = relu(x W^T) with the ReLU in the GEMM epilogue (hipBLASLt
+    `_addmm_activation` with a zero bias: one kernel instead of GEMM + an
+    elementwise pass over the [N, width] activation, bit-identical output).
+    The backward is ReLU's own (threshold on the saved output), then the
+    same data / weight gradients as `_Linear`."""
+
+    @staticmethod
+    def forward(ctx, x, w_master, dtype):
+        w = w_master.to(dtype)
+        if x.is_cuda:
+            y = torch._addmm_activation(_zero_bias(w.size(0), dtype, x.device), x, w.t(),
+                                        use_gelu=False)
+        else:
+            y = torch.relu(x @ w.t())
+        ctx.save_for_backward(x, w, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, y = ctx.saved_tensors
+        g = torch.ops.aten.threshold_backward(gy, y, 0).contiguous()
+        gx = g @ w if ctx.needs_input_grad[0] else None
+        gw = _wgrad(g, x) if ctx.needs_input_grad[1] else None
+        return gx, gw, None
+
+
 class MLP(nn.Module):
     """tcnn.Network(n_in, n_out, {n_neurons, n_hidden_layers, activation ReLU,
     output_activation None}) without biases."""
@@ -114,15 +153,21 @@ class MLP(nn.Module):
         output layer is applied to."""
         x = x.to(self.dtype).contiguous()
         for lin in self.layers[:-1]:
-            x = F.relu(_Linear.apply(x, lin.weight, self.dtype))
+            x = _LinearReLU.apply(x, lin.weight, self.dtype)
         return x
 
     def last(self, h):
         """The bias-free output layer (output_activation None)."""
         return _Linear.apply(h.contiguous(), self.layers[-1].weight, self.dtype)
 
-    def forward(self, x):
-        return self.last(self.hidden(x))
+    def forward(self, x, out_relu=False):
+        """The network; `out_relu=True` returns relu(output) with the ReLU in
+        the last GEMM's epilogue (for callers that only use the rectified
+        output, model.py:316, 323)."""
+        h = self.hidden(x)
+        if out_relu:
+            return _LinearReLU.apply(h.contiguous(), self.layers[-1].weight, self.dtype)
+        return self.last(h)
 
 
 class _Broadcast(torch.autograd.Function):
@@ -275,10 +320,10 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
         tx_view = (tx_view.reshape(-1, 3) + 1) / 2
         pos_e = _grouped(self._pos_encoding, pts, L, "sample")
         txp_e = _grouped(self._tx_pos_encoding, tx, L, "pose")
-        feat = self._model_encoder_sigma(_cat_features([pos_e, txp_e], L))
-        attn = self._model_decoder_sigma(F.relu(feat))
-        dt = feat.dtype
-        rf = F.relu(feat)
+        # the sigma feature is only used rectified (model.py:316, 323)
+        rf = self._model_encoder_sigma(_cat_features([pos_e, txp_e], L), out_relu=True)
+        attn = self._model_decoder_sigma(rf)
+        dt = rf.dtype
         parts = [rf if L is None else rf.view(*L, -1),
                  _grouped(self._dir_encoding, view, L, "ray").to(dt),
                  _grouped(self._tx_dir_encoding, tx_view, L, "pose").to(dt),
