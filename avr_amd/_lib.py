@@ -85,6 +85,14 @@ def render_params(cfg: dict, T: int, n_rays: int | None = None) -> RenderParams:
     return p
 
 
+class TablePtrs(ctypes.Structure):
+    """Mirror of `avr_table_ptrs` (include/avr_hip.h)."""
+
+    _fields_ = [("d_vals", ctypes.c_void_p), ("shift", ctypes.c_void_p),
+                ("pl_table", ctypes.c_void_p), ("phase", ctypes.c_void_p),
+                ("twiddle", ctypes.c_void_p), ("ir_twiddle", ctypes.c_void_p)]
+
+
 _SIGS = {
     "avr_last_error": (ctypes.c_char_p, []),
     "avr_abi_version": (ctypes.c_int, []),
@@ -122,6 +130,9 @@ _SIGS = {
     "avr_das_fwd": (ctypes.c_int, [_c_i32] + [_vp] * 5 + [_c_f32] * 3 + [_vp, _vp, _c_i64, _vp]),
     "avr_das_bwd": (ctypes.c_int, [_c_i32] + [_vp] * 3 + [_c_f32] * 3 + [_vp, _vp, _c_i64, _vp, _vp]),
     "avr_scale_sanitize": (ctypes.c_int, [_c_i32, _vp, _vp, _vp, _vp]),
+    "avr_render_core_layout": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp, _vp]),
+    "avr_render_core_fwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32, _vp, _c_i32] + [_vp] * 5
+                            + [_c_i64] + [_vp] * 5),
 }
 
 EXPORTS = tuple(_SIGS)

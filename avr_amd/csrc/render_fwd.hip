@@ -1015,3 +1015,98 @@ extern "C" int avr_irfft(int32_t B, int32_t F, const float* spec, const float* t
                          void* stream) {
     return avr::launch_irfft(B, F, spec, nullptr, tw, ir, nullptr, stream);
 }
+
+// ---------------------------------------------------- one-call render core
+// weights -> ray reduction -> DFT + phase -> finalize [-> irfft] with one
+// host call: the stages above in order on one stream, sized by
+// avr_render_core_layout.  Cuts the host issue cost of a pose to one
+// ctypes call (the Python path otherwise issues four, each with its own
+// allocation and argument marshalling).
+namespace {
+struct CoreLayout {
+    int64_t w, delay, part, spart, bytes;
+    int32_t n_split, k_split, P;
+};
+
+CoreLayout core_layout(const avr_render_params* p, int B, int sig_dtype) {
+    CoreLayout L{};
+    const int64_t R = n_rays(*p), S = p->n_samples, T = p->T, F = T / 2 + 1;
+    int32_t ns = 1;
+    avr_reduce_splits(p, B, sig_dtype, &ns);
+    L.n_split = ns;
+    const int nkc = (int)((T + kKc - 1) / kKc);
+    int ks = 1;
+    if (const char* f = getenv("AVR_KSPLIT")) {
+        ks = atoi(f);
+    } else {
+        const int64_t base = ((F + 127) / 128) * ((S + 31) / 32) * B;
+        ks = (int)((256 + (base > 0 ? base : 1) - 1) / (base > 0 ? base : 1));
+    }
+    if (ks < 1) ks = 1;
+    if (ks > nkc) ks = nkc;
+    L.k_split = ks;
+    L.P = (int32_t)(((S + 31) / 32) * ks);
+    auto al = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
+    int64_t o = 0;
+    L.w = o;
+    o += al((int64_t)B * R * S * 4);
+    L.delay = o;
+    o += al((int64_t)B * R * S * 4);
+    L.part = o;
+    o += al((int64_t)ns * B * S * T * 4);
+    L.spart = o;
+    o += al((int64_t)B * L.P * F * 8);
+    L.bytes = o;
+    return L;
+}
+}  // namespace
+
+extern "C" int avr_render_core_layout(const avr_render_params* p, int32_t B, int32_t sig_dtype,
+                                      int64_t* offsets /*[5]: w, delay, part, spart, bytes*/,
+                                      int32_t* splits /*[2]: n_split, k_split*/) {
+    if (int e = validate(p)) return e;
+    AVR_REQUIRE(B >= 1 && offsets && splits, "avr_render_core_layout: bad args");
+    const CoreLayout L = core_layout(p, B, sig_dtype);
+    offsets[0] = L.w;
+    offsets[1] = L.delay;
+    offsets[2] = L.part;
+    offsets[3] = L.spart;
+    offsets[4] = L.bytes;
+    splits[0] = L.n_split;
+    splits[1] = L.k_split;
+    return 0;
+}
+
+extern "C" int avr_render_core_fwd(const avr_render_params* p, int32_t B, const void* attn,
+                                   int32_t attn_dtype, const void* signal, int32_t sig_dtype,
+                                   const float* rays_o, const float* pos_tx, const float* dirs,
+                                   const avr_table_ptrs* tab, void* workspace,
+                                   int64_t workspace_bytes, float* out, float* ir, void* ev_begin,
+                                   void* ev_end, void* stream) {
+    if (int e = validate(p)) return e;
+    AVR_REQUIRE(tab && workspace && out, "avr_render_core_fwd: null pointer");
+    const CoreLayout L = core_layout(p, B, sig_dtype);
+    AVR_REQUIRE(workspace_bytes >= L.bytes, "avr_render_core_fwd: workspace too small");
+    char* ws = reinterpret_cast<char*>(workspace);
+    float* w = reinterpret_cast<float*>(ws + L.w);
+    int32_t* delay = reinterpret_cast<int32_t*>(ws + L.delay);
+    float* part = reinterpret_cast<float*>(ws + L.part);
+    float* spart = reinterpret_cast<float*>(ws + L.spart);
+    if (int e = avr_weights_fwd(p, B, attn, attn_dtype, rays_o, pos_tx, dirs, tab->d_vals, w,
+                                delay, stream))
+        return e;
+    hipStream_t s = as_stream(stream);
+    if (ev_begin) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s);
+    if (int e = avr_ray_reduce_fwd(p, B, signal, sig_dtype, w, delay, L.n_split, part, stream))
+        return e;
+    if (ev_end) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s);
+    if (int e = avr_dft_phase_fwd(p, B, part, L.n_split, tab->pl_table, tab->shift, tab->phase,
+                                  tab->twiddle, L.k_split, spart, stream))
+        return e;
+    if (int e = avr_spectrum_finalize(B, L.P, p->T / 2 + 1, spart, out, stream)) return e;
+    if (ir) {
+        AVR_REQUIRE(tab->ir_twiddle, "avr_render_core_fwd: ir requested without ir_twiddle");
+        if (int e = avr_irfft(B, p->T / 2 + 1, out, tab->ir_twiddle, ir, stream)) return e;
+    }
+    return 0;
+}

@@ -46,6 +46,23 @@ def _stream(device):
     return torch.cuda.current_stream(device).cuda_stream
 
 
+class _NoGuard:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NO_GUARD = _NoGuard()
+
+
+def _on(dev):
+    """torch.cuda.device(dev), skipped when dev is already current (the
+    common case: entering the guard costs more host time than a launch)."""
+    return _NO_GUARD if torch.cuda.current_device() == dev.index else torch.cuda.device(dev)
+
+
 def _dtype_code(t):
     if t.dtype == torch.float32:
         return DTYPE_F32
@@ -84,6 +101,24 @@ class Tables:
         # shift values are needed on the host for the reference's range check
         shifts = self.shift.cpu()
         self.max_shift = int(shifts.max().item()) if S > 0 else 0
+        self.ptrs = _lib.TablePtrs(self.d_vals.data_ptr(), self.shift.data_ptr(),
+                                   self.pl.data_ptr(), self.phase.data_ptr(),
+                                   self.twiddle.data_ptr(),
+                                   self.ir_twiddle.data_ptr() if n >= 2 else None)
+        self._layouts = {}
+
+    def core_layout(self, p, B, sig_code):
+        """(offsets[5], n_split, k_split) of avr_render_core_fwd's workspace."""
+        # tuning overrides read by the library (tools/tune.py) are part of the key
+        key = (p.n_rays, B, sig_code, os.environ.get("AVR_NSPLIT"), os.environ.get("AVR_KSPLIT"))
+        v = self._layouts.get(key)
+        if v is None:
+            off = (ctypes.c_int64 * 5)()
+            sp = (ctypes.c_int32 * 2)()
+            _lib.call("avr_render_core_layout", ctypes_ref(p), B, sig_code, off, sp)
+            v = (tuple(off), int(sp[0]), int(sp[1]))
+            self._layouts[key] = v
+        return v
 
 
 def ctypes_ref(p):
@@ -194,6 +229,28 @@ def _grad_attn(p, tables, attn, grad_w, st):
     return grad_attn
 
 
+def _render_core_fwd(attn, signal, p, tables, rays_o, position_tx, dirs, ir_out):
+    """avr_render_core_fwd -> (out [B, F, 2], workspace, layout offsets)."""
+    dev = signal.device
+    B = signal.size(0)
+    F = p.T // 2 + 1
+    sig_code = _dtype_code(signal)
+    off, n_split, _ = tables.core_layout(p, B, sig_code)
+    ws = torch.empty(off[4], dtype=torch.uint8, device=dev)
+    out = torch.empty(B, F, 2, dtype=torch.float32, device=dev)
+    ev0 = ev1 = None
+    timer = KERNEL_TIMER
+    if timer is not None:
+        R, S = p.n_rays, p.n_samples
+        delay = ws[off[1]:off[1] + B * R * S * 4].view(torch.int32).view(B, R, S)
+        ev0, ev1 = timer.events(n_split=n_split, delay=delay, shift=tables.shift)
+    _lib.call("avr_render_core_fwd", ctypes_ref(p), B, _ptr(attn), _dtype_code(attn),
+              _ptr(signal), sig_code, _ptr(rays_o), _ptr(position_tx), _ptr(dirs),
+              ctypes.byref(tables.ptrs), _ptr(ws), off[4], _ptr(out), _ptr(ir_out), ev0, ev1,
+              _stream(dev))
+    return out, ws, off
+
+
 class RenderCore(torch.autograd.Function):
     """Everything after the network call (renderer.py:75-121) as HIP kernels.
 
@@ -203,23 +260,14 @@ class RenderCore(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, attn, signal, p, tables, rays_o, position_tx, dirs):
-        dev = signal.device
-        B = signal.size(0)
-        S, T = p.n_samples, p.T
-        st = _stream(dev)
-        pref = ctypes_ref(p)
-        w, delay = _weights(p, attn, rays_o, position_tx, dirs, tables, st)
-        n_split = reduce_splits(p, B, _dtype_code(signal))
-        part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
-        timer = KERNEL_TIMER
-        if timer is not None:
-            timer.begin(dev, n_split=n_split, delay=delay, shift=tables.shift)
-        _lib.call("avr_ray_reduce_fwd", pref, B, _ptr(signal), _dtype_code(signal), _ptr(w),
-                  _ptr(delay), n_split, _ptr(part), st)
-        if timer is not None:
-            timer.end(dev)
-        out = _spectrum(p, tables, part, n_split, B, dev, st)
+    def forward(ctx, attn, signal, p, tables, rays_o, position_tx, dirs, ir_out=None):
+        """One native call (avr_render_core_fwd): weights, ray reduction, DFT
+        + phase, finalize, and the irfft into `ir_out` [B, 2(F-1)] when given
+        (forward only, as spectrum_to_ir)."""
+        out, ws, off = _render_core_fwd(attn, signal, p, tables, rays_o, position_tx, dirs, ir_out)
+        B, R, S = signal.size(0), p.n_rays, p.n_samples
+        w = ws[off[0]:off[0] + B * R * S * 4].view(torch.float32).view(B, R, S)
+        delay = ws[off[1]:off[1] + B * R * S * 4].view(torch.int32).view(B, R, S)
         ctx.p, ctx.tables = p, tables
         ctx.save_for_backward(attn, signal, w, delay)
         return out
@@ -239,7 +287,7 @@ class RenderCore(torch.autograd.Function):
                   _ptr(gz), _ptr(w), _ptr(delay), _ptr(grad_signal), _ptr(grad_w), st)
         grad_attn = _grad_attn(p, tables, attn, grad_w, st) if ctx.needs_input_grad[0] else None
         return (grad_attn, grad_signal if ctx.needs_input_grad[1] else None,
-                None, None, None, None, None)
+                None, None, None, None, None, None)
 
 
 class FusedHeadCore(torch.autograd.Function):
@@ -360,6 +408,7 @@ class AVRRender(nn.Module):
         # fold the signal network's last layer into the render when the
         # network offers it (avr_amd.model networks; FusedHeadCore)
         self.fused_head = bool(kwargs.get("fused_head", True))
+        self._pcache = {}
 
     # -- stages, exposed for tests and for callers that bring their own network
     def _device(self, rays_o):
@@ -386,7 +435,7 @@ class AVRRender(nn.Module):
         r0, r1 = self.ray_range if self.ray_range is not None else (0, R_all)
         if not (0 <= r0 < r1 <= R_all):
             raise ValueError(f"ray_range {self.ray_range} outside [0, {R_all})")
-        p0 = render_params(self._cfg, 2, n_rays=r1 - r0)
+        p0 = self._params(2, r1 - r0)
         R, S = r1 - r0, p0.n_samples
         f32 = dict(dtype=torch.float32, device=dev)
         rays_o = rays_o.to(dev, torch.float32).contiguous()
@@ -399,7 +448,7 @@ class AVRRender(nn.Module):
         view = torch.empty(B, R * S, 3, **f32)
         tx = torch.empty(B, R * S, 3, **f32)
         dtx = torch.empty(B, R * S, 3, **f32) if direction_tx is not None else None
-        with torch.cuda.device(dev):
+        with _on(dev):
             if p0.n_azi <= _lib.MAX_AZI:
                 # one fused launch; the jitter travels in the kernel arguments
                 u_host = np.ascontiguousarray(u_azi.detach().cpu().numpy(), dtype=np.float32)
@@ -421,8 +470,18 @@ class AVRRender(nn.Module):
                     n_rays=R)
         return pts, view, tx, dtx, geom
 
-    def render_from_network_output(self, attn, signal, geom):
-        """Render core (renderer.py:74-124) on given network outputs."""
+    def _params(self, T, R):
+        """render_params for (T, rays), cached: the scalars never change."""
+        key = (T, R)
+        p = self._pcache.get(key)
+        if p is None:
+            p = render_params(self._cfg, T, n_rays=R)
+            self._pcache[key] = p
+        return p
+
+    def render_from_network_output(self, attn, signal, geom, ir_out=None):
+        """Render core (renderer.py:74-124) on given network outputs; the IR
+        (utils/criterion.py:71) is also written into `ir_out` when given."""
         dev, B = geom["device"], geom["B"]
         S = int(self.n_samples)
         native = (torch.float32, torch.float16, torch.bfloat16)
@@ -437,12 +496,16 @@ class AVRRender(nn.Module):
         if attn.size(1) != R * S or signal.size(1) != R * S:
             raise ValueError(f"network output has {signal.size(1)} ray-samples, expected "
                              f"{R}x{S}={R * S}")
-        p = render_params(self._cfg, T, n_rays=R)
-        with torch.cuda.device(dev):
+        p = self._params(T, R)
+        with _on(dev):
             tables = get_tables(p, dev)
             check_config(p, tables)
+            if not (torch.is_grad_enabled() and (attn.requires_grad or signal.requires_grad)):
+                # inference: the same native call without the autograd node
+                return _render_core_fwd(attn, signal, p, tables, geom["rays_o"],
+                                        geom["position_tx"], geom["dirs"], ir_out)[0]
             return RenderCore.apply(attn, signal, p, tables, geom["rays_o"], geom["position_tx"],
-                                    geom["dirs"])
+                                    geom["dirs"], ir_out)
 
     def _head_supported(self, geom, h, weight, dtype):
         """Whether the fused-head kernels take this shape (T <= 4096, <= 4096
@@ -480,6 +543,17 @@ class AVRRender(nn.Module):
 
     def forward(self, rays_o, position_tx, direction_tx=None, ch_idx=None):
         """Render [B, F, 2] (real, imag) spectra; see renderer.py:31-124."""
+        return self._render(rays_o, position_tx, direction_tx, ch_idx, None)
+
+    def render_ir(self, rays_o, position_tx, direction_tx=None, ch_idx=None):
+        """(spectrum [B, F, 2], IR [B, 2(F-1)]): forward plus
+        `torch.real(torch.fft.irfft(...))` (utils/criterion.py:71), the IR
+        computed in the same native call (forward only, like spectrum_to_ir)."""
+        ir = []
+        out = self._render(rays_o, position_tx, direction_tx, ch_idx, ir)
+        return out, (ir[0] if ir else spectrum_to_ir(out))
+
+    def _render(self, rays_o, position_tx, direction_tx, ch_idx, ir_slot):
         pts, view, tx, dtx, geom = self.sample(rays_o, position_tx, direction_tx)
         kw = {} if ch_idx is None else {"ch_idx": ch_idx}
         if getattr(self.network_fn, "accepts_ray_layout", False):
@@ -497,7 +571,14 @@ class AVRRender(nn.Module):
             attn, signal = self.network_fn(pts, view, tx, dtx, **kw)
         else:
             attn, signal = self.network_fn(pts, view, tx, **kw)
-        return self.render_from_network_output(attn, signal, geom)
+        ir_out = None
+        if ir_slot is not None:
+            F = signal.size(-1) // 2 + 1
+            if F >= 2:
+                ir_out = torch.empty(geom["B"], 2 * (F - 1), dtype=torch.float32,
+                                     device=geom["device"])
+                ir_slot.append(ir_out)
+        return self.render_from_network_output(attn, signal, geom, ir_out)
 
 
 # --------------------------------------------------------------------------

@@ -25,7 +25,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from avr_amd import AVRRender, spectrum_to_ir  # noqa: E402
+from avr_amd import AVRRender  # noqa: E402
 from avr_amd import renderer as rmod  # noqa: E402
 from avr_amd.workloads import WORKLOADS  # noqa: E402
 
@@ -53,23 +53,25 @@ class KernelTimer:
     def __init__(self, n=0):
         self.pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                      for _ in range(n)]
+        for a, b in self.pool:  # torch creates the HIP event at its first record
+            a.record()
+            b.record()
+        torch.cuda.synchronize()
         self.used = 0
         self.rows = []
         self.n_split = None
         self.enabled = False
 
-    def begin(self, dev, n_split=None, delay=None, shift=None):
+    def events(self, n_split=None, delay=None, shift=None):
+        """(begin, end) raw hipEvent_t handles the library records around the
+        ray-reduction launch on its stream (avr_render_core_fwd), or Nones."""
         if not self.enabled or self.used >= len(self.pool):
-            return
+            return None, None
         self.n_split = n_split
-        self.pool[self.used][0].record(torch.cuda.current_stream(dev))
         self.rows.append((delay, shift))
-
-    def end(self, dev):
-        if not self.enabled or self.used >= len(self.pool):
-            return
-        self.pool[self.used][1].record(torch.cuda.current_stream(dev))
+        a, b = self.pool[self.used]
         self.used += 1
+        return a.cuda_event, b.cuda_event
 
     def mean_ms(self):
         ts = [a.elapsed_time(b) for a, b in self.pool[:self.used]]
@@ -190,8 +192,7 @@ def main():
         i = pose[0] % P
         pose[0] += 1
         with torch.no_grad():
-            out = renderer(rays_o[i], tx[i], dtx[i])
-            return spectrum_to_ir(out)
+            return renderer.render_ir(rays_o[i], tx[i], dtx[i])
 
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
 

@@ -155,6 +155,36 @@ int avr_spectrum_finalize(int32_t B, int32_t P, int32_t F, const float* spart, f
 int avr_irfft(int32_t B, int32_t F, const float* spec, const float* tw, float* ir,
               void* stream);
 
+/* ---- a7-a13 in one host call -------------------------------------------
+ * The pose-independent tables of avr_tables / avr_ir_twiddle. */
+typedef struct avr_table_ptrs {
+    const float* d_vals;      /* [S] */
+    const int32_t* shift;     /* [S] */
+    const float* pl_table;    /* [pl_len] */
+    const float* phase;       /* [S][F][2] */
+    const float* twiddle;     /* [T][2] */
+    const float* ir_twiddle;  /* [2(F-1)][2], only needed when ir is requested */
+} avr_table_ptrs;
+
+/* Workspace layout of avr_render_core_fwd for this shape: byte offsets of
+ * w [B][R][S] fp32, delay [B][R][S] int32, the ray-reduction partials and
+ * the spectrum partials, then the total size (offsets[5]); the ray splits
+ * and DFT k-slices it uses (splits[2]). */
+int avr_render_core_layout(const avr_render_params* p, int32_t B, int32_t sig_dtype,
+                           int64_t* offsets, int32_t* splits);
+
+/* avr_weights_fwd -> avr_ray_reduce_fwd -> avr_dft_phase_fwd ->
+ * avr_spectrum_finalize [-> avr_irfft when ir != NULL] on one stream.
+ * out [B][F][2]; w and delay stay in the workspace for the backward.
+ * ev_begin / ev_end: optional hipEvent_t recorded around the ray-reduction
+ * launch (benchmark instrumentation; NULL otherwise).
+ * Replaces renderer.py:74-124 + utils/criterion.py:71. */
+int avr_render_core_fwd(const avr_render_params* p, int32_t B, const void* attn,
+                        int32_t attn_dtype, const void* signal, int32_t sig_dtype,
+                        const float* rays_o, const float* pos_tx, const float* dirs,
+                        const avr_table_ptrs* tables, void* workspace, int64_t workspace_bytes,
+                        float* out, float* ir, void* ev_begin, void* ev_end, void* stream);
+
 /* ---- a14: backward ------------------------------------------------------
  * grad_out[B][F][2] -> gz[B][S][T] = pl*tail * d out / d z   (adjoint DFT) */
 int avr_dft_phase_bwd(const avr_render_params* p, int32_t B, const float* grad_out,
