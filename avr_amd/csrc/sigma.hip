@@ -1,0 +1,493 @@
+// Fused sigma networks (a5/a6): the width-128 bias-free ReLU MLPs the
+// reference runs as tcnn FullyFusedMLP (sigma encoder + decoder,
+// model.py:117-121, 146-150 / 267-277; configs avr_meshrir.yml:70-84,
+// avr_raf_*.yml:89-101), plus the concatenation of the signal network's input
+// (model.py:221 / 325), in ONE kernel for inference.
+//
+// Per sample n (262144 per config-2 pose):
+//   AVRModel (variant 0):
+//     h = relu(W3 relu(W2 relu(W1 relu(W0 e))))   e = pos_enc[n] (40)
+//     sigma_feat = W3' ...                         (encoder output, 128, linear)
+//     a = W7 relu(W6 relu(W5 relu(W4 relu(sigma_feat))))    (decoder, -> 1)
+//     attn = |leaky_relu(a)|,  base[n] = [sigma_feat | dir_enc[ray] | tx_enc[pose]]
+//   AVRModel_complex (variant 1):
+//     rf = relu(W3 relu(W2 relu(W1 relu(W0 [pos_e[n] | txp_e[pose]]))))   (-> 256)
+//     a = W5 relu(W4 rf),  attn = |leaky_relu(a, slope)|,
+//     base[n] = [rf | dir[ray] | txdir[pose] | pos_sig[n] | txpos_sig[pose]]
+//
+// Unfused, this is 8 GEMMs whose [N,128] bf16 activations each make an HBM
+// round trip, plus the concatenation copies (~0.35 ms per config-2 pose).
+// Here activations never leave registers: every layer is computed TRANSPOSED,
+// Y^T = W X^T, with v_mfma_f32_32x32x16_bf16 (A = weight fragment, B =
+// activation fragment; sample on the lane).  The 32x32 fp32 result has its
+// sample column on the lane and its output rows in the 16 registers, which is
+// exactly the B-operand layout of the next layer's k-steps (registers 8s..8s+7
+// = k-step s, cdna_hip_programming.md §3 "accumulator tile as the next MFMA's
+// operand"); the k permutation that implies is folded into the packed weight
+// fragments on the host (avr_amd/sigma.py), so the chain needs no LDS and no
+// lane movement.  Weights (216-256 KB per net, bf16) stream through two 32 KB
+// LDS buffers, one chunk (a layer or half a layer) each, one barrier per
+// chunk, the next chunk's global loads in flight under the current chunk's
+// MFMAs; every wave reads one 16-byte fragment per NT MFMAs with
+// conflict-free ds_read_b128.
+//
+// Rounding is the unfused bf16 path's: fp32 accumulation, bf16 activations
+// (ReLU before or after the rounding is the same), the decoder output rounded
+// to bf16 before leaky_relu (computed in fp32, rounded to bf16) and abs.
+#include "common.h"
+
+using namespace avr;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kChunk = 32768;  // bytes of packed fragments per LDS stage
+constexpr int kFrag = 1024;    // one fragment: 64 lanes x 8 bf16
+
+struct Src {
+    const void* p;
+    int dtype;
+    int rows_div;
+};
+
+struct Args {
+    int64_t N;
+    Src in0, in1;
+    int n_extra;
+    Src extra[AVR_SIGMA_MAX_EXTRA];
+    int extra_col[AVR_SIGMA_MAX_EXTRA];
+    int extra_width[AVR_SIGMA_MAX_EXTRA];
+    const char* wpack;
+    __hip_bfloat16* base;
+    int ldb;
+    __hip_bfloat16* attn;
+    float slope;
+};
+
+// two fp32 -> a dword of two bf16 (v_cvt_pk_bf16_f32, round to nearest even)
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
+    const bf16x2 p = __builtin_convertvector((f32x2v){a, b}, bf16x2);
+    return __builtin_bit_cast(uint32_t, p);
+}
+
+// ReLU of two packed bf16 (v_pk_max_i16 with 0: a set sign bit is a negative
+// int16).  One VALU op per two values; a NaN with the sign bit set becomes 0.
+__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t u) {
+    const s16x2 r = __builtin_elementwise_max(__builtin_bit_cast(s16x2, u), (s16x2){0, 0});
+    return __builtin_bit_cast(uint32_t, r);
+}
+
+// 8 consecutive features (fp16 or fp32) of row `row` starting at `col` -> bf16
+__device__ __forceinline__ bf16x8 load8(const Src& s, int64_t row, int width, int col) {
+    float f[8];
+    if (s.dtype == AVR_DTYPE_F16) {
+        const u32x4v v = *reinterpret_cast<const u32x4v*>(
+            static_cast<const __half*>(s.p) + row * width + col);
+        Vec16<__half>::cvt(v, f);
+    } else {
+        const float* q = static_cast<const float*>(s.p) + row * width + col;
+        const f32x4 a = *reinterpret_cast<const f32x4*>(q);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(q + 4);
+        f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
+        f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
+    }
+    u32x4v r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = pack_bf16(f[2 * q], f[2 * q + 1]);
+    return __builtin_bit_cast(bf16x8, r);
+}
+
+__device__ __forceinline__ float relu(float v) { return v < 0.0f ? 0.0f : v; }  // NaN passes
+
+// Cooperative global -> LDS staging of 32 KB chunks into two LDS buffers.
+// Chunk c is read from buffer c & 1; while it is computed, chunk c+1 sits in
+// registers (its loads were issued a whole chunk earlier).  After computing
+// chunk c each wave writes its share of chunk c+1 into the other buffer (whose
+// last readers, chunk c-1, all passed the previous barrier), then ONE raw
+// barrier (LDS writes drained, outstanding global stores NOT waited for),
+// then the loads of chunk c+2 are issued.
+// DBG (timing experiments only, tools/probe_sigma.py tile_cfg >= 16): bit 0
+// drops the barrier, bit 1 the staging loads/writes (results are garbage).
+template <int WAVES, int DBG = 0>
+struct Stager {
+    static constexpr int kPer = kChunk / (64 * WAVES * 16);
+    u32x4v r[kPer];
+    const u32x4v* src;
+    char* lds;
+    int cur, n_chunks, tid;
+    __device__ void issue(int c) {
+        const u32x4v* p = src + (int64_t)c * (kChunk / 16);
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) r[i] = p[tid + 64 * WAVES * i];
+    }
+    __device__ void write(int c) {
+        u32x4v* d = reinterpret_cast<u32x4v*>(lds + (c & 1) * kChunk);
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) d[tid + 64 * WAVES * i] = r[i];
+    }
+    __device__ static void barrier() {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    __device__ void start(const char* wpack, char* lds_base, int chunks) {
+        src = reinterpret_cast<const u32x4v*>(wpack);
+        lds = lds_base;
+        tid = threadIdx.x;
+        n_chunks = chunks;
+        cur = 0;
+        issue(0);
+        write(0);
+        if (chunks > 1) issue(1);
+        barrier();
+    }
+    __device__ const char* buffer() const { return lds + (cur & 1) * kChunk; }
+    __device__ void finish_chunk() {
+        if constexpr (!(DBG & 2)) {
+            if (cur + 1 < n_chunks) write(cur + 1);
+        }
+        if constexpr (!(DBG & 1)) barrier();
+        if constexpr (!(DBG & 2)) {
+            if (cur + 2 < n_chunks) issue(cur + 2);
+        }
+        ++cur;
+    }
+};
+
+// acc[nt][ot] = W X^T for one layer: KS k-steps of input fragments, OT output
+// tiles, CO tiles per LDS chunk.
+template <int NT, int KS, int OT, int CO, class ST>
+__device__ __forceinline__ void dense(ST& st, int lane,
+                                      const bf16x8 (&x)[NT][KS], f32x16 (&acc)[NT][OT]) {
+    static_assert(OT % CO == 0 && CO * KS * kFrag <= kChunk, "chunk overflow");
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[nt][ot][i] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < OT / CO; ++c) {
+        const char* lds = st.buffer();
+        // k-step outer: the CO*NT accumulators of a k-step are independent,
+        // so no MFMA waits on the previous one's result
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+            for (int o = 0; o < CO; ++o) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(lds + (o * KS + ks) * kFrag + lane * 16);
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt)
+                    acc[nt][c * CO + o] =
+                        __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, x[nt][ks], acc[nt][c * CO + o], 0, 0, 0);
+            }
+        st.finish_chunk();
+    }
+}
+
+// one accumulator tile -> 8 dwords of bf16: dword q holds registers 2q, 2q+1
+__device__ __forceinline__ void pack_tile(const f32x16& acc, uint32_t (&d)[8]) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) d[q] = pack_bf16(acc[2 * q], acc[2 * q + 1]);
+}
+
+// packed tile -> next layer's B fragments (k-step 2*ot + s = registers 8s..8s+7)
+__device__ __forceinline__ void tile_frags(const uint32_t (&d)[8], bool rectify, bf16x8& x0, bf16x8& x1) {
+    u32x4v a, b;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        a[q] = rectify ? relu_bf16x2(d[q]) : d[q];
+        b[q] = rectify ? relu_bf16x2(d[4 + q]) : d[4 + q];
+    }
+    x0 = __builtin_bit_cast(bf16x8, a);
+    x1 = __builtin_bit_cast(bf16x8, b);
+}
+
+template <int NT, int OT>
+__device__ __forceinline__ void to_frags(const f32x16 (&acc)[NT][OT], bf16x8 (&x)[NT][2 * OT]) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int ot = 0; ot < OT; ++ot) {
+            uint32_t d[8];
+            pack_tile(acc[nt][ot], d);
+            tile_frags(d, true, x[nt][2 * ot], x[nt][2 * ot + 1]);
+        }
+}
+
+// store OT output tiles (bf16, optionally rectified) into base columns
+// [0, 32*OT) and return them as the next layer's (rectified) fragments: lane
+// (column n, half h) holds rows 8g + 4h + 0..3 of each tile in registers
+// 4g..4g+3 -> one 8-byte store per g.
+template <int NT, int OT>
+__device__ __forceinline__ void store_and_frags(const Args& a, const f32x16 (&acc)[NT][OT], int64_t n0,
+                                                int lane, bool rectify, bf16x8 (&x)[NT][2 * OT]) {
+    const int h = lane >> 5;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int64_t n = n0 + 32 * nt + (lane & 31);
+        __hip_bfloat16* row = a.base + n * a.ldb;
+#pragma unroll
+        for (int ot = 0; ot < OT; ++ot) {
+            uint32_t d[8];
+            pack_tile(acc[nt][ot], d);
+            if (rectify) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) d[q] = relu_bf16x2(d[q]);
+            }
+            if (n < a.N) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    *reinterpret_cast<u32x2v*>(row + 32 * ot + 8 * g + 4 * h) = u32x2v{d[2 * g], d[2 * g + 1]};
+            }
+            tile_frags(d, !rectify, x[nt][2 * ot], x[nt][2 * ot + 1]);
+        }
+    }
+}
+
+// decoder output (row 0 of the single output tile: register 0 of lanes 0..31)
+template <int NT>
+__device__ __forceinline__ void store_attn(const Args& a, const f32x16 (&acc)[NT][1], int64_t n0, int lane) {
+    if (lane >= 32) return;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int64_t n = n0 + 32 * nt + lane;
+        if (n >= a.N) continue;
+        const float y = (float)(__bf16)acc[nt][0][0];       // the GEMM's bf16 output
+        const float l = y > 0.0f ? y : y * a.slope;          // leaky_relu in fp32 ...
+        const float r = fabsf((float)(__bf16)l);             // ... rounded to bf16, abs
+        a.attn[n] = __float2bfloat16(r);
+    }
+}
+
+// row of source s that sample n reads (32-bit: N < 2^31 is checked on the host)
+__device__ __forceinline__ int64_t src_row(const Src& s, int64_t n) {
+    return (int64_t)((uint32_t)n / (uint32_t)s.rows_div);
+}
+
+// extra feature segments copied (as bf16) into base columns after the MLP
+// output: lane (sample r, half h) copies 8-feature chunks h, h+2, ... of its
+// sample's row of every segment (one division per segment and lane)
+template <int NT>
+__device__ __forceinline__ void copy_extras(const Args& a, int64_t n0, int lane) {
+    const int h = lane >> 5;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int64_t n = n0 + 32 * nt + (lane & 31);
+        if (n >= a.N) continue;
+        __hip_bfloat16* row = a.base + n * a.ldb;
+        for (int e = 0; e < a.n_extra; ++e) {
+            const Src s = a.extra[e];
+            const int w = a.extra_width[e];
+            const int64_t r = src_row(s, n);
+            for (int c = 8 * h; c < w; c += 16)
+                *reinterpret_cast<bf16x8*>(row + a.extra_col[e] + c) = load8(s, r, w, c);
+        }
+    }
+}
+
+// first-layer input fragments: lane (sample r, half h) k-step ks holds
+// features 8c..8c+7 with c = 2ks + h; chunks [0, 5) come from in0 (40 per
+// sample), [5, 10) from in1 (40 per pose) when the net has two inputs.
+template <int NT, int KS0>
+__device__ __forceinline__ void load_input(const Args& a, int64_t n0, int lane, bf16x8 (&x)[NT][KS0]) {
+    const int h = lane >> 5;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        int64_t n = n0 + 32 * nt + (lane & 31);
+        n = n < a.N ? n : a.N - 1;
+        const int64_t r0 = src_row(a.in0, n);
+        const int64_t r1 = KS0 > 3 ? src_row(a.in1, n) : 0;
+#pragma unroll
+        for (int ks = 0; ks < KS0; ++ks) {
+            const int c = 2 * ks + h;
+            if (c < 5) {
+                x[nt][ks] = load8(a.in0, r0, 40, 8 * c);
+            } else if (KS0 > 3 && c < 10) {
+                x[nt][ks] = load8(a.in1, r1, 40, 8 * (c - 5));
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x[nt][ks][j] = (__bf16)0.0f;
+            }
+        }
+    }
+}
+
+// Variant 0 (AVRModel): 40 -> 128 -> 128 -> 128 -> 128 (linear, = sigma_feat)
+// -> relu -> 128 -> 128 -> 128 -> 1.  8 chunks.
+template <int NT, int WAVES, int OCC, int DBG = 0>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
+void sigma_meshrir_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * kChunk];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t n0 = ((int64_t)blockIdx.x * WAVES + wave) * 32 * NT;
+    Stager<WAVES, DBG> st;
+    st.start(a.wpack, lds, 8);
+
+    bf16x8 x0[NT][3];
+    load_input<NT, 3>(a, n0, lane, x0);
+    bf16x8 x[NT][8];
+    {
+        f32x16 acc[NT][4];
+        dense<NT, 3, 4, 4>(st, lane, x0, acc);
+        to_frags<NT, 4>(acc, x);
+    }
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+        f32x16 acc[NT][4];
+        dense<NT, 8, 4, 4>(st, lane, x, acc);
+        to_frags<NT, 4>(acc, x);
+    }
+    {
+        f32x16 acc[NT][4];
+        dense<NT, 8, 4, 4>(st, lane, x, acc);
+        // sigma_feat (linear) -> base; relu(sigma_feat) -> decoder
+        store_and_frags<NT, 4>(a, acc, n0, lane, false, x);
+    }
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+        f32x16 acc[NT][4];
+        dense<NT, 8, 4, 4>(st, lane, x, acc);
+        to_frags<NT, 4>(acc, x);
+    }
+    {
+        f32x16 acc[NT][1];
+        dense<NT, 8, 1, 1>(st, lane, x, acc);
+        store_attn<NT>(a, acc, n0, lane);
+    }
+    if constexpr (!(DBG & 4)) copy_extras<NT>(a, n0, lane);
+}
+
+// Variant 1 (AVRModel_complex): [40 | 40] -> 128 -> 128 -> 128 -> 256 (relu,
+// = rf) -> 128 -> 1.  8 chunks (the 256-wide layers take two each).
+template <int NT, int WAVES, int OCC>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
+void sigma_raf_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * kChunk];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t n0 = ((int64_t)blockIdx.x * WAVES + wave) * 32 * NT;
+    Stager<WAVES> st;
+    st.start(a.wpack, lds, 8);
+
+    bf16x8 x0[NT][5];
+    load_input<NT, 5>(a, n0, lane, x0);
+    bf16x8 x[NT][8];
+    {
+        f32x16 acc[NT][4];
+        dense<NT, 5, 4, 4>(st, lane, x0, acc);
+        to_frags<NT, 4>(acc, x);
+    }
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+        f32x16 acc[NT][4];
+        dense<NT, 8, 4, 4>(st, lane, x, acc);
+        to_frags<NT, 4>(acc, x);
+    }
+    bf16x8 rf[NT][16];
+    {
+        f32x16 acc[NT][8];
+        dense<NT, 8, 8, 4>(st, lane, x, acc);
+        store_and_frags<NT, 8>(a, acc, n0, lane, true, rf);  // rf = relu(sigma_feature)
+    }
+    {
+        f32x16 acc[NT][4];
+        dense<NT, 16, 4, 2>(st, lane, rf, acc);
+        to_frags<NT, 4>(acc, x);
+    }
+    {
+        f32x16 acc[NT][1];
+        dense<NT, 8, 1, 1>(st, lane, x, acc);
+        store_attn<NT>(a, acc, n0, lane);
+    }
+    copy_extras<NT>(a, n0, lane);
+}
+
+bool src_ok(const avr_feat_src& s) {
+    return s.data && (s.dtype == AVR_DTYPE_F16 || s.dtype == AVR_DTYPE_F32) && s.rows_div >= 1 &&
+           reinterpret_cast<uintptr_t>(s.data) % 16 == 0;
+}
+
+Src to_src(const avr_feat_src& s) { return Src{s.data, (int)s.dtype, (int)s.rows_div}; }
+
+template <int NT, int WAVES, int OCC, int DBG = 0>
+int launch_meshrir(const Args& a, hipStream_t st) {
+    const int64_t per_block = 32 * NT * WAVES;
+    const dim3 grid((unsigned)((a.N + per_block - 1) / per_block));
+    hipLaunchKernelGGL((sigma_meshrir_kernel<NT, WAVES, OCC, DBG>), grid, dim3(64 * WAVES), 0, st, a);
+    return check_launch("avr_sigma_fwd");
+}
+
+template <int WAVES, int OCC>
+int launch_raf(const Args& a, hipStream_t st) {
+    const int64_t per_block = 32 * WAVES;
+    const dim3 grid((unsigned)((a.N + per_block - 1) / per_block));
+    hipLaunchKernelGGL((sigma_raf_kernel<1, WAVES, OCC>), grid, dim3(64 * WAVES), 0, st, a);
+    return check_launch("avr_sigma_fwd");
+}
+
+}  // namespace
+
+extern "C" int avr_sigma_pack_bytes(int32_t variant, int64_t* bytes) {
+    AVR_REQUIRE(bytes && (variant == AVR_SIGMA_MESHRIR || variant == AVR_SIGMA_RAF),
+                "avr_sigma_pack_bytes: bad variant");
+    *bytes = 8 * (int64_t)kChunk;
+    return 0;
+}
+
+extern "C" int avr_sigma_fwd(const avr_sigma_desc* d, const void* wpack, void* base, int32_t ldb,
+                             void* attn, void* stream) {
+    AVR_REQUIRE(d && wpack && base && attn, "avr_sigma_fwd: null argument");
+    AVR_REQUIRE(d->variant == AVR_SIGMA_MESHRIR || d->variant == AVR_SIGMA_RAF, "avr_sigma_fwd: bad variant");
+    AVR_REQUIRE(d->n_samples >= 1 && d->n_samples < (int64_t(1) << 31),
+                "avr_sigma_fwd: n_samples must be in [1, 2^31)");
+    const bool two = d->variant == AVR_SIGMA_RAF;
+    AVR_REQUIRE(src_ok(d->input[0]) && (!two || src_ok(d->input[1])), "avr_sigma_fwd: bad input source");
+    AVR_REQUIRE(d->n_extra >= 0 && d->n_extra <= AVR_SIGMA_MAX_EXTRA, "avr_sigma_fwd: bad n_extra");
+    const int out_w = two ? 256 : 128;
+    AVR_REQUIRE(ldb % 8 == 0 && reinterpret_cast<uintptr_t>(base) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(wpack) % 16 == 0,
+                "avr_sigma_fwd: base/wpack must be 16-byte aligned, ldb a multiple of 8");
+    Args a{};
+    a.N = d->n_samples;
+    a.in0 = to_src(d->input[0]);
+    a.in1 = two ? to_src(d->input[1]) : a.in0;
+    a.n_extra = d->n_extra;
+    int col = out_w;
+    for (int e = 0; e < d->n_extra; ++e) {
+        AVR_REQUIRE(src_ok(d->extra[e]) && d->extra_width[e] >= 8 && d->extra_width[e] % 8 == 0,
+                    "avr_sigma_fwd: bad extra feature source");
+        a.extra[e] = to_src(d->extra[e]);
+        a.extra_width[e] = d->extra_width[e];
+        a.extra_col[e] = col;
+        col += d->extra_width[e];
+    }
+    AVR_REQUIRE(col <= ldb, "avr_sigma_fwd: ldb smaller than the concatenated features");
+    a.wpack = static_cast<const char*>(wpack);
+    a.base = static_cast<__hip_bfloat16*>(base);
+    a.ldb = ldb;
+    a.attn = static_cast<__hip_bfloat16*>(attn);
+    a.slope = d->leaky_slope;
+    hipStream_t st = as_stream(stream);
+    const int cfg = d->tile_cfg;
+    // tile configs (tools/probe_sigma.py, MI355X at config 2): MeshRIR
+    // 0 = 64 samples per wave, 4 waves, 2 waves/SIMD (72 us); 1 = 32 per
+    // wave, 8 waves (80 us); 2 = 32 per wave, 4 waves; 3 = 64 per wave, 4
+    // waves, 1 wave/SIMD.  RAF: 0 = 4 waves (120 us), 1 = 8 waves (137 us).
+    if (two) return cfg == 1 ? launch_raf<8, 1>(a, st) : launch_raf<4, 2>(a, st);
+    if (cfg == 1) return launch_meshrir<1, 8, 1>(a, st);
+    if (cfg == 2) return launch_meshrir<1, 4, 4>(a, st);
+    if (cfg == 3) return launch_meshrir<2, 4, 1>(a, st);
+    if (cfg == 16) return launch_meshrir<1, 8, 1, 1>(a, st);
+    if (cfg == 17) return launch_meshrir<1, 8, 1, 2>(a, st);
+    if (cfg == 18) return launch_meshrir<1, 8, 1, 3>(a, st);
+    if (cfg == 19) return launch_meshrir<1, 8, 1, 4>(a, st);
+    if (cfg == 20) return launch_meshrir<1, 8, 1, 7>(a, st);
+    return launch_meshrir<2, 4, 2>(a, st);
+}
+
+extern "C" int avr_sigma_desc_size(void) { return (int)sizeof(avr_sigma_desc); }

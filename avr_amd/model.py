@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import sigma as _sigma
 from .encoding import HashGridEncoding
 
 
@@ -209,6 +210,30 @@ def _grouped(enc, x, layout, per):
     return _Broadcast.apply(e, (B, 1, 1, e.size(-1)), (B, R, S, e.size(-1)))
 
 
+def _fused_sigma_ok(model, pts, layout, variant):
+    """Inference with the renderer's ray layout on a GPU and the sigma
+    networks in the shapes `csrc/sigma.hip` implements: run the fused
+    kernel.  Training (autograd recording) keeps the per-layer path, whose
+    saved activations the backward needs."""
+    return (layout is not None and pts.is_cuda and not torch.is_grad_enabled()
+            and os.environ.get("AVR_FUSED_SIGMA", "1") != "0"
+            and _sigma.variant_of(model) == variant)
+
+
+def _per_ray(x, layout):
+    B, R, S = layout
+    return x.view(B, R, S, 3)[:, :, 0].reshape(B * R, 3)
+
+
+def _per_pose(x, layout):
+    B, R, S = layout
+    return x.view(B, R * S, 3)[:, 0].contiguous()
+
+
+def _sigma_params(model):
+    return _sigma.network_layers(model._model_encoder_sigma) + _sigma.network_layers(model._model_decoder_sigma)
+
+
 def _cat_features(parts, layout):
     """Concatenate per-sample features ([N, E] or [B, R, S, E] views) into
     one contiguous [N, sum E] MLP input."""
@@ -232,6 +257,7 @@ class AVRModel(nn.Module):
         self._model_decoder_sigma = MLP(128, 1, cfg["sigma_decoder_network"], mlp_dtype)
         sig_in = 128 + self._dir_encoding.n_output_dims + self._tx_encoding.n_output_dims
         self._model_signal = MLP(sig_in, self.signal_output_dim, cfg["signal_network"], mlp_dtype)
+        self._sigma_pack = _sigma.SigmaWeights()
 
     # AVRRender passes ray_layout=(B, R, S) to networks that declare this
     accepts_ray_layout = True
@@ -245,6 +271,8 @@ class AVRModel(nn.Module):
             raise NotImplementedError("channel-embedding variants are not provided")
         bs, n = pts.size(0), pts.size(1)
         L = ray_layout
+        if _fused_sigma_ok(self, pts, L, _sigma.MESHRIR):
+            return self._trunk_fused(pts, view, tx, L)
         pos_enc = self._pos_encoding((pts.reshape(-1, 3) + 1) / 2)
         sigma_feat = self._model_encoder_sigma(pos_enc)
         attn = self._model_decoder_sigma(F.relu(sigma_feat))
@@ -255,6 +283,19 @@ class AVRModel(nn.Module):
         base = _cat_features([sf, dir_enc.to(dt), tx_enc.to(dt)], L)
         attn = torch.abs(F.leaky_relu(attn)).view(bs, n, 1)
         return attn, base
+
+    def _trunk_fused(self, pts, view, tx, L):
+        """Encodings (per sample / ray / pose) + one `avr_sigma_fwd` launch:
+        attn [B, N, 1] and the signal network's input [N, 208] (bf16)."""
+        B, R, S = L
+        bs, n = pts.size(0), pts.size(1)
+        pos_enc = self._pos_encoding((pts.reshape(-1, 3) + 1) / 2)
+        dir_e = self._dir_encoding(_per_ray((view.reshape(-1, 3) + 1) / 2, L))
+        tx_e = self._tx_encoding(_per_pose((tx.reshape(-1, 3) + 1) / 2, L))
+        packed = self._sigma_pack.get(_sigma.MESHRIR, _sigma_params(self))
+        attn, base = _sigma.sigma_fwd(_sigma.MESHRIR, packed, bs * n, [(pos_enc, 1)],
+                                      [(dir_e, S), (tx_e, R * S)], 128, 0.01)
+        return attn.view(bs, n, 1), base
 
     def forward(self, pts, view, tx, ch_idx=None, ray_layout=None):
         attn, base = self._trunk(pts, view, tx, ch_idx, ray_layout)
@@ -294,6 +335,7 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
         n_sig = (256 + self._dir_encoding.n_output_dims + self._tx_dir_encoding.n_output_dims
                  + self._pos_signal_encoding.n_output_dims + self._tx_pos_signal_encoding.n_output_dims)
         self._model_signal = MLP(n_sig, self.signal_output_dim, cfg["signal_network"], mlp_dtype)
+        self._sigma_pack = _sigma.SigmaWeights()
 
     accepts_ray_layout = True
     supports_fused_head = True
@@ -314,6 +356,8 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
     def _trunk(self, pts, view, tx, tx_view, ray_layout):
         bs, n = pts.size(0), pts.size(1)
         L = ray_layout
+        if _fused_sigma_ok(self, pts, L, _sigma.RAF):
+            return self._trunk_fused(pts, view, tx, tx_view, L)
         pts = (pts.reshape(-1, 3) + 1) / 2
         view = (view.reshape(-1, 3) + 1) / 2
         tx = (tx.reshape(-1, 3) + 1) / 2
@@ -331,3 +375,21 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
                  _grouped(self._tx_pos_signal_encoding, tx, L, "pose").to(dt)]
         attn = torch.abs(F.leaky_relu(attn, negative_slope=self.leaky_relu)).view(bs, n, 1)
         return attn, _cat_features(parts, L)
+
+    def _trunk_fused(self, pts, view, tx, tx_view, L):
+        """Six encodings at their own granularity + one `avr_sigma_fwd`
+        launch: attn [B, N, 1] and the signal network's input [N, 416]."""
+        B, R, S = L
+        bs, n = pts.size(0), pts.size(1)
+        p = (pts.reshape(-1, 3) + 1) / 2
+        t = _per_pose((tx.reshape(-1, 3) + 1) / 2, L)
+        v = _per_ray((view.reshape(-1, 3) + 1) / 2, L)
+        tv = _per_pose((tx_view.reshape(-1, 3) + 1) / 2, L)
+        packed = self._sigma_pack.get(_sigma.RAF, _sigma_params(self))
+        attn, base = _sigma.sigma_fwd(
+            _sigma.RAF, packed, bs * n,
+            [(self._pos_encoding(p), 1), (self._tx_pos_encoding(t), R * S)],
+            [(self._dir_encoding(v), S), (self._tx_dir_encoding(tv), R * S),
+             (self._pos_signal_encoding(p), 1), (self._tx_pos_signal_encoding(t), R * S)],
+            256, self.leaky_relu)
+        return attn.view(bs, n, 1), base

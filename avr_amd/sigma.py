@@ -1,0 +1,207 @@
+"""Fused sigma networks for inference (`csrc/sigma.hip`, `avr_sigma_fwd`).
+
+The sigma encoder and decoder of the reference networks are width-128
+bias-free ReLU MLPs that tcnn runs as FullyFusedMLP (model.py:117-121,
+146-150, 267-277).  With no autograd graph to record, `AVRModel` and
+`AVRModel_complex` run them, and the concatenation of the signal network's
+input (model.py:221, 325), as one HIP launch: activations stay in registers
+from layer to layer (bf16 MFMA, fp32 accumulation) and the only HBM traffic
+is the encodings in and `base` + `attn` out.
+
+Weights are packed once per parameter version into MFMA A-operand fragments
+(`pack_layers`): fragment (tile ot, k-step ks) holds, for lane l (r = l & 31,
+h = l >> 5) and element j, W[32 ot + r][k] with
+    k = 16 ks + 8 h + j                      first layer (inputs loaded from memory)
+    k = 16 ks + 8 (j >> 2) + 4 h + (j & 3)   later layers (inputs = the previous
+                                             layer's accumulator registers)
+grouped into 32 KB chunks (one LDS stage each) of CO tiles.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+MESHRIR = 0  # AVR_SIGMA_MESHRIR
+RAF = 1      # AVR_SIGMA_RAF
+MAX_EXTRA = 4
+CHUNK = 32768
+
+# per variant: (M, K, first, tiles per chunk) of every layer, in chunk order
+SCHEDULE = {
+    MESHRIR: [(128, 40, True, 4)] + [(128, 128, False, 4)] * 6 + [(1, 128, False, 1)],
+    RAF: [(128, 80, True, 4), (128, 128, False, 4), (128, 128, False, 4), (256, 128, False, 4),
+          (128, 256, False, 2), (1, 128, False, 1)],
+}
+
+
+class FeatSrc(ctypes.Structure):
+    """Mirror of `avr_feat_src` (include/avr_hip.h)."""
+
+    _fields_ = [("data", ctypes.c_void_p), ("dtype", ctypes.c_int32), ("rows_div", ctypes.c_int32)]
+
+
+class SigmaDesc(ctypes.Structure):
+    """Mirror of `avr_sigma_desc` (include/avr_hip.h)."""
+
+    _fields_ = [("variant", ctypes.c_int32), ("tile_cfg", ctypes.c_int32),
+                ("n_samples", ctypes.c_int64), ("leaky_slope", ctypes.c_float),
+                ("input", FeatSrc * 2), ("n_extra", ctypes.c_int32),
+                ("extra", FeatSrc * MAX_EXTRA), ("extra_width", ctypes.c_int32 * MAX_EXTRA)]
+
+
+def fragment_index(M, K, first):
+    """(o, k, valid) arrays of shape [OT, KS, 64, 8]: the weight element each
+    fragment slot holds (see the module docstring)."""
+    OT, KS = -(-M // 32), -(-K // 16)
+    ot, ks, lane, j = np.meshgrid(np.arange(OT), np.arange(KS), np.arange(64), np.arange(8),
+                                  indexing="ij")
+    r, h = lane & 31, lane >> 5
+    o = 32 * ot + r
+    if first:
+        k = 16 * ks + 8 * h + j
+    else:
+        k = 16 * ks + 8 * (j >> 2) + 4 * h + (j & 3)
+    valid = (o < M) & (k < K)
+    return o, k, valid
+
+
+def pack_layers(variant, weights):
+    """Weights (fp32 [M, K] tensors, in SCHEDULE order) -> packed bf16
+    fragments, one 32 KB chunk per LDS stage (zero padded), as a flat
+    torch.bfloat16 tensor on the weights' device."""
+    sched = SCHEDULE[variant]
+    if len(weights) != len(sched):
+        raise ValueError(f"variant {variant} takes {len(sched)} layers, got {len(weights)}")
+    chunks = []
+    for w, (M, K, first, co) in zip(weights, sched):
+        if tuple(w.shape) != (M, K):
+            raise ValueError(f"layer shape {tuple(w.shape)} != {(M, K)}")
+        o, k, valid = fragment_index(M, K, first)
+        OT, KS = o.shape[:2]
+        wp = torch.zeros(OT * 32 + 1, KS * 16 + 1, dtype=torch.float32, device=w.device)
+        wp[:M, :K] = w.detach().float()
+        # invalid slots read the zero corner
+        oi = torch.from_numpy(np.where(valid, o, OT * 32)).to(w.device)
+        ki = torch.from_numpy(np.where(valid, k, KS * 16)).to(w.device)
+        frags = wp[oi, ki].to(torch.bfloat16)  # [OT, KS, 64, 8]
+        for c in range(OT // co):
+            part = frags[c * co:(c + 1) * co].reshape(-1)
+            pad = CHUNK // 2 - part.numel()
+            if pad < 0:
+                raise AssertionError("chunk overflow")
+            chunks.append(torch.cat([part, part.new_zeros(pad)]))
+    return torch.cat(chunks)
+
+
+def network_layers(mlp):
+    """The nn.Linear weights of an `avr_amd.model.MLP`."""
+    return [lin.weight for lin in mlp.layers]
+
+
+def _dims(mlp):
+    return [(lin.weight.shape[0], lin.weight.shape[1]) for lin in mlp.layers]
+
+
+def variant_of(model):
+    """AVR_SIGMA_* if the model's sigma networks have exactly the shapes the
+    fused kernel implements (and bf16 MLPs), else None."""
+    enc, dec = model._model_encoder_sigma, model._model_decoder_sigma
+    if enc.dtype != torch.bfloat16 or dec.dtype != torch.bfloat16:
+        return None
+    dims = _dims(enc) + _dims(dec)
+    for v, sched in SCHEDULE.items():
+        if dims == [(M, K) for M, K, _, _ in sched]:
+            return v
+    return None
+
+
+class SigmaWeights:
+    """Packed fragments of a model's sigma networks, repacked when any weight
+    changes (parameter version counters)."""
+
+    def __init__(self):
+        self.key = None
+        self.packed = None
+
+    def get(self, variant, params):
+        key = (variant,) + tuple((p.data_ptr(), p._version) for p in params)
+        if key != self.key:
+            self.packed = pack_layers(variant, params)
+            self.key = key
+        return self.packed
+
+
+def _src(t, rows_div):
+    if t.dtype == torch.float16:
+        code = _lib.DTYPE_F16
+    elif t.dtype == torch.float32:
+        code = _lib.DTYPE_F32
+    else:
+        raise TypeError(f"sigma inputs must be fp16 or fp32, got {t.dtype}")
+    if not t.is_contiguous() or t.data_ptr() % 16:
+        raise ValueError("sigma inputs must be contiguous and 16-byte aligned")
+    return FeatSrc(t.data_ptr(), code, int(rows_div))
+
+
+def sigma_fwd(variant, packed, n_samples, inputs, extras, out_width, slope, tile_cfg=0):
+    """One launch: inputs = [(tensor [rows, 40], rows_div)] (1 for MESHRIR, 2
+    for RAF); extras = [(tensor [rows, width], rows_div)] appended after the
+    MLP output.  Returns (attn [N] bf16, base [N, out_width + sum widths] bf16)."""
+    dev = packed.device
+    widths = [int(t.size(1)) for t, _ in extras]
+    ldb = out_width + sum(widths)
+    if ldb % 8:
+        raise ValueError("concatenated feature width must be a multiple of 8")
+    base = torch.empty(n_samples, ldb, dtype=torch.bfloat16, device=dev)
+    attn = torch.empty(n_samples, dtype=torch.bfloat16, device=dev)
+    d = SigmaDesc()
+    d.variant = variant
+    d.tile_cfg = tile_cfg
+    d.n_samples = n_samples
+    d.leaky_slope = float(np.float32(slope))
+    for i, (t, div) in enumerate(inputs):
+        if t.size(1) != 40:
+            raise ValueError("sigma network inputs are 40-wide encodings")
+        d.input[i] = _src(t, div)
+    d.n_extra = len(extras)
+    for i, (t, div) in enumerate(extras):
+        d.extra[i] = _src(t, div)
+        d.extra_width[i] = widths[i]
+    keep = [t for t, _ in list(inputs) + list(extras)]  # noqa: F841  (alive across the call)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    _lib.call("avr_sigma_fwd", ctypes.byref(d), ctypes.c_void_p(packed.data_ptr()),
+              ctypes.c_void_p(base.data_ptr()), int(ldb), ctypes.c_void_p(attn.data_ptr()),
+              ctypes.c_void_p(st))
+    return attn, base
+
+
+def reference_fwd(variant, weights, inputs, extras, n_samples, slope):
+    """Plain PyTorch statement of the same computation with the unfused bf16
+    path's roundings (fp32 GEMMs on bf16-rounded operands, bf16 outputs); the
+    test oracle for `sigma_fwd`.  Runs on any device."""
+    bf = torch.bfloat16
+
+    def lin(x, w, relu):
+        y = (x.float() @ w.to(bf).float().t())
+        if relu:
+            y = torch.relu(y)
+        return y.to(bf)
+
+    idx = torch.arange(n_samples, device=weights[0].device)
+    x = torch.cat([t[idx // div].to(bf) for t, div in inputs], -1)
+    nw = len(weights)
+    n_enc = 4
+    for i in range(n_enc - 1):
+        x = lin(x, weights[i], True)
+    feat = lin(x, weights[n_enc - 1], variant == RAF)
+    x = torch.relu(feat)
+    for i in range(n_enc, nw - 1):
+        x = lin(x, weights[i], True)
+    a = lin(x, weights[nw - 1], False).float()
+    attn = torch.abs(torch.where(a > 0, a, a * float(np.float32(slope))).to(bf))
+    base = torch.cat([feat] + [t[idx // div].to(bf) for t, div in extras], -1)
+    return attn.view(-1), base

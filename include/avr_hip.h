@@ -229,6 +229,46 @@ int avr_linear_wgrad_splits(int64_t N, int32_t M, int32_t K, int32_t* splits);
 int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* grad_y, const void* x,
                      float* workspace, int32_t splits, float* grad_w, void* stream);
 
+/* ---- a5/a6: fused sigma networks (inference) ---------------------------
+ * The width-128 bias-free ReLU MLPs the reference runs as tcnn
+ * FullyFusedMLP (sigma encoder + decoder, model.py:117-121, 146-150, 199-216
+ * for AVRModel; 267-277, 314-317 for AVRModel_complex) and the concatenation
+ * of the signal network's input (model.py:221, 325) in one launch:
+ *   AVR_SIGMA_MESHRIR: input[0] = pos_enc [N][40];
+ *     base[n][0:128] = sigma_feat, attn[n] = |leaky_relu(decoder(relu(sigma_feat)))|
+ *     (encoder 40-128-128-128-128, decoder 128-128-128-128-1)
+ *   AVR_SIGMA_RAF: input[0] = pos_e [N][40], input[1] = tx_pos_e (per pose);
+ *     base[n][0:256] = relu(sigma_feature), attn as above with leaky_slope
+ *     (encoder 80-128-128-128-256, decoder 256-128-1)
+ * then base[n][out:...] = the extra sources in order (bf16).  Source rows:
+ * sample n reads row n / rows_div (1 per sample, S per ray, R*S per pose).
+ * wpack = avr_sigma_pack_bytes bytes of bf16 MFMA fragments laid out by
+ * avr_amd/sigma.py (pack_sigma_weights).  base, attn are bf16. */
+#define AVR_SIGMA_MESHRIR 0
+#define AVR_SIGMA_RAF 1
+#define AVR_SIGMA_MAX_EXTRA 4
+typedef struct {
+    const void* data; /* [rows][width], fp16 or fp32, 16-byte aligned */
+    int32_t dtype;    /* AVR_DTYPE_F16 / AVR_DTYPE_F32 */
+    int32_t rows_div;
+} avr_feat_src;
+
+typedef struct {
+    int32_t variant;  /* AVR_SIGMA_* */
+    int32_t tile_cfg; /* 0 = default tiling (tuning knob) */
+    int64_t n_samples;
+    float leaky_slope;
+    avr_feat_src input[2];
+    int32_t n_extra;
+    avr_feat_src extra[AVR_SIGMA_MAX_EXTRA];
+    int32_t extra_width[AVR_SIGMA_MAX_EXTRA];
+} avr_sigma_desc;
+
+int avr_sigma_pack_bytes(int32_t variant, int64_t* bytes);
+int avr_sigma_desc_size(void); /* sizeof(avr_sigma_desc), for binding checks */
+int avr_sigma_fwd(const avr_sigma_desc* d, const void* wpack, void* base, int32_t ldb, void* attn,
+                  void* stream);
+
 /* ---- §8f rank 1: fused signal head -------------------------------------
  * The signal network's last bias-free linear layer (model.py:176-180,
  * output_activation None) folded into the ray reduction:

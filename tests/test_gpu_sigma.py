@@ -1,0 +1,132 @@
+"""GPU: the fused sigma networks (`csrc/sigma.hip`) against the plain
+PyTorch statement of the unfused bf16 path (`sigma.reference_fwd`, fp32
+GEMMs on bf16 operands with bf16 outputs), and inside the networks against
+the per-layer path (AVR_FUSED_SIGMA=0).
+
+Tolerance: both sides round every activation to bf16; they differ only in
+fp32 summation order, so an activation may land one bf16 ulp (2^-8
+relative) apart and the difference propagates through later layers.  The
+bar: relative L2 error <= 4e-3 and >= 99% of elements within 2 bf16 ulps."""
+
+import numpy as np
+import pytest
+import torch
+
+from avr_amd import AVRRender, sigma
+from avr_amd.model import AVRModel, AVRModel_complex
+from avr_amd.workloads import MESHRIR_MODEL, RAF_MODEL, WORKLOADS
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _close(a, b, what):
+    a, b = a.float(), b.float()
+    assert a.shape == b.shape, what
+    assert torch.isfinite(a).all(), what
+    rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
+    within = float(((a - b).abs() <= 2 * 2 ** -8 * b.abs() + 1e-4).float().mean())
+    assert rel <= 4e-3 and within >= 0.99, f"{what}: rel {rel:.2e}, within-2ulp {within:.4f}"
+
+
+def _weights(variant, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    # He-scaled so activations keep their magnitude through the layers
+    return [torch.randn(M, K, device=DEV, generator=g) * np.sqrt(2.0 / K)
+            for M, K, _, _ in sigma.SCHEDULE[variant]]
+
+
+def _sources(variant, N, S, RS, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    B = -(-N // RS)
+    R = RS // S
+    rnd = lambda rows, dt: (torch.rand(rows, 40, device=DEV, generator=g) * 2 - 1).to(dt)  # noqa: E731
+    if variant == sigma.MESHRIR:
+        inputs = [(rnd(N, torch.float16), 1)]
+        extras = [(rnd(B * R, torch.float16), S), (rnd(B, torch.float16), RS)]
+    else:
+        inputs = [(rnd(N, torch.float32), 1), (rnd(B, torch.float32), RS)]
+        extras = [(rnd(B * R, torch.float32), S), (rnd(B, torch.float32), RS),
+                  (rnd(N, torch.float32), 1), (rnd(B, torch.float32), RS)]
+    return inputs, extras
+
+
+@pytest.mark.parametrize("variant", [sigma.MESHRIR, sigma.RAF])
+@pytest.mark.parametrize("N,S,RS", [(32 * 64, 64, 32 * 64), (1000, 10, 500), (7, 7, 7),
+                                    (262144, 256, 262144)])
+def test_sigma_kernel_matches_reference(variant, N, S, RS):
+    ws = _weights(variant, 1)
+    inputs, extras = _sources(variant, N, S, RS, 2)
+    slope = 0.01 if variant == sigma.MESHRIR else 0.03
+    packed = sigma.pack_layers(variant, ws)
+    out_w = 128 if variant == sigma.MESHRIR else 256
+    ra, rb = sigma.reference_fwd(variant, ws, inputs, extras, N, slope)
+    for cfg in (0, 1, 2, 3):
+        attn, base = sigma.sigma_fwd(variant, packed, N, inputs, extras, out_w, slope, tile_cfg=cfg)
+        torch.cuda.synchronize()
+        _close(base[:, :out_w], rb[:, :out_w], f"features cfg {cfg}")
+        # the copied encodings are exact (fp16/fp32 -> bf16)
+        assert torch.equal(base[:, out_w:], rb[:, out_w:])
+        _close(attn, ra, f"attn cfg {cfg}")
+
+
+def test_sigma_rejects_bad_arguments():
+    ws = _weights(sigma.MESHRIR, 0)
+    packed = sigma.pack_layers(sigma.MESHRIR, ws)
+    x = torch.zeros(64, 40, dtype=torch.float16, device=DEV)
+    with pytest.raises(ValueError):
+        sigma.sigma_fwd(sigma.MESHRIR, packed, 64, [(x[:, :39], 1)], [], 128, 0.01)
+    with pytest.raises(RuntimeError):  # rows_div 0 is refused by the library
+        sigma.sigma_fwd(sigma.MESHRIR, packed, 64, [(x, 0)], [], 128, 0.01)
+
+
+def _net_pair(cls):
+    w = WORKLOADS["c1_meshrir_plumbing"]
+    B, R, S = 2, w.n_rays, w.n_samples
+    torch.manual_seed(0)
+    if cls == "AVRModel":
+        m = AVRModel(dict(MESHRIR_MODEL, signal_output_dim=254), mlp_dtype=torch.bfloat16).to(DEV)
+        extra = ()
+    else:
+        m = AVRModel_complex(dict(RAF_MODEL, signal_output_dim=254), mlp_dtype=torch.bfloat16).to(DEV)
+        extra = (torch.rand(B, R * S, 3, device=DEV) * 2 - 1,)
+    # trained-looking weights: He-scaled instead of nn.Linear's default
+    for p in m.parameters():
+        if p.dim() == 2:
+            p.data.normal_(0, float(np.sqrt(2.0 / p.size(1))))
+    pts = torch.rand(B, R * S, 3, device=DEV) * 2 - 1
+    view = torch.rand(B, R, 1, 3, device=DEV).expand(B, R, S, 3).reshape(B, R * S, 3) * 2 - 1
+    tx = torch.rand(B, 1, 3, device=DEV).expand(B, R * S, 3).contiguous() * 2 - 1
+    if extra:
+        extra = (extra[0][:, :1].expand(B, R * S, 3).contiguous(),)
+    return m, (pts, view, tx) + extra, (B, R, S)
+
+
+@pytest.mark.parametrize("cls", ["AVRModel", "AVRModel_complex"])
+def test_network_fused_sigma_matches_per_layer(cls, monkeypatch):
+    m, args, L = _net_pair(cls)
+    with torch.no_grad():
+        monkeypatch.setenv("AVR_FUSED_SIGMA", "0")
+        a0, h0, _, _ = m.forward_fused(*args, ray_layout=L)
+        monkeypatch.setenv("AVR_FUSED_SIGMA", "1")
+        a1, h1, _, _ = m.forward_fused(*args, ray_layout=L)
+    torch.cuda.synchronize()
+    _close(a1, a0, "attn")
+    _close(h1, h0, "signal hidden")
+
+
+def test_render_with_fused_sigma_matches_per_layer(monkeypatch):
+    w = WORKLOADS["c1_meshrir_plumbing"].replace(T=1022)
+    m = AVRModel(dict(MESHRIR_MODEL, signal_output_dim=1022), mlp_dtype=torch.bfloat16).to(DEV)
+    r = AVRRender(m, **w.render).to(DEV)
+    ro = torch.rand(1, 3, device=DEV) * 2 - 1
+    tx = torch.rand(1, 3, device=DEV) * 2 - 1
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("AVR_FUSED_SIGMA", flag)
+        torch.manual_seed(5)
+        with torch.no_grad():
+            outs.append(r(ro, tx))
+    torch.cuda.synchronize()
+    rel = float((outs[1] - outs[0]).norm() / outs[0].norm())
+    assert rel < 2e-2, rel

@@ -1,7 +1,8 @@
 """End-to-end inference benchmark: the reference network (AVRModel, MeshRIR
 `model:` block, random weights) + the renderer + IR for config 2
 (1024 rays x 256 samples, T=1022), with and without the fused signal head
-(SURVEY.md §8f rank 1).  One pose per step, no grad.
+ and with / without the fused sigma networks
+(csrc/sigma.hip).  One pose per step, no grad.
 
     python tools/bench_infer.py [--steps 20] [--mlp-dtype bf16]
 """
@@ -41,7 +42,9 @@ def main():
     res = {"workload": w.name, "ray_samples_per_pose": w.ray_samples, "mlp_dtype": args.mlp_dtype,
            "network": "AVRModel (avr_meshrir.yml model block, random init)"}
     outs = {}
-    for fused in (False, True):
+    # (key, fused signal head, fused sigma networks)
+    for key, fused, fsig in (("unfused", False, "0"), ("fused_head_only", True, "0"), ("fused", True, "1")):
+        os.environ["AVR_FUSED_SIGMA"] = fsig
         r = AVRRender(model, fused_head=fused, **w.render)
 
         def step():
@@ -56,7 +59,6 @@ def main():
             out = step()
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / args.steps
-        key = "fused" if fused else "unfused"
         res[f"{key}_ms_per_pose"] = ms
         res[f"{key}_ray_samples_per_s"] = w.ray_samples / (ms * 1e-3)
         torch.manual_seed(0)
