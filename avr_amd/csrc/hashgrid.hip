@@ -118,6 +118,46 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(int64_t N, int L,
     store_pair(out, q, acc);
 }
 
+// Level-major forward for inference: grid (points / 256, L), blockIdx.y =
+// level, so the blocks in flight work on one or two levels at a time and the
+// level's table (<= 2 MiB fp32) stays resident in each XCD's 4 MiB L2
+// instead of all L tables (36 MiB for the MeshRIR position grid) streaming
+// from the Infinity Cache.  out is level-major [L][N][2] (coalesced stores);
+// consumers read feature pair l of point i at out[l*N + i].
+template <typename Tp, typename To>
+__global__ __launch_bounds__(256) void hashgrid_fwd_lm_kernel(int64_t N, const float* __restrict__ x,
+                                                              const Tp* __restrict__ params,
+                                                              LevelTable lt, To* __restrict__ out) {
+    const int l = blockIdx.y;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    const float xi[3] = {x[i * 3 + 0], x[i * 3 + 1], x[i * 3 + 2]};
+    const Corner c = locate(xi, lt.scale[l]);
+    const uint32_t size = (uint32_t)(lt.offset[l + 1] - lt.offset[l]);
+    const uint32_t res = lt.res[l];
+    const Tp* table = params + 2 * lt.offset[l];
+    float2 acc = make_float2(0.0f, 0.0f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        float wgt = 1.0f;
+        uint32_t g[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            if (k & (1 << d)) {
+                wgt *= c.pos[d];
+                g[d] = c.grid[d] + 1;
+            } else {
+                wgt *= 1.0f - c.pos[d];
+                g[d] = c.grid[d];
+            }
+        }
+        const float2 v = load_pair(table, grid_index(size, res, g[0], g[1], g[2]));
+        acc.x = fmaf(wgt, v.x, acc.x);
+        acc.y = fmaf(wgt, v.y, acc.y);
+    }
+    store_pair(out, (int64_t)l * N + i, acc);
+}
+
 // Backward: scatter-add of w_corner * dL/dy into the tables.
 //
 // Float atomics execute at the memory side and cost one request per 64-B
@@ -247,4 +287,32 @@ extern "C" int avr_hashgrid_bwd(int64_t N, int32_t n_levels, const float* x, con
     else
         return fail(AVR_E_ARG, "avr_hashgrid_bwd: unknown grad dtype");
     return check_launch("avr_hashgrid_bwd");
+}
+
+extern "C" int avr_hashgrid_fwd_lm(int64_t N, int32_t n_levels, const float* x, const void* params,
+                                   int32_t param_dtype, const int64_t* level_offset,
+                                   const float* level_scale, const int32_t* level_res, void* out,
+                                   int32_t out_dtype, void* stream) {
+    AVR_REQUIRE(N >= 0 && x && params && level_offset && level_scale && level_res && out,
+                "avr_hashgrid_fwd_lm: bad args");
+    if (N == 0) return 0;
+    LevelTable lt;
+    if (int e = make_table(n_levels, level_offset, level_scale, level_res, &lt)) return e;
+    const dim3 grid((unsigned)((N + 255) / 256), (unsigned)n_levels);
+    hipStream_t st = as_stream(stream);
+    if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F32)
+        hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<float, float>), grid, dim3(256), 0, st, N, x,
+                           (const float*)params, lt, (float*)out);
+    else if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F16)
+        hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<float, __half>), grid, dim3(256), 0, st, N, x,
+                           (const float*)params, lt, (__half*)out);
+    else if (param_dtype == AVR_DTYPE_F16 && out_dtype == AVR_DTYPE_F16)
+        hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<__half, __half>), grid, dim3(256), 0, st, N, x,
+                           (const __half*)params, lt, (__half*)out);
+    else if (param_dtype == AVR_DTYPE_F16 && out_dtype == AVR_DTYPE_F32)
+        hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<__half, float>), grid, dim3(256), 0, st, N, x,
+                           (const __half*)params, lt, (float*)out);
+    else
+        return fail(AVR_E_ARG, "avr_hashgrid_fwd_lm: unknown dtype");
+    return check_launch("avr_hashgrid_fwd_lm");
 }

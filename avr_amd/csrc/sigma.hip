@@ -55,6 +55,7 @@ struct Src {
     const void* p;
     int dtype;
     int rows_div;
+    int64_t lm_rows;  // 0: row-major [rows][width]; else level-major [width/2][lm_rows][2]
 };
 
 struct Args {
@@ -87,7 +88,21 @@ __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t u) {
 // 8 consecutive features (fp16 or fp32) of row `row` starting at `col` -> bf16
 __device__ __forceinline__ bf16x8 load8(const Src& s, int64_t row, int width, int col) {
     float f[8];
-    if (s.dtype == AVR_DTYPE_F16) {
+    if (s.lm_rows > 0) {  // feature pairs col/2 .. col/2+3 of the row, one per level plane
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t e = ((int64_t)(col / 2 + q) * s.lm_rows + row) * 2;
+            if (s.dtype == AVR_DTYPE_F16) {
+                const float2 v = __half22float2(*reinterpret_cast<const __half2*>(static_cast<const __half*>(s.p) + e));
+                f[2 * q] = v.x;
+                f[2 * q + 1] = v.y;
+            } else {
+                const float2 v = *reinterpret_cast<const float2*>(static_cast<const float*>(s.p) + e);
+                f[2 * q] = v.x;
+                f[2 * q + 1] = v.y;
+            }
+        }
+    } else if (s.dtype == AVR_DTYPE_F16) {
         const u32x4v v = *reinterpret_cast<const u32x4v*>(
             static_cast<const __half*>(s.p) + row * width + col);
         Vec16<__half>::cvt(v, f);
@@ -103,8 +118,6 @@ __device__ __forceinline__ bf16x8 load8(const Src& s, int64_t row, int width, in
     for (int q = 0; q < 4; ++q) r[q] = pack_bf16(f[2 * q], f[2 * q + 1]);
     return __builtin_bit_cast(bf16x8, r);
 }
-
-__device__ __forceinline__ float relu(float v) { return v < 0.0f ? 0.0f : v; }  // NaN passes
 
 // Cooperative global -> LDS staging of 32 KB chunks into two LDS buffers.
 // Chunk c is read from buffer c & 1; while it is computed, chunk c+1 sits in
@@ -409,10 +422,10 @@ void sigma_raf_kernel(Args a) {
 
 bool src_ok(const avr_feat_src& s) {
     return s.data && (s.dtype == AVR_DTYPE_F16 || s.dtype == AVR_DTYPE_F32) && s.rows_div >= 1 &&
-           reinterpret_cast<uintptr_t>(s.data) % 16 == 0;
+           s.lm_rows >= 0 && reinterpret_cast<uintptr_t>(s.data) % 16 == 0;
 }
 
-Src to_src(const avr_feat_src& s) { return Src{s.data, (int)s.dtype, (int)s.rows_div}; }
+Src to_src(const avr_feat_src& s) { return Src{s.data, (int)s.dtype, (int)s.rows_div, s.lm_rows}; }
 
 template <int NT, int WAVES, int OCC, int DBG = 0>
 int launch_meshrir(const Args& a, hipStream_t st) {

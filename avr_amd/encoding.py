@@ -109,6 +109,20 @@ class HashGridEncoding(nn.Module):
         init = (torch.rand(self.n_params, generator=g) * 2 - 1) * 1e-4
         self.params = nn.Parameter(init)
 
+    def forward_level_major(self, x):
+        """Inference-only encoding with level-major output [L, N, 2]
+        (`avr_hashgrid_fwd_lm`): the same values as forward(x) transposed."""
+        if not x.is_cuda:
+            raise RuntimeError("HashGridEncoding needs a HIP tensor (no CPU fallback)")
+        x = x.reshape(-1, 3).float().contiguous()
+        N = x.size(0)
+        out = torch.empty(self.n_levels, N, 2, dtype=self.dtype, device=x.device)
+        st = torch.cuda.current_stream(x.device).cuda_stream
+        _lib.call("avr_hashgrid_fwd_lm", N, self.n_levels, x.data_ptr(), self.params.data_ptr(),
+                  _code(self.params.dtype), self._off.ctypes.data, self._scale.ctypes.data,
+                  self._res.ctypes.data, out.data_ptr(), _code(out.dtype), st)
+        return out
+
     def forward(self, x):
         if not x.is_cuda:
             raise RuntimeError("HashGridEncoding needs a HIP tensor (no CPU fallback)")

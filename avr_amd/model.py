@@ -17,6 +17,7 @@ import torch.nn.functional as F
 
 from . import sigma as _sigma
 from .encoding import HashGridEncoding
+from .wcache import cast_weight
 
 
 import os
@@ -81,8 +82,8 @@ class _Linear(torch.autograd.Function):
     the weight gradient uses the split-K GEMM above and is returned in fp32."""
 
     @staticmethod
-    def forward(ctx, x, w_master, dtype):
-        w = w_master.to(dtype)
+    def forward(ctx, x, w_master, dtype, cache=False):
+        w = cast_weight(w_master, dtype, cache)
         ctx.save_for_backward(x, w)
         return x @ w.t()
 
@@ -92,7 +93,7 @@ class _Linear(torch.autograd.Function):
         gy = gy.contiguous()
         gx = gy @ w if ctx.needs_input_grad[0] else None
         gw = _wgrad(gy, x) if ctx.needs_input_grad[1] else None
-        return gx, gw, None
+        return gx, gw, None, None
 
 
 _ZERO_BIAS: dict = {}
@@ -115,8 +116,8 @@ class _LinearReLU(torch.autograd.Function):
     same data / weight gradients as `_Linear`."""
 
     @staticmethod
-    def forward(ctx, x, w_master, dtype):
-        w = w_master.to(dtype)
+    def forward(ctx, x, w_master, dtype, cache=False):
+        w = cast_weight(w_master, dtype, cache)
         if x.is_cuda:
             y = torch._addmm_activation(_zero_bias(w.size(0), dtype, x.device), x, w.t(),
                                         use_gelu=False)
@@ -131,7 +132,7 @@ class _LinearReLU(torch.autograd.Function):
         g = torch.ops.aten.threshold_backward(gy, y, 0).contiguous()
         gx = g @ w if ctx.needs_input_grad[0] else None
         gw = _wgrad(g, x) if ctx.needs_input_grad[1] else None
-        return gx, gw, None
+        return gx, gw, None, None
 
 
 class MLP(nn.Module):
@@ -154,12 +155,12 @@ class MLP(nn.Module):
         output layer is applied to."""
         x = x.to(self.dtype).contiguous()
         for lin in self.layers[:-1]:
-            x = _LinearReLU.apply(x, lin.weight, self.dtype)
+            x = _LinearReLU.apply(x, lin.weight, self.dtype, not torch.is_grad_enabled())
         return x
 
     def last(self, h):
         """The bias-free output layer (output_activation None)."""
-        return _Linear.apply(h.contiguous(), self.layers[-1].weight, self.dtype)
+        return _Linear.apply(h.contiguous(), self.layers[-1].weight, self.dtype, not torch.is_grad_enabled())
 
     def forward(self, x, out_relu=False):
         """The network; `out_relu=True` returns relu(output) with the ReLU in
@@ -167,7 +168,8 @@ class MLP(nn.Module):
         output, model.py:316, 323)."""
         h = self.hidden(x)
         if out_relu:
-            return _LinearReLU.apply(h.contiguous(), self.layers[-1].weight, self.dtype)
+            return _LinearReLU.apply(h.contiguous(), self.layers[-1].weight, self.dtype,
+                                     not torch.is_grad_enabled())
         return self.last(h)
 
 
@@ -289,7 +291,7 @@ class AVRModel(nn.Module):
         attn [B, N, 1] and the signal network's input [N, 208] (bf16)."""
         B, R, S = L
         bs, n = pts.size(0), pts.size(1)
-        pos_enc = self._pos_encoding((pts.reshape(-1, 3) + 1) / 2)
+        pos_enc = self._pos_encoding.forward_level_major((pts.reshape(-1, 3) + 1) / 2)
         dir_e = self._dir_encoding(_per_ray((view.reshape(-1, 3) + 1) / 2, L))
         tx_e = self._tx_encoding(_per_pose((tx.reshape(-1, 3) + 1) / 2, L))
         packed = self._sigma_pack.get(_sigma.MESHRIR, _sigma_params(self))
@@ -388,8 +390,8 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
         packed = self._sigma_pack.get(_sigma.RAF, _sigma_params(self))
         attn, base = _sigma.sigma_fwd(
             _sigma.RAF, packed, bs * n,
-            [(self._pos_encoding(p), 1), (self._tx_pos_encoding(t), R * S)],
+            [(self._pos_encoding.forward_level_major(p), 1), (self._tx_pos_encoding(t), R * S)],
             [(self._dir_encoding(v), S), (self._tx_dir_encoding(tv), R * S),
-             (self._pos_signal_encoding(p), 1), (self._tx_pos_signal_encoding(t), R * S)],
+             (self._pos_signal_encoding.forward_level_major(p), 1), (self._tx_pos_signal_encoding(t), R * S)],
             256, self.leaky_relu)
         return attn.view(bs, n, 1), base

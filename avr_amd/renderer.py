@@ -29,6 +29,7 @@ import torch.nn as nn
 
 from . import _lib
 from ._lib import DTYPE_BF16, DTYPE_F16, DTYPE_F32, render_params
+from .wcache import cast_weight
 
 # Optional instrumentation for bench.py: an object with begin(stream) / end(stream)
 # called around the dominant kernel (the ray-reduction stream).  None in normal use.
@@ -302,13 +303,13 @@ class FusedHeadCore(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, attn, h, w_master, dtype, p, tables, rays_o, position_tx, dirs):
+    def forward(ctx, attn, h, w_master, dtype, p, tables, rays_o, position_tx, dirs, cache=False):
         dev = h.device
         B, K = h.size(0), h.size(-1)
         S, T = p.n_samples, p.T
         st = _stream(dev)
         pref = ctypes_ref(p)
-        W = w_master.to(dtype).contiguous()
+        W = cast_weight(w_master, dtype, cache)
         code = _dtype_code(h)
         w, delay = _weights(p, attn, rays_o, position_tx, dirs, tables, st)
         R = p.n_rays
@@ -349,7 +350,7 @@ class FusedHeadCore(torch.autograd.Function):
                   _ptr(work), nbytes.value, st)
         grad_attn = _grad_attn(p, tables, attn, grad_w, st) if ctx.needs_input_grad[0] else None
         return (grad_attn, grad_h if ctx.needs_input_grad[1] else None,
-                grad_W if ctx.needs_input_grad[2] else None, None, None, None, None, None, None)
+                grad_W if ctx.needs_input_grad[2] else None, None, None, None, None, None, None, None)
 
 
 # --------------------------------------------------------------------------
@@ -539,7 +540,7 @@ class AVRRender(nn.Module):
             tables = get_tables(p, dev)
             check_config(p, tables)
             return FusedHeadCore.apply(attn, h, weight, dtype, p, tables, geom["rays_o"],
-                                       geom["position_tx"], geom["dirs"])
+                                       geom["position_tx"], geom["dirs"], not torch.is_grad_enabled())
 
     def forward(self, rays_o, position_tx, direction_tx=None, ch_idx=None):
         """Render [B, F, 2] (real, imag) spectra; see renderer.py:31-124."""

@@ -41,7 +41,8 @@ SCHEDULE = {
 class FeatSrc(ctypes.Structure):
     """Mirror of `avr_feat_src` (include/avr_hip.h)."""
 
-    _fields_ = [("data", ctypes.c_void_p), ("dtype", ctypes.c_int32), ("rows_div", ctypes.c_int32)]
+    _fields_ = [("data", ctypes.c_void_p), ("dtype", ctypes.c_int32), ("rows_div", ctypes.c_int32),
+                ("lm_rows", ctypes.c_int64)]
 
 
 class SigmaDesc(ctypes.Structure):
@@ -136,6 +137,8 @@ class SigmaWeights:
 
 
 def _src(t, rows_div):
+    """FeatSrc of a [rows, width] tensor, or of a level-major [L, rows, 2]
+    hash-grid output (HashGridEncoding.forward_level_major)."""
     if t.dtype == torch.float16:
         code = _lib.DTYPE_F16
     elif t.dtype == torch.float32:
@@ -144,15 +147,27 @@ def _src(t, rows_div):
         raise TypeError(f"sigma inputs must be fp16 or fp32, got {t.dtype}")
     if not t.is_contiguous() or t.data_ptr() % 16:
         raise ValueError("sigma inputs must be contiguous and 16-byte aligned")
-    return FeatSrc(t.data_ptr(), code, int(rows_div))
+    lm = int(t.size(1)) if t.dim() == 3 else 0
+    return FeatSrc(t.data_ptr(), code, int(rows_div), lm)
+
+
+def _width(t):
+    return int(t.size(0) * t.size(2)) if t.dim() == 3 else int(t.size(1))
+
+
+def _rows(t, idx):
+    """Rows idx of a row-major or level-major source as [len(idx), width]."""
+    if t.dim() == 3:
+        return t[:, idx].permute(1, 0, 2).reshape(len(idx), -1)
+    return t[idx]
 
 
 def sigma_fwd(variant, packed, n_samples, inputs, extras, out_width, slope, tile_cfg=0):
-    """One launch: inputs = [(tensor [rows, 40], rows_div)] (1 for MESHRIR, 2
-    for RAF); extras = [(tensor [rows, width], rows_div)] appended after the
-    MLP output.  Returns (attn [N] bf16, base [N, out_width + sum widths] bf16)."""
+    """One launch: inputs = [(tensor [rows, 40] or level-major [20, rows, 2],
+    rows_div)] (1 for MESHRIR, 2 for RAF); extras = [(tensor, rows_div)]
+    appended after the MLP output.  Returns (attn [N] bf16, base [N, out_width + sum widths] bf16)."""
     dev = packed.device
-    widths = [int(t.size(1)) for t, _ in extras]
+    widths = [_width(t) for t, _ in extras]
     ldb = out_width + sum(widths)
     if ldb % 8:
         raise ValueError("concatenated feature width must be a multiple of 8")
@@ -164,7 +179,7 @@ def sigma_fwd(variant, packed, n_samples, inputs, extras, out_width, slope, tile
     d.n_samples = n_samples
     d.leaky_slope = float(np.float32(slope))
     for i, (t, div) in enumerate(inputs):
-        if t.size(1) != 40:
+        if _width(t) != 40:
             raise ValueError("sigma network inputs are 40-wide encodings")
         d.input[i] = _src(t, div)
     d.n_extra = len(extras)
@@ -192,7 +207,7 @@ def reference_fwd(variant, weights, inputs, extras, n_samples, slope):
         return y.to(bf)
 
     idx = torch.arange(n_samples, device=weights[0].device)
-    x = torch.cat([t[idx // div].to(bf) for t, div in inputs], -1)
+    x = torch.cat([_rows(t, idx // div).to(bf) for t, div in inputs], -1)
     nw = len(weights)
     n_enc = 4
     for i in range(n_enc - 1):
@@ -203,5 +218,5 @@ def reference_fwd(variant, weights, inputs, extras, n_samples, slope):
         x = lin(x, weights[i], True)
     a = lin(x, weights[nw - 1], False).float()
     attn = torch.abs(torch.where(a > 0, a, a * float(np.float32(slope))).to(bf))
-    base = torch.cat([feat] + [t[idx // div].to(bf) for t, div in extras], -1)
+    base = torch.cat([feat] + [_rows(t, idx // div).to(bf) for t, div in extras], -1)
     return attn.view(-1), base

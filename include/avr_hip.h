@@ -213,6 +213,12 @@ int avr_hashgrid_fwd(int64_t N, int32_t n_levels, const float* x, const void* pa
                      int32_t param_dtype, const int64_t* level_offset, const float* level_scale,
                      const int32_t* level_res, void* out, int32_t out_dtype, void* stream);
 
+/* Same encoding, level-major output out[L][N][2] (inference: the blocks in
+ * flight share one level's table, which then stays in L2). */
+int avr_hashgrid_fwd_lm(int64_t N, int32_t n_levels, const float* x, const void* params,
+                        int32_t param_dtype, const int64_t* level_offset, const float* level_scale,
+                        const int32_t* level_res, void* out, int32_t out_dtype, void* stream);
+
 /* grad_out[N][L*2] -> grad_params (fp32, accumulated with atomics; zero it
  * first). */
 int avr_hashgrid_bwd(int64_t N, int32_t n_levels, const float* x, const void* grad_out,
@@ -248,9 +254,11 @@ int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* grad_y, const 
 #define AVR_SIGMA_RAF 1
 #define AVR_SIGMA_MAX_EXTRA 4
 typedef struct {
-    const void* data; /* [rows][width], fp16 or fp32, 16-byte aligned */
+    const void* data; /* [rows][width] (row-major) or [width/2][rows][2] (level-major,
+                         avr_hashgrid_fwd_lm output), fp16 or fp32, 16-byte aligned */
     int32_t dtype;    /* AVR_DTYPE_F16 / AVR_DTYPE_F32 */
     int32_t rows_div;
+    int64_t lm_rows;  /* 0: row-major; > 0: level-major with this many rows */
 } avr_feat_src;
 
 typedef struct {

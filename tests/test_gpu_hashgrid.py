@@ -57,3 +57,17 @@ def test_level_layout_matches_tcnn_rule():
     assert list(res[:4]) == [16, 32, 64, 128]
     assert list(sizes[:4]) == [4096, 32768, 262144, 262144]
     assert int(off[-1]) * 2 == 9510912  # 9.51M params, SURVEY.md §8 a5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_level_major_forward_is_transposed_forward(dtype):
+    """avr_hashgrid_fwd_lm: same values as the row-major kernel, [L, N, 2]."""
+    enc = HashGridEncoding(3, CFG, dtype=dtype, seed=7).to(DEV)
+    with torch.no_grad():
+        enc.params.uniform_(-1, 1)
+        for n in (8, 255, 4097):
+            x = torch.from_numpy(_points(n, 1)).to(DEV)
+            a = enc(x)
+            b = enc.forward_level_major(x)
+            assert b.shape == (20, n, 2)
+            assert torch.equal(a, b.permute(1, 0, 2).reshape(n, 40))

@@ -130,3 +130,20 @@ def test_render_with_fused_sigma_matches_per_layer(monkeypatch):
     torch.cuda.synchronize()
     rel = float((outs[1] - outs[0]).norm() / outs[0].norm())
     assert rel < 2e-2, rel
+
+
+@pytest.mark.parametrize("variant", [sigma.MESHRIR, sigma.RAF])
+def test_level_major_sources_match_row_major(variant):
+    """Per-sample encodings handed over level-major ([20, N, 2], the
+    avr_hashgrid_fwd_lm output) give bit-identical results."""
+    N, S, RS = 4096, 64, 4096
+    ws = _weights(variant, 3)
+    inputs, extras = _sources(variant, N, S, RS, 4)
+    packed = sigma.pack_layers(variant, ws)
+    out_w = 128 if variant == sigma.MESHRIR else 256
+    lm = lambda t, d: (t.view(-1, 20, 2).permute(1, 0, 2).contiguous(), d) if d == 1 else (t, d)  # noqa: E731
+    a0, b0 = sigma.sigma_fwd(variant, packed, N, inputs, extras, out_w, 0.02)
+    a1, b1 = sigma.sigma_fwd(variant, packed, N, [lm(*i) for i in inputs], [lm(*e) for e in extras],
+                             out_w, 0.02)
+    torch.cuda.synchronize()
+    assert torch.equal(a0, a1) and torch.equal(b0, b1)

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mlp-dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--variants", default="unfused,fused_head_only,fused")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     w = WORKLOADS[args.workload]
@@ -44,6 +45,8 @@ def main():
     outs = {}
     # (key, fused signal head, fused sigma networks)
     for key, fused, fsig in (("unfused", False, "0"), ("fused_head_only", True, "0"), ("fused", True, "1")):
+        if key not in args.variants.split(","):
+            continue
         os.environ["AVR_FUSED_SIGMA"] = fsig
         r = AVRRender(model, fused_head=fused, **w.render)
 
@@ -63,7 +66,8 @@ def main():
         res[f"{key}_ray_samples_per_s"] = w.ray_samples / (ms * 1e-3)
         torch.manual_seed(0)
         outs[key] = out
-    res["speedup"] = res["unfused_ms_per_pose"] / res["fused_ms_per_pose"]
+    if "unfused_ms_per_pose" in res and "fused_ms_per_pose" in res:
+        res["speedup"] = res["unfused_ms_per_pose"] / res["fused_ms_per_pose"]
     print(json.dumps(res))
 
 

@@ -11,4 +11,4 @@ timeout -k 10 200 python tools/probe_sigma.py --variant 1 --cfgs 0,1 >> gpurun_o
 grep -v amdgpu gpurun_out/probe_sigma.log
 timeout -k 10 300 python tools/bench_infer.py > gpurun_out/infer.log 2>&1 || exit 1
 tail -1 gpurun_out/infer.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profinfer -o run --output-format csv -- python tools/bench_infer.py --steps 5 --warmup 2 > gpurun_out/profinfer.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/profinfer -o run --output-format csv -- python tools/bench_infer.py --steps 5 --warmup 2 --variants fused > gpurun_out/profinfer.log 2>&1 || exit 1
