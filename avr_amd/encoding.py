@@ -26,6 +26,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from .wcache import cast_weight
 from ._lib import DTYPE_F16, DTYPE_F32
 
 
@@ -58,12 +59,13 @@ def _code(dtype):
 
 class _HashGridFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, params, enc):
+    def forward(ctx, x, params, enc, cache=False):
         N = x.size(0)
         out = torch.empty(N, enc.n_output_dims, dtype=enc.dtype, device=x.device)
         st = torch.cuda.current_stream(x.device).cuda_stream
-        _lib.call("avr_hashgrid_fwd", N, enc.n_levels, x.data_ptr(), params.data_ptr(),
-                  _code(params.dtype), enc._off.ctypes.data, enc._scale.ctypes.data,
+        table = enc.table(cache)
+        _lib.call("avr_hashgrid_fwd", N, enc.n_levels, x.data_ptr(), table.data_ptr(),
+                  _code(table.dtype), enc._off.ctypes.data, enc._scale.ctypes.data,
                   enc._res.ctypes.data, out.data_ptr(), _code(out.dtype), st)
         ctx.enc = enc
         ctx.save_for_backward(x)
@@ -81,7 +83,7 @@ class _HashGridFn(torch.autograd.Function):
         _lib.call("avr_hashgrid_bwd", x.size(0), enc.n_levels, x.data_ptr(), g.data_ptr(),
                   _code(g.dtype), enc._off.ctypes.data, enc._scale.ctypes.data,
                   enc._res.ctypes.data, gp.data_ptr(), st)
-        return None, gp, None
+        return None, gp, None, None
 
 
 class HashGridEncoding(nn.Module):
@@ -102,12 +104,20 @@ class HashGridEncoding(nn.Module):
         self.per_level_scale = float(cfg.get("per_level_scale", 2.0))
         self.n_output_dims = 2 * self.n_levels
         self.dtype = torch.float16 if dtype is None else dtype
+        # tcnn runs a module's forward on params cast to its precision
+        # (Module.forward: self.params.to(param_precision)): fp16 tables for
+        # fp16 encodings, the fp32 master copy receives the gradient
+        self.param_dtype = torch.float16 if self.dtype == torch.float16 else torch.float32
         self._off, self._scale, self._res = level_layout(self.n_levels, self.log2_hashmap_size,
                                                          self.base_resolution, self.per_level_scale)
         self.n_params = int(self._off[-1]) * 2
         g = torch.Generator().manual_seed(1337 if seed is None else seed)
         init = (torch.rand(self.n_params, generator=g) * 2 - 1) * 1e-4
         self.params = nn.Parameter(init)
+
+    def table(self, cache=False):
+        """The level tables in the module's param precision."""
+        return cast_weight(self.params, self.param_dtype, cache)
 
     def forward_level_major(self, x):
         """Inference-only encoding with level-major output [L, N, 2]
@@ -118,8 +128,9 @@ class HashGridEncoding(nn.Module):
         N = x.size(0)
         out = torch.empty(self.n_levels, N, 2, dtype=self.dtype, device=x.device)
         st = torch.cuda.current_stream(x.device).cuda_stream
-        _lib.call("avr_hashgrid_fwd_lm", N, self.n_levels, x.data_ptr(), self.params.data_ptr(),
-                  _code(self.params.dtype), self._off.ctypes.data, self._scale.ctypes.data,
+        table = self.table(not torch.is_grad_enabled())
+        _lib.call("avr_hashgrid_fwd_lm", N, self.n_levels, x.data_ptr(), table.data_ptr(),
+                  _code(table.dtype), self._off.ctypes.data, self._scale.ctypes.data,
                   self._res.ctypes.data, out.data_ptr(), _code(out.dtype), st)
         return out
 
@@ -127,4 +138,4 @@ class HashGridEncoding(nn.Module):
         if not x.is_cuda:
             raise RuntimeError("HashGridEncoding needs a HIP tensor (no CPU fallback)")
         x = x.reshape(-1, 3).float().contiguous()
-        return _HashGridFn.apply(x, self.params, self)
+        return _HashGridFn.apply(x, self.params, self, not torch.is_grad_enabled())

@@ -32,8 +32,10 @@ def test_forward_matches_restatement(dtype):
         enc.params.uniform_(-1, 1)
     x = _points(4096, 0)
     out = enc(torch.from_numpy(x).to(DEV)).detach().float().cpu().numpy()
-    ref = hgo.encode(x, enc.params.detach().cpu().numpy(), enc._off, enc._scale, enc._res)
-    tol = 2e-6 if dtype == torch.float32 else 2e-3
+    # fp16 encodings read fp16 tables (tcnn's param precision), fp32 ones fp32
+    table = enc.params.detach().to(enc.param_dtype).float().cpu().numpy()
+    ref = hgo.encode(x, table, enc._off, enc._scale, enc._res)
+    tol = 2e-6 if dtype == torch.float32 else 1e-3
     np.testing.assert_allclose(out, ref, rtol=tol, atol=tol)
 
 

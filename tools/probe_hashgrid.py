@@ -25,7 +25,7 @@ def main():
     r = AVRRender(_Null(), **w.render)
     pts = r.sample(torch.rand(1, 3, device=dev) * 4 - 2, torch.rand(1, 3, device=dev) * 4 - 2)[0]
     x = ((pts.reshape(-1, 3) + 1) / 2).contiguous()
-    for dt in (torch.float16,):
+    for dt in (torch.float16, torch.float32):
         enc = HashGridEncoding(3, MESHRIR_MODEL["pos_encoding_sigma"], dtype=dt).to(dev)
         with torch.no_grad():
             enc.params.uniform_(-1, 1)
