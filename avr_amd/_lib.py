@@ -131,6 +131,8 @@ _SIGS = {
     "avr_das_fwd": (ctypes.c_int, [_c_i32] + [_vp] * 5 + [_c_f32] * 3 + [_vp, _vp, _c_i64, _vp]),
     "avr_das_bwd": (ctypes.c_int, [_c_i32] + [_vp] * 3 + [_c_f32] * 3 + [_vp, _vp, _c_i64, _vp, _vp]),
     "avr_scale_sanitize": (ctypes.c_int, [_c_i32, _vp, _vp, _vp, _vp]),
+    "avr_concat_fwd": (ctypes.c_int, [_c_i64, _c_i32, _vp, _vp, _c_i32, _vp]),
+    "avr_concat_bwd": (ctypes.c_int, [_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp]),
     "avr_sigma_pack_bytes": (ctypes.c_int, [_c_i32, _vp]),
     "avr_sigma_desc_size": (ctypes.c_int, []),
     "avr_sigma_fwd": (ctypes.c_int, [_vp] * 3 + [_c_i32, _vp, _vp]),

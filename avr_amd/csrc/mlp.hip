@@ -159,25 +159,32 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(int64_t N, int M, int
         }
 }
 
-// dW = sum over splits of the partials.  One wavefront per 4 consecutive
-// outputs: its lanes stride over the splits (16-byte loads), then a fixed
-// shuffle tree combines them (deterministic, and no long serial chains when
-// a small layer is split many ways).
-__global__ __launch_bounds__(256) void wgrad_finalize_kernel(int64_t MK, int splits,
+// dW = sum over splits of the partials.  A workgroup covers Q = 256/G
+// consecutive 16-byte output quads; its G thread groups each sum the splits
+// g, g+G, g+2G, ... of every quad in order (consecutive threads read
+// consecutive quads of one split: coalesced), then the G partial sums are
+// added in group order through LDS.  G grows (up to 64) while the grid is too
+// small to fill the chip, so a small layer split many ways does not become a
+// long serial chain.  The order is fixed, so the result is deterministic.
+__global__ __launch_bounds__(256) void wgrad_finalize_kernel(int64_t MK, int splits, int G,
                                                               const float* __restrict__ partial,
                                                               float* __restrict__ out) {
-    const int lane = threadIdx.x & 63;
-    const int64_t i = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4;
-    if (i >= MK) return;  // wave-uniform; MK % 8 == 0
+    __shared__ f32x4 red[256];
+    const int Q = 256 / G;
+    const int q = threadIdx.x % Q, g = threadIdx.x / Q;
+    const int64_t i = ((int64_t)blockIdx.x * Q + q) * 4;
     f32x4 s = {0.0f, 0.0f, 0.0f, 0.0f};
-    for (int k = lane; k < splits; k += 64)
-        s += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(partial + (int64_t)k * MK + i));
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) s[c] += __shfl_xor(s[c], off, 64);
+    if (i < MK) {
+#pragma unroll 4
+        for (int k = g; k < splits; k += G)
+            s += __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(partial + (int64_t)k * MK + i));
     }
-    if (lane == 0) *reinterpret_cast<f32x4*>(out + i) = s;
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (g == 0 && i < MK) {
+        for (int h = 1; h < G; ++h) s += red[h * Q + q];
+        *reinterpret_cast<f32x4*>(out + i) = s;
+    }
 }
 
 int wgrad_splits(int64_t N, int M, int K) {
@@ -212,7 +219,10 @@ extern "C" int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* gra
                        (const __hip_bfloat16*)grad_y, (const __hip_bfloat16*)x, workspace);
     if (int e = check_launch("avr_linear_wgrad")) return e;
     const int64_t MK = (int64_t)M * K;
-    hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)((MK / 4 + 3) / 4)), dim3(256), 0, st,
-                       MK, used, workspace, grad_w);
+    int G = 1;
+    while (G < 64 && 2 * G <= used && (MK / 4) * G < 131072) G *= 2;
+    const int64_t quads_per_block = 256 / G;
+    hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)((MK / 4 + quads_per_block - 1) / quads_per_block)),
+                       dim3(256), 0, st, MK, used, G, workspace, grad_w);
     return check_launch("avr_linear_wgrad_finalize");
 }

@@ -489,11 +489,11 @@ extern "C" int avr_sigma_fwd(const avr_sigma_desc* d, const void* wpack, void* b
     const int cfg = d->tile_cfg;
     // tile configs (tools/probe_sigma.py, MI355X at config 2): MeshRIR
     // 0 = 64 samples per wave, 4 waves, 2 waves/SIMD (72 us); 1 = 32 per
-    // wave, 8 waves (80 us); 2 = 32 per wave, 4 waves; 3 = 64 per wave, 4
+    // wave, 8 waves (80 us); 2 = 32 per wave, 4 waves at 2 waves/SIMD; 3 = 64 per wave, 4
     // waves, 1 wave/SIMD.  RAF: 0 = 4 waves (120 us), 1 = 8 waves (137 us).
     if (two) return cfg == 1 ? launch_raf<8, 1>(a, st) : launch_raf<4, 2>(a, st);
     if (cfg == 1) return launch_meshrir<1, 8, 1>(a, st);
-    if (cfg == 2) return launch_meshrir<1, 4, 4>(a, st);
+    if (cfg == 2) return launch_meshrir<1, 4, 2>(a, st);
     if (cfg == 3) return launch_meshrir<2, 4, 1>(a, st);
     if (cfg == 16) return launch_meshrir<1, 8, 1, 1>(a, st);
     if (cfg == 17) return launch_meshrir<1, 8, 1, 2>(a, st);

@@ -16,6 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import sigma as _sigma
+from .concat import grouped_concat
 from .encoding import HashGridEncoding
 from .wcache import cast_weight
 
@@ -222,6 +223,11 @@ def _fused_sigma_ok(model, pts, layout, variant):
             and _sigma.variant_of(model) == variant)
 
 
+def _concat_ok(pts, layout):
+    """Grouped concatenation on the HIP path (renderer layout, GPU tensors)."""
+    return layout is not None and pts.is_cuda and os.environ.get("AVR_GROUPED_CONCAT", "1") != "0"
+
+
 def _per_ray(x, layout):
     B, R, S = layout
     return x.view(B, R, S, 3)[:, :, 0].reshape(B * R, 3)
@@ -278,6 +284,13 @@ class AVRModel(nn.Module):
         pos_enc = self._pos_encoding((pts.reshape(-1, 3) + 1) / 2)
         sigma_feat = self._model_encoder_sigma(pos_enc)
         attn = self._model_decoder_sigma(F.relu(sigma_feat))
+        if _concat_ok(pts, L):
+            B, R, S = L
+            dir_e = self._dir_encoding(_per_ray((view.reshape(-1, 3) + 1) / 2, L))
+            tx_e = self._tx_encoding(_per_pose((tx.reshape(-1, 3) + 1) / 2, L))
+            base = grouped_concat([(sigma_feat, 1), (dir_e, S), (tx_e, R * S)], bs * n, sigma_feat.dtype,
+                                  splits=[1, 1, R])
+            return torch.abs(F.leaky_relu(attn)).view(bs, n, 1), base
         dir_enc = _grouped(self._dir_encoding, (view.reshape(-1, 3) + 1) / 2, L, "ray")
         tx_enc = _grouped(self._tx_encoding, (tx.reshape(-1, 3) + 1) / 2, L, "pose")
         dt = sigma_feat.dtype
@@ -364,6 +377,8 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
         view = (view.reshape(-1, 3) + 1) / 2
         tx = (tx.reshape(-1, 3) + 1) / 2
         tx_view = (tx_view.reshape(-1, 3) + 1) / 2
+        if _concat_ok(pts, L):
+            return self._trunk_grouped(pts, view, tx, tx_view, L)
         pos_e = _grouped(self._pos_encoding, pts, L, "sample")
         txp_e = _grouped(self._tx_pos_encoding, tx, L, "pose")
         # the sigma feature is only used rectified (model.py:316, 323)
@@ -377,6 +392,26 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
                  _grouped(self._tx_pos_signal_encoding, tx, L, "pose").to(dt)]
         attn = torch.abs(F.leaky_relu(attn, negative_slope=self.leaky_relu)).view(bs, n, 1)
         return attn, _cat_features(parts, L)
+
+    def _trunk_grouped(self, pts, view, tx, tx_view, L):
+        """Training path with the renderer's layout: per-ray / per-pose
+        encodings evaluated once per group and concatenated by
+        `avr_concat_fwd` (backward: fixed-order group sums)."""
+        B, R, S = L
+        N = B * R * S
+        t = _per_pose(tx, L)
+        txp_e = self._tx_pos_encoding(t)
+        enc_in = grouped_concat([(self._pos_encoding(pts), 1), (txp_e, R * S)], N,
+                                self._model_encoder_sigma.dtype, splits=[1, R])
+        rf = self._model_encoder_sigma(enc_in, out_relu=True)
+        attn = self._model_decoder_sigma(rf)
+        base = grouped_concat(
+            [(rf, 1), (self._dir_encoding(_per_ray(view, L)), S),
+             (self._tx_dir_encoding(_per_pose(tx_view, L)), R * S),
+             (self._pos_signal_encoding(pts), 1), (self._tx_pos_signal_encoding(t), R * S)],
+            N, rf.dtype, splits=[1, 1, R, 1, R])
+        attn = torch.abs(F.leaky_relu(attn, negative_slope=self.leaky_relu)).view(B, R * S, 1)
+        return attn, base
 
     def _trunk_fused(self, pts, view, tx, tx_view, L):
         """Six encodings at their own granularity + one `avr_sigma_fwd`

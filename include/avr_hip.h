@@ -277,6 +277,32 @@ int avr_sigma_desc_size(void); /* sizeof(avr_sigma_desc), for binding checks */
 int avr_sigma_fwd(const avr_sigma_desc* d, const void* wpack, void* base, int32_t ldb, void* attn,
                   void* stream);
 
+/* ---- a6: grouped feature concatenation (training path) ------------------
+ * out[n][col_i + c] = src_i[n / rows_div_i][c] (cast to out_dtype), the
+ * sources side by side in order (col_0 = 0); the inputs of the sigma
+ * encoder and of the signal network (model.py:199-221, 314-325) with the
+ * per-ray / per-pose encodings read per group instead of expanded.
+ * Backward: grad_i[r][c] = sum over the rows_div rows of group r of
+ * grad_out[n][col_i + c], fp32 sums in a fixed order, stored in src dtype
+ * (skipped where grad is NULL); with split > 1 the group is summed in two
+ * passes (rows_div/split rows, then split partials) through `workspace`
+ * (fp32, N / (rows_div/split) * width floats).  Widths multiples of 8,
+ * total <= 512, pointers 16-byte aligned. */
+#define AVR_CONCAT_MAX_SRC 8
+typedef struct {
+    const void* data;
+    void* grad;
+    int32_t dtype;  /* AVR_DTYPE_F32 / F16 / BF16 */
+    int32_t rows_div;
+    int32_t width;
+    int32_t split;
+} avr_concat_src;
+
+int avr_concat_fwd(int64_t N, int32_t n_src, const avr_concat_src* src, void* out, int32_t out_dtype,
+                   void* stream);
+int avr_concat_bwd(int64_t N, int32_t n_src, const avr_concat_src* src, const void* grad_out,
+                   int32_t grad_dtype, float* workspace, void* stream);
+
 /* ---- §8f rank 1: fused signal head -------------------------------------
  * The signal network's last bias-free linear layer (model.py:176-180,
  * output_activation None) folded into the ray reduction:
