@@ -70,6 +70,8 @@ struct Args {
     int ldb;
     __hip_bfloat16* attn;
     float slope;
+    const float* bias;  // variant 2: per-group bias of the signal network's first layer [rows][512]
+    int bias_div;
 };
 
 // two fp32 -> a dword of two bf16 (v_cvt_pk_bf16_f32, round to nearest even)
@@ -80,6 +82,8 @@ __device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
 
 // ReLU of two packed bf16 (v_pk_max_i16 with 0: a set sign bit is a negative
 // int16).  One VALU op per two values; a NaN with the sign bit set becomes 0.
+__device__ __forceinline__ float relu(float v) { return v < 0.0f ? 0.0f : v; }  // NaN passes
+
 __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t u) {
     const s16x2 r = __builtin_elementwise_max(__builtin_bit_cast(s16x2, u), (s16x2){0, 0});
     return __builtin_bit_cast(uint32_t, r);
@@ -188,17 +192,27 @@ __device__ __forceinline__ void dense(ST& st, int lane,
     for (int c = 0; c < OT / CO; ++c) {
         const char* lds = st.buffer();
         // k-step outer: the CO*NT accumulators of a k-step are independent,
-        // so no MFMA waits on the previous one's result
+        // so no MFMA waits on the previous one's result; the next k-step's
+        // CO weight fragments are read while this one's MFMAs run
+        bf16x8 a[2][CO];
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
+        for (int o = 0; o < CO; ++o)
+            a[0][o] = *reinterpret_cast<const bf16x8*>(lds + (o * KS) * kFrag + lane * 16);
 #pragma unroll
-            for (int o = 0; o < CO; ++o) {
-                const bf16x8 a = *reinterpret_cast<const bf16x8*>(lds + (o * KS + ks) * kFrag + lane * 16);
+        for (int ks = 0; ks < KS; ++ks) {
+            if (ks + 1 < KS) {
+#pragma unroll
+                for (int o = 0; o < CO; ++o)
+                    a[(ks + 1) & 1][o] =
+                        *reinterpret_cast<const bf16x8*>(lds + (o * KS + ks + 1) * kFrag + lane * 16);
+            }
+#pragma unroll
+            for (int o = 0; o < CO; ++o)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt)
-                    acc[nt][c * CO + o] =
-                        __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, x[nt][ks], acc[nt][c * CO + o], 0, 0, 0);
-            }
+                    acc[nt][c * CO + o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks & 1][o], x[nt][ks],
+                                                                                  acc[nt][c * CO + o], 0, 0, 0);
+        }
         st.finish_chunk();
     }
 }
@@ -376,6 +390,90 @@ void sigma_meshrir_kernel(Args a) {
     if constexpr (!(DBG & 4)) copy_extras<NT>(a, n0, lane);
 }
 
+// signal layer 1 epilogue (variant 2): h1[n][128c + o] = bf16(relu(acc + bias[n / bias_div][128c + o]))
+template <int NT>
+__device__ __forceinline__ void store_h1(const Args& a, const f32x16 (&acc)[NT][4], int64_t n0, int lane, int c) {
+    const int h = lane >> 5;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+        const int64_t n = n0 + 32 * nt + (lane & 31);
+        const int64_t nl = n < a.N ? n : a.N - 1;
+        const float* brow = a.bias + (int64_t)((uint32_t)nl / (uint32_t)a.bias_div) * 512 + 128 * c;
+        __hip_bfloat16* row = a.base + n * a.ldb + 128 * c;
+#pragma unroll
+        for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 b = *reinterpret_cast<const f32x4*>(brow + 32 * ot + 8 * g + 4 * h);
+                const f32x16& v = acc[nt][ot];
+                const uint32_t w0 = pack_bf16(relu(v[4 * g] + b[0]), relu(v[4 * g + 1] + b[1]));
+                const uint32_t w1 = pack_bf16(relu(v[4 * g + 2] + b[2]), relu(v[4 * g + 3] + b[3]));
+                if (n < a.N) *reinterpret_cast<u32x2v*>(row + 32 * ot + 8 * g + 4 * h) = u32x2v{w0, w1};
+            }
+    }
+}
+
+// Variant 2 (AVRModel, sigma networks + the signal network's first layer):
+// as variant 0, then h1 = relu(W1[:, :128] sigma_feat + bias[ray]) with the
+// per-ray / per-pose columns of the layer (dir_enc, tx_enc) folded into
+// `bias` on the host, written as [N][512] bf16 in place of the
+// concatenated input.  12 chunks.
+template <int NT, int WAVES, int OCC>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
+void sigma_meshrir_h1_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * kChunk];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t n0 = ((int64_t)blockIdx.x * WAVES + wave) * 32 * NT;
+    Stager<WAVES> st;
+    st.start(a.wpack, lds, 12);
+
+    bf16x8 x0[NT][3];
+    load_input<NT, 3>(a, n0, lane, x0);
+    bf16x8 x[NT][8];
+    {
+        f32x16 acc[NT][4];
+        dense<NT, 3, 4, 4>(st, lane, x0, acc);
+        to_frags<NT, 4>(acc, x);
+    }
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+        f32x16 acc[NT][4];
+        dense<NT, 8, 4, 4>(st, lane, x, acc);
+        to_frags<NT, 4>(acc, x);
+    }
+    bf16x8 xs[NT][8];  // bf16(sigma_feat): the signal network's per-sample input
+    {
+        f32x16 acc[NT][4];
+        dense<NT, 8, 4, 4>(st, lane, x, acc);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int ot = 0; ot < 4; ++ot) {
+                uint32_t d[8];
+                pack_tile(acc[nt][ot], d);
+                tile_frags(d, false, xs[nt][2 * ot], xs[nt][2 * ot + 1]);
+                tile_frags(d, true, x[nt][2 * ot], x[nt][2 * ot + 1]);
+            }
+    }
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+        f32x16 acc[NT][4];
+        dense<NT, 8, 4, 4>(st, lane, x, acc);
+        to_frags<NT, 4>(acc, x);
+    }
+    {
+        f32x16 acc[NT][1];
+        dense<NT, 8, 1, 1>(st, lane, x, acc);
+        store_attn<NT>(a, acc, n0, lane);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        f32x16 acc[NT][4];
+        dense<NT, 8, 4, 4>(st, lane, xs, acc);
+        store_h1<NT>(a, acc, n0, lane, c);
+    }
+}
+
 // Variant 1 (AVRModel_complex): [40 | 40] -> 128 -> 128 -> 128 -> 256 (relu,
 // = rf) -> 128 -> 1.  8 chunks (the 256-wide layers take two each).
 template <int NT, int WAVES, int OCC>
@@ -435,6 +533,14 @@ int launch_meshrir(const Args& a, hipStream_t st) {
     return check_launch("avr_sigma_fwd");
 }
 
+template <int NT, int WAVES, int OCC>
+int launch_meshrir_h1(const Args& a, hipStream_t st) {
+    const int64_t per_block = 32 * NT * WAVES;
+    const dim3 grid((unsigned)((a.N + per_block - 1) / per_block));
+    hipLaunchKernelGGL((sigma_meshrir_h1_kernel<NT, WAVES, OCC>), grid, dim3(64 * WAVES), 0, st, a);
+    return check_launch("avr_sigma_fwd");
+}
+
 template <int WAVES, int OCC>
 int launch_raf(const Args& a, hipStream_t st) {
     const int64_t per_block = 32 * WAVES;
@@ -446,22 +552,29 @@ int launch_raf(const Args& a, hipStream_t st) {
 }  // namespace
 
 extern "C" int avr_sigma_pack_bytes(int32_t variant, int64_t* bytes) {
-    AVR_REQUIRE(bytes && (variant == AVR_SIGMA_MESHRIR || variant == AVR_SIGMA_RAF),
+    AVR_REQUIRE(bytes && (variant == AVR_SIGMA_MESHRIR || variant == AVR_SIGMA_RAF ||
+                          variant == AVR_SIGMA_MESHRIR_H1),
                 "avr_sigma_pack_bytes: bad variant");
-    *bytes = 8 * (int64_t)kChunk;
+    *bytes = (variant == AVR_SIGMA_MESHRIR_H1 ? 12 : 8) * (int64_t)kChunk;
     return 0;
 }
 
 extern "C" int avr_sigma_fwd(const avr_sigma_desc* d, const void* wpack, void* base, int32_t ldb,
                              void* attn, void* stream) {
     AVR_REQUIRE(d && wpack && base && attn, "avr_sigma_fwd: null argument");
-    AVR_REQUIRE(d->variant == AVR_SIGMA_MESHRIR || d->variant == AVR_SIGMA_RAF, "avr_sigma_fwd: bad variant");
+    AVR_REQUIRE(d->variant == AVR_SIGMA_MESHRIR || d->variant == AVR_SIGMA_RAF ||
+                    d->variant == AVR_SIGMA_MESHRIR_H1,
+                "avr_sigma_fwd: bad variant");
+    const bool h1 = d->variant == AVR_SIGMA_MESHRIR_H1;
+    AVR_REQUIRE(!h1 || (d->bias && d->bias_div >= 1 && ldb == 512 && d->n_extra == 0 &&
+                        reinterpret_cast<uintptr_t>(d->bias) % 16 == 0),
+                "avr_sigma_fwd: variant MESHRIR_H1 needs bias, bias_div >= 1, ldb 512, no extras");
     AVR_REQUIRE(d->n_samples >= 1 && d->n_samples < (int64_t(1) << 31),
                 "avr_sigma_fwd: n_samples must be in [1, 2^31)");
     const bool two = d->variant == AVR_SIGMA_RAF;
     AVR_REQUIRE(src_ok(d->input[0]) && (!two || src_ok(d->input[1])), "avr_sigma_fwd: bad input source");
     AVR_REQUIRE(d->n_extra >= 0 && d->n_extra <= AVR_SIGMA_MAX_EXTRA, "avr_sigma_fwd: bad n_extra");
-    const int out_w = two ? 256 : 128;
+    const int out_w = two ? 256 : (d->variant == AVR_SIGMA_MESHRIR_H1 ? 512 : 128);
     AVR_REQUIRE(ldb % 8 == 0 && reinterpret_cast<uintptr_t>(base) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(wpack) % 16 == 0,
                 "avr_sigma_fwd: base/wpack must be 16-byte aligned, ldb a multiple of 8");
@@ -485,7 +598,13 @@ extern "C" int avr_sigma_fwd(const avr_sigma_desc* d, const void* wpack, void* b
     a.ldb = ldb;
     a.attn = static_cast<__hip_bfloat16*>(attn);
     a.slope = d->leaky_slope;
+    a.bias = d->bias;
+    a.bias_div = d->bias_div;
     hipStream_t st = as_stream(stream);
+    if (h1) {
+        if (d->tile_cfg == 1) return launch_meshrir_h1<1, 8, 1>(a, st);
+        return launch_meshrir_h1<1, 4, 2>(a, st);
+    }
     const int cfg = d->tile_cfg;
     // tile configs (tools/probe_sigma.py, MI355X at config 2): MeshRIR
     // 0 = 64 samples per wave, 4 waves, 2 waves/SIMD (72 us); 1 = 32 per

@@ -159,6 +159,14 @@ class MLP(nn.Module):
             x = _LinearReLU.apply(x, lin.weight, self.dtype, not torch.is_grad_enabled())
         return x
 
+    def hidden_from(self, x, start):
+        """Hidden layers start .. n-2 (each followed by ReLU) on x, the
+        rectified output of layer start-1."""
+        x = x.to(self.dtype).contiguous()
+        for lin in self.layers[start:-1]:
+            x = _LinearReLU.apply(x, lin.weight, self.dtype, not torch.is_grad_enabled())
+        return x
+
     def last(self, h):
         """The bias-free output layer (output_activation None)."""
         return _Linear.apply(h.contiguous(), self.layers[-1].weight, self.dtype, not torch.is_grad_enabled())
@@ -312,15 +320,45 @@ class AVRModel(nn.Module):
                                       [(dir_e, S), (tx_e, R * S)], 128, 0.01)
         return attn.view(bs, n, 1), base
 
-    def forward(self, pts, view, tx, ch_idx=None, ray_layout=None):
+    def _trunk_fused_h1(self, pts, view, tx, L):
+        """Inference: encodings + one `avr_sigma_fwd` (MESHRIR_H1) launch that
+        also applies the signal network's first layer to sigma_feat; the
+        layer's dir / tx columns act per ray, as a bias computed here once per
+        ray (model.py:221 concatenates them to every sample).  Returns attn
+        and h1 = relu(layer 1) [N, 512] bf16."""
+        B, R, S = L
+        bs, n = pts.size(0), pts.size(1)
+        pos_enc = self._pos_encoding.forward_level_major((pts.reshape(-1, 3) + 1) / 2)
+        dir_e = self._dir_encoding(_per_ray((view.reshape(-1, 3) + 1) / 2, L))
+        tx_e = self._tx_encoding(_per_pose((tx.reshape(-1, 3) + 1) / 2, L))
+        w1 = self._model_signal.layers[0].weight
+        wb = cast_weight(w1, torch.bfloat16, True).float()
+        bias = dir_e.to(torch.bfloat16).float() @ wb[:, 128:168].t()
+        bias = (bias.view(B, R, -1) + (tx_e.to(torch.bfloat16).float() @ wb[:, 168:208].t()).view(B, 1, -1))
+        bias = bias.reshape(B * R, -1).contiguous()
+        params = _sigma_params(self) + [w1[:, :128]]
+        packed = self._sigma_pack.get(_sigma.MESHRIR_H1, params)
+        attn, h1 = _sigma.sigma_fwd(_sigma.MESHRIR_H1, packed, bs * n, [(pos_enc, 1)], [], 512, 0.01,
+                                    bias=bias, bias_div=S)
+        return attn.view(bs, n, 1), h1
+
+    def _signal_hidden(self, pts, view, tx, ch_idx, ray_layout):
+        """(attn, h): h the signal network's last hidden activation."""
+        if (ch_idx is None and _fused_sigma_ok(self, pts, ray_layout, _sigma.MESHRIR)
+                and os.environ.get("AVR_FUSED_H1", "1") != "0" and _sigma.h1_ok(self)):
+            attn, h1 = self._trunk_fused_h1(pts, view, tx, ray_layout)
+            return attn, self._model_signal.hidden_from(h1, 1)
         attn, base = self._trunk(pts, view, tx, ch_idx, ray_layout)
-        signal = self._model_signal(base)
+        return attn, self._model_signal.hidden(base)
+
+    def forward(self, pts, view, tx, ch_idx=None, ray_layout=None):
+        attn, h = self._signal_hidden(pts, view, tx, ch_idx, ray_layout)
+        signal = self._model_signal.last(h)
         return attn, signal.view(pts.size(0), pts.size(1), self.signal_output_dim)
 
     def forward_fused(self, pts, view, tx, ch_idx=None, ray_layout=None):
         """(attn, h, W, dtype) with signal = h @ W^T left to the renderer."""
-        attn, base = self._trunk(pts, view, tx, ch_idx, ray_layout)
-        h = self._model_signal.hidden(base)
+        attn, h = self._signal_hidden(pts, view, tx, ch_idx, ray_layout)
         return (attn, h.view(pts.size(0), pts.size(1), -1), self._model_signal.layers[-1].weight,
                 self._model_signal.dtype)
 

@@ -27,6 +27,7 @@ from . import _lib
 
 MESHRIR = 0  # AVR_SIGMA_MESHRIR
 RAF = 1      # AVR_SIGMA_RAF
+MESHRIR_H1 = 2  # AVR_SIGMA_MESHRIR_H1: MESHRIR + the signal network's first layer
 MAX_EXTRA = 4
 CHUNK = 32768
 
@@ -36,6 +37,7 @@ SCHEDULE = {
     RAF: [(128, 80, True, 4), (128, 128, False, 4), (128, 128, False, 4), (256, 128, False, 4),
           (128, 256, False, 2), (1, 128, False, 1)],
 }
+SCHEDULE[MESHRIR_H1] = SCHEDULE[MESHRIR] + [(512, 128, False, 4)]
 
 
 class FeatSrc(ctypes.Structure):
@@ -51,7 +53,8 @@ class SigmaDesc(ctypes.Structure):
     _fields_ = [("variant", ctypes.c_int32), ("tile_cfg", ctypes.c_int32),
                 ("n_samples", ctypes.c_int64), ("leaky_slope", ctypes.c_float),
                 ("input", FeatSrc * 2), ("n_extra", ctypes.c_int32),
-                ("extra", FeatSrc * MAX_EXTRA), ("extra_width", ctypes.c_int32 * MAX_EXTRA)]
+                ("extra", FeatSrc * MAX_EXTRA), ("extra_width", ctypes.c_int32 * MAX_EXTRA),
+                ("bias", ctypes.c_void_p), ("bias_div", ctypes.c_int32)]
 
 
 def fragment_index(M, K, first):
@@ -114,10 +117,19 @@ def variant_of(model):
     if enc.dtype != torch.bfloat16 or dec.dtype != torch.bfloat16:
         return None
     dims = _dims(enc) + _dims(dec)
-    for v, sched in SCHEDULE.items():
-        if dims == [(M, K) for M, K, _, _ in sched]:
+    for v in (MESHRIR, RAF):
+        if dims == [(M, K) for M, K, _, _ in SCHEDULE[v]]:
             return v
     return None
+
+
+def h1_ok(model):
+    """MESHRIR_H1 applies: an AVRModel whose signal network starts with a
+    bias-free 208 -> 512 layer on [sigma_feat 128 | dir 40 | tx 40] in bf16
+    and has at least one more hidden layer."""
+    sig = model._model_signal
+    return (variant_of(model) == MESHRIR and sig.dtype == torch.bfloat16 and len(sig.layers) >= 3
+            and tuple(sig.layers[0].weight.shape) == (512, 208))
 
 
 class SigmaWeights:
@@ -162,7 +174,8 @@ def _rows(t, idx):
     return t[idx]
 
 
-def sigma_fwd(variant, packed, n_samples, inputs, extras, out_width, slope, tile_cfg=0):
+def sigma_fwd(variant, packed, n_samples, inputs, extras, out_width, slope, tile_cfg=0, bias=None,
+              bias_div=1):
     """One launch: inputs = [(tensor [rows, 40] or level-major [20, rows, 2],
     rows_div)] (1 for MESHRIR, 2 for RAF); extras = [(tensor, rows_div)]
     appended after the MLP output.  Returns (attn [N] bf16, base [N, out_width + sum widths] bf16)."""
@@ -186,6 +199,11 @@ def sigma_fwd(variant, packed, n_samples, inputs, extras, out_width, slope, tile
     for i, (t, div) in enumerate(extras):
         d.extra[i] = _src(t, div)
         d.extra_width[i] = widths[i]
+    if bias is not None:
+        if bias.dtype != torch.float32 or not bias.is_contiguous() or bias.size(-1) != 512:
+            raise ValueError("bias must be a contiguous fp32 [groups, 512] tensor")
+        d.bias = bias.data_ptr()
+        d.bias_div = int(bias_div)
     keep = [t for t, _ in list(inputs) + list(extras)]  # noqa: F841  (alive across the call)
     st = torch.cuda.current_stream(dev).cuda_stream
     _lib.call("avr_sigma_fwd", ctypes.byref(d), ctypes.c_void_p(packed.data_ptr()),
@@ -194,7 +212,7 @@ def sigma_fwd(variant, packed, n_samples, inputs, extras, out_width, slope, tile
     return attn, base
 
 
-def reference_fwd(variant, weights, inputs, extras, n_samples, slope):
+def reference_fwd(variant, weights, inputs, extras, n_samples, slope, bias=None, bias_div=1):
     """Plain PyTorch statement of the same computation with the unfused bf16
     path's roundings (fp32 GEMMs on bf16-rounded operands, bf16 outputs); the
     test oracle for `sigma_fwd`.  Runs on any device."""
@@ -208,6 +226,9 @@ def reference_fwd(variant, weights, inputs, extras, n_samples, slope):
 
     idx = torch.arange(n_samples, device=weights[0].device)
     x = torch.cat([_rows(t, idx // div).to(bf) for t, div in inputs], -1)
+    w_h1 = None
+    if variant == MESHRIR_H1:
+        weights, w_h1 = weights[:-1], weights[-1]
     nw = len(weights)
     n_enc = 4
     for i in range(n_enc - 1):
@@ -218,5 +239,8 @@ def reference_fwd(variant, weights, inputs, extras, n_samples, slope):
         x = lin(x, weights[i], True)
     a = lin(x, weights[nw - 1], False).float()
     attn = torch.abs(torch.where(a > 0, a, a * float(np.float32(slope))).to(bf))
+    if w_h1 is not None:
+        h1 = torch.relu(feat.float() @ w_h1.to(bf).float().t() + bias[idx // bias_div])
+        return attn.view(-1), h1.to(bf)
     base = torch.cat([feat] + [_rows(t, idx // div).to(bf) for t, div in extras], -1)
     return attn.view(-1), base

@@ -252,6 +252,12 @@ int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* grad_y, const 
  * avr_amd/sigma.py (pack_sigma_weights).  base, attn are bf16. */
 #define AVR_SIGMA_MESHRIR 0
 #define AVR_SIGMA_RAF 1
+/* AVR_SIGMA_MESHRIR_H1: AVR_SIGMA_MESHRIR followed by the signal network's
+ * first layer on the per-sample features (model.py:176-180, 221):
+ *   base[n][0:512] = relu(W1[:, :128] sigma_feat[n] + bias[n / bias_div])
+ * with bias[g] = W1[:, 128:] [dir_enc | tx_enc] of the group (per ray), so
+ * ldb = 512 and no extras; the signal network continues from layer 2. */
+#define AVR_SIGMA_MESHRIR_H1 2
 #define AVR_SIGMA_MAX_EXTRA 4
 typedef struct {
     const void* data; /* [rows][width] (row-major) or [width/2][rows][2] (level-major,
@@ -270,6 +276,8 @@ typedef struct {
     int32_t n_extra;
     avr_feat_src extra[AVR_SIGMA_MAX_EXTRA];
     int32_t extra_width[AVR_SIGMA_MAX_EXTRA];
+    const float* bias; /* AVR_SIGMA_MESHRIR_H1: [groups][512] fp32 */
+    int32_t bias_div;  /* sample n uses bias row n / bias_div */
 } avr_sigma_desc;
 
 int avr_sigma_pack_bytes(int32_t variant, int64_t* bytes);

@@ -147,3 +147,34 @@ def test_level_major_sources_match_row_major(variant):
                              out_w, 0.02)
     torch.cuda.synchronize()
     assert torch.equal(a0, a1) and torch.equal(b0, b1)
+
+
+@pytest.mark.parametrize("N,S", [(262144, 256), (1000, 10), (7, 7)])
+def test_sigma_h1_kernel_matches_reference(N, S):
+    """MESHRIR_H1: the sigma networks plus the signal network's first layer
+    (per-sample columns in the kernel, per-ray columns as a bias)."""
+    g = torch.Generator(device=DEV).manual_seed(8)
+    ws = _weights(sigma.MESHRIR_H1, 5)
+    inputs, _ = _sources(sigma.MESHRIR, N, S, N, 6)
+    bias = torch.randn(-(-N // S), 512, device=DEV, generator=g) * 0.3
+    packed = sigma.pack_layers(sigma.MESHRIR_H1, ws)
+    ra, rh = sigma.reference_fwd(sigma.MESHRIR_H1, ws, inputs, [], N, 0.01, bias=bias, bias_div=S)
+    for cfg in (0, 1):
+        attn, h1 = sigma.sigma_fwd(sigma.MESHRIR_H1, packed, N, inputs, [], 512, 0.01, tile_cfg=cfg,
+                                   bias=bias, bias_div=S)
+        torch.cuda.synchronize()
+        _close(h1, rh, f"h1 cfg {cfg}")
+        _close(attn, ra, f"attn cfg {cfg}")
+
+
+def test_network_fused_h1_matches_per_layer(monkeypatch):
+    m, args, L = _net_pair("AVRModel")
+    with torch.no_grad():
+        monkeypatch.setenv("AVR_FUSED_SIGMA", "0")
+        a0, h0, _, _ = m.forward_fused(*args, ray_layout=L)
+        monkeypatch.setenv("AVR_FUSED_SIGMA", "1")
+        monkeypatch.setenv("AVR_FUSED_H1", "1")
+        a1, h1, _, _ = m.forward_fused(*args, ray_layout=L)
+    torch.cuda.synchronize()
+    _close(a1, a0, "attn")
+    _close(h1, h0, "signal hidden")

@@ -35,7 +35,7 @@ def mfma(afrag, bfrag, c):
     return out
 
 
-def run_model(variant, packed, inputs, extras, slope):
+def run_model(variant, packed, inputs, extras, slope, bias=None, bias_div=1):
     """Software model of one wave (32 samples, NT = 1) of the kernel."""
     sched = sigma.SCHEDULE[variant]
     chunks = packed.view(-1, sigma.CHUNK // 2)
@@ -62,8 +62,13 @@ def run_model(variant, packed, inputs, extras, slope):
     base_cols = {}
     attn = None
     n_enc = 4
+    h1_layer = 8 if variant == sigma.MESHRIR_H1 else -1
+    xs = None
+    h1 = torch.zeros(32, 512)
     for li, (M, K, first, co) in enumerate(sched):
         OT, KS = -(-M // 32), -(-K // 16)
+        if li == h1_layer:
+            x = xs
         assert len(x) == KS
         acc = [torch.zeros(64, 16) for _ in range(OT)]
         for c in range(OT // co):
@@ -72,6 +77,19 @@ def run_model(variant, packed, inputs, extras, slope):
             for o in range(co):
                 for ks in range(KS):
                     acc[c * co + o] = mfma(fr[o, ks], x[ks], acc[c * co + o])
+        if li == h1_layer:  # relu(acc + bias) -> h1
+            for ot in range(OT):
+                for i in range(16):
+                    col = 32 * ot + (i & 3) + 8 * (i >> 2) + 4 * h
+                    for lane in range(64):
+                        r = int(n[lane])
+                        h1[r, int(col[lane])] = acc[ot][lane, i] + bias[r // bias_div, int(col[lane])]
+            continue
+        if li == n_enc - 1 and variant == sigma.MESHRIR_H1:
+            xs = []
+            for ot in range(OT):
+                for s_ in range(2):
+                    xs.append(acc[ot][:, 8 * s_:8 * s_ + 8].to(BF))
         if li == n_enc - 1:  # encoder output -> base columns
             for ot in range(OT):
                 v = acc[ot]
@@ -81,7 +99,7 @@ def run_model(variant, packed, inputs, extras, slope):
                     col = 32 * ot + (i & 3) + 8 * (i >> 2) + 4 * h
                     for lane in range(64):
                         base_cols[(int(n[lane]), int(col[lane]))] = v[lane, i].to(BF)
-        if li == len(sched) - 1:
+        if OT == 1:
             y = acc[0][:32, 0].to(BF).float()
             attn = torch.abs(torch.where(y > 0, y, y * float(np.float32(slope))).to(BF))
         else:
@@ -89,6 +107,9 @@ def run_model(variant, packed, inputs, extras, slope):
             for ot in range(OT):
                 for s in range(2):
                     x.append(torch.relu(acc[ot][:, 8 * s:8 * s + 8]).to(BF))
+    if variant == sigma.MESHRIR_H1:
+        assert ci == len(chunks)
+        return attn, torch.relu(h1).to(BF)
     out_w = 256 if variant == sigma.RAF else 128
     feat = torch.zeros(32, out_w, dtype=BF)
     for (i, c), v in base_cols.items():
@@ -164,3 +185,18 @@ def test_desc_struct_matches_library():
     b = ctypes.c_int64(0)
     _lib.call("avr_sigma_pack_bytes", sigma.MESHRIR, ctypes.byref(b))
     assert b.value == 8 * sigma.CHUNK
+
+
+def test_kernel_model_h1_matches_reference():
+    """MESHRIR_H1: sigma networks + the signal network's first layer on the
+    raw sigma_feat fragments (12 chunks), bias per group."""
+    g = torch.Generator().manual_seed(4)
+    ws = _weights(sigma.MESHRIR_H1, 2)
+    packed = sigma.pack_layers(sigma.MESHRIR_H1, ws)
+    assert packed.numel() * 2 == 12 * sigma.CHUNK
+    inputs = [(torch.rand(32, 40, generator=g).half(), 1)]
+    bias = torch.randn(4, 512, generator=g) * 0.1
+    attn, h1 = run_model(sigma.MESHRIR_H1, packed, inputs, [], 0.01, bias=bias, bias_div=8)
+    ra, rh = sigma.reference_fwd(sigma.MESHRIR_H1, ws, inputs, [], 32, 0.01, bias=bias, bias_div=8)
+    torch.testing.assert_close(h1.float(), rh.float(), rtol=2 ** -7, atol=2e-3)
+    torch.testing.assert_close(attn.float(), ra.float(), rtol=2 ** -7, atol=1e-3)

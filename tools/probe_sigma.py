@@ -30,7 +30,13 @@ def main():
     packed = sigma.pack_layers(v, ws)
     N, S, RS = a.n, 256, 262144
     B = -(-N // RS)
-    if v == sigma.MESHRIR:
+    bias = None
+    if v == sigma.MESHRIR_H1:
+        inputs = [(torch.rand(N, 40, device=dev).half(), 1)]
+        extras = []
+        out_w = 512
+        bias = torch.randn(-(-N // S), 512, device=dev) * 0.1
+    elif v == sigma.MESHRIR:
         inputs = [(torch.rand(N, 40, device=dev).half(), 1)]
         extras = [(torch.rand(B * RS // S, 40, device=dev).half(), S), (torch.rand(B, 40, device=dev).half(), RS)]
         out_w = 128
@@ -42,11 +48,11 @@ def main():
     flops = 2 * N * sum(M * K for M, K, _, _ in sigma.SCHEDULE[v])
     for cfg in [int(c) for c in a.cfgs.split(",")]:
         for _ in range(3):
-            sigma.sigma_fwd(v, packed, N, inputs, extras, out_w, 0.01, tile_cfg=cfg)
+            sigma.sigma_fwd(v, packed, N, inputs, extras, out_w, 0.01, tile_cfg=cfg, bias=bias, bias_div=S)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.iters):
-            sigma.sigma_fwd(v, packed, N, inputs, extras, out_w, 0.01, tile_cfg=cfg)
+            sigma.sigma_fwd(v, packed, N, inputs, extras, out_w, 0.01, tile_cfg=cfg, bias=bias, bias_div=S)
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.iters
