@@ -21,6 +21,8 @@
 // second kernel (deterministic).
 #include "common.h"
 
+#include <stdlib.h>
+
 using namespace avr;
 
 namespace {
@@ -45,14 +47,31 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds_base, int byte_off) {
         (__attribute__((address_space(3))) s16x4*)(lds_base + byte_off));
 }
 
+// Block -> (split, tile): with xcd_map, block id b runs on XCD b % 8 and
+// all tiles of a split go to the same XCD (split = b % 8 + 8 * (b / 8 / tiles)),
+// so the split's row range of gy and x is read from HBM/MALL once into that
+// XCD's L2 and re-read from there by its other tiles; otherwise tiles are
+// fastest (each split's tiles spread over all XCDs).
 __global__ __launch_bounds__(256) void linear_wgrad_kernel(int64_t N, int M, int K, int64_t rows_per_split,
+                                                            int used, int xcd_map,
                                                             const __hip_bfloat16* __restrict__ gy,
                                                             const __hip_bfloat16* __restrict__ x,
                                                             float* __restrict__ partial) {
     __shared__ __attribute__((aligned(16))) char lds[2 * kImg];  // [A image][B image]
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int m0 = blockIdx.y * kTile, k0 = blockIdx.x * kTile;
-    const int split = blockIdx.z;
+    const int tiles_k = (K + kTile - 1) / kTile;
+    const int tiles = tiles_k * ((M + kTile - 1) / kTile);
+    const int b = blockIdx.x;
+    int tile, split;
+    if (xcd_map) {
+        tile = (b >> 3) % tiles;
+        split = (b & 7) + 8 * ((b >> 3) / tiles);
+    } else {
+        tile = b % tiles;
+        split = b / tiles;
+    }
+    if (split >= used) return;  // padding blocks of the XCD map (block-uniform)
+    const int m0 = (tile / tiles_k) * kTile, k0 = (tile % tiles_k) * kTile;
     const int64_t n_begin = (int64_t)split * rows_per_split;
     const int64_t n_end = min(N, n_begin + rows_per_split);
 
@@ -187,9 +206,15 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(int64_t MK, int spl
     }
 }
 
+int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v && *v ? atoi(v) : dflt;
+}
+
 int wgrad_splits(int64_t N, int M, int K) {
     const int tiles = ((M + kTile - 1) / kTile) * ((K + kTile - 1) / kTile);
-    int splits = (512 + tiles - 1) / tiles;  // ~2 workgroups per CU
+    const int target = env_int("AVR_WGRAD_WGS", 512);  // ~2 workgroups per CU
+    int splits = (target + tiles - 1) / tiles;
     const int64_t max_by_rows = N / 256 > 1 ? N / 256 : 1;  // >= 8 slabs per split
     return (int)(splits < max_by_rows ? splits : max_by_rows);
 }
@@ -214,9 +239,11 @@ extern "C" int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* gra
     rows = (rows + kSlab - 1) / kSlab * kSlab;
     const int used = (int)((N + rows - 1) / rows);
     hipStream_t st = as_stream(stream);
-    const dim3 grid((K + kTile - 1) / kTile, (M + kTile - 1) / kTile, used);
-    hipLaunchKernelGGL(linear_wgrad_kernel, grid, dim3(256), 0, st, N, (int)M, (int)K, rows,
-                       (const __hip_bfloat16*)grad_y, (const __hip_bfloat16*)x, workspace);
+    const int tiles = ((K + kTile - 1) / kTile) * ((M + kTile - 1) / kTile);
+    const int xcd_map = env_int("AVR_WGRAD_XCD", 1);
+    const int64_t blocks = xcd_map ? (int64_t)tiles * ((used + 7) / 8 * 8) : (int64_t)tiles * used;
+    hipLaunchKernelGGL(linear_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, N, (int)M, (int)K, rows,
+                       used, xcd_map, (const __hip_bfloat16*)grad_y, (const __hip_bfloat16*)x, workspace);
     if (int e = check_launch("avr_linear_wgrad")) return e;
     const int64_t MK = (int64_t)M * K;
     int G = 1;

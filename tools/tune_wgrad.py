@@ -21,15 +21,17 @@ from avr_amd.model import _wgrad_hip  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=83200)
-    ap.add_argument("--targets", default="512,1024,1536,2048,4096")
+    ap.add_argument("--targets", default="512,1024,2048")
+    ap.add_argument("--xcd", default="0,1")
     ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     shapes = ((512, 512), (1600, 512), (512, 336), (256, 128), (128, 128), (128, 80))
     data = [(torch.randn(args.n, m, device=dev).to(torch.bfloat16),
              torch.randn(args.n, k, device=dev).to(torch.bfloat16)) for m, k in shapes]
-    for tgt in args.targets.split(","):
+    for tgt, xcd in [(t, x) for t in args.targets.split(",") for x in args.xcd.split(",")]:
         os.environ["AVR_WGRAD_WGS"] = tgt
+        os.environ["AVR_WGRAD_XCD"] = xcd
         for (m, k), (gy, x) in zip(shapes, data):
             _wgrad_hip(gy, x)
             torch.cuda.synchronize()
@@ -40,7 +42,7 @@ def main():
             e1.record()
             e1.synchronize()
             us = e0.elapsed_time(e1) / args.iters * 1e3
-            print(json.dumps({"target": int(tgt), "N": args.n, "M": m, "K": k, "us": round(us, 1),
+            print(json.dumps({"target": int(tgt), "xcd": int(xcd), "N": args.n, "M": m, "K": k, "us": round(us, 1),
                               "TFLOPs": round(2 * args.n * m * k / us / 1e6, 1)}), flush=True)
 
 
