@@ -72,6 +72,7 @@ struct Args {
     float slope;
     const float* bias;  // variant 2: per-group bias of the signal network's first layer [rows][512]
     int bias_div;
+    int nt_store;       // variant 2: streaming (non-temporal) h1 stores
 };
 
 // two fp32 -> a dword of two bf16 (v_cvt_pk_bf16_f32, round to nearest even)
@@ -390,26 +391,53 @@ void sigma_meshrir_kernel(Args a) {
     if constexpr (!(DBG & 4)) copy_extras<NT>(a, n0, lane);
 }
 
-// signal layer 1 epilogue (variant 2): h1[n][128c + o] = bf16(relu(acc + bias[n / bias_div][128c + o]))
-template <int NT>
-__device__ __forceinline__ void store_h1(const Args& a, const f32x16 (&acc)[NT][4], int64_t n0, int lane, int c) {
-    const int h = lane >> 5;
+// signal layer 1 epilogue (variant 2): h1[n][128c + o] = bf16(relu(acc + bias[n / bias_div][128c + o])).
+// The MFMA result has the sample on the lane, so written straight out every
+// store instruction would touch 32 rows x 16 B; instead each pair of tiles
+// (32 samples x 64 columns, 4 KB) goes through a per-wave LDS area (16-byte
+// chunks XOR-swizzled by row: conflict-free) and leaves as 4 instructions
+// of 8 rows x 128 contiguous bytes (full cache lines).
+template <int NT, bool STORE = true>
+__device__ __forceinline__ void store_h1(const Args& a, const f32x16 (&acc)[NT][4], int64_t n0, int lane, int c,
+                                         char* tr) {
+    const int h = lane >> 5, r = lane & 31;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-        const int64_t n = n0 + 32 * nt + (lane & 31);
+        const int64_t n = n0 + 32 * nt + r;
         const int64_t nl = n < a.N ? n : a.N - 1;
         const float* brow = a.bias + (int64_t)((uint32_t)nl / (uint32_t)a.bias_div) * 512 + 128 * c;
-        __hip_bfloat16* row = a.base + n * a.ldb + 128 * c;
 #pragma unroll
-        for (int ot = 0; ot < 4; ++ot)
+        for (int p = 0; p < 2; ++p) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const f32x4 b = *reinterpret_cast<const f32x4*>(brow + 32 * ot + 8 * g + 4 * h);
-                const f32x16& v = acc[nt][ot];
-                const uint32_t w0 = pack_bf16(relu(v[4 * g] + b[0]), relu(v[4 * g + 1] + b[1]));
-                const uint32_t w1 = pack_bf16(relu(v[4 * g + 2] + b[2]), relu(v[4 * g + 3] + b[3]));
-                if (n < a.N) *reinterpret_cast<u32x2v*>(row + 32 * ot + 8 * g + 4 * h) = u32x2v{w0, w1};
+            for (int j = 0; j < 2; ++j) {
+                const int ot = 2 * p + j;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 b = *reinterpret_cast<const f32x4*>(brow + 32 * ot + 8 * g + 4 * h);
+                    const f32x16& v = acc[nt][ot];
+                    const uint32_t w0 = pack_bf16(relu(v[4 * g] + b[0]), relu(v[4 * g + 1] + b[1]));
+                    const uint32_t w1 = pack_bf16(relu(v[4 * g + 2] + b[2]), relu(v[4 * g + 3] + b[3]));
+                    const int ch = (4 * j + g) ^ (r & 7);  // 16-B chunk of the 128-B row
+                    *reinterpret_cast<u32x2v*>(tr + r * 128 + ch * 16 + 8 * h) = u32x2v{w0, w1};
+                }
             }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = 8 * q + (lane >> 3), chunk = lane & 7;
+                const u32x4v v = *reinterpret_cast<const u32x4v*>(tr + row * 128 + ((chunk ^ (row & 7)) * 16));
+                const int64_t nr = n0 + 32 * nt + row;
+                // (STORE = false: timing experiments; a.ldb < 0 never holds)
+                if (STORE ? nr < a.N : a.ldb < 0) {
+                    u32x4v* dst = reinterpret_cast<u32x4v*>(a.base + nr * a.ldb + 128 * c + 64 * p + 8 * chunk);
+                    if (a.nt_store)
+                        __builtin_nontemporal_store(v, dst);
+                    else
+                        *dst = v;
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
     }
 }
 
@@ -418,13 +446,13 @@ __device__ __forceinline__ void store_h1(const Args& a, const f32x16 (&acc)[NT][
 // per-ray / per-pose columns of the layer (dir_enc, tx_enc) folded into
 // `bias` on the host, written as [N][512] bf16 in place of the
 // concatenated input.  12 chunks.
-template <int NT, int WAVES, int OCC>
+template <int NT, int WAVES, int OCC, int DBG = 0>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
 void sigma_meshrir_h1_kernel(Args a) {
-    __shared__ __attribute__((aligned(16))) char lds[2 * kChunk];
+    __shared__ __attribute__((aligned(16))) char lds[2 * kChunk + WAVES * 4096];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t n0 = ((int64_t)blockIdx.x * WAVES + wave) * 32 * NT;
-    Stager<WAVES> st;
+    Stager<WAVES, DBG & 3> st;
     st.start(a.wpack, lds, 12);
 
     bf16x8 x0[NT][3];
@@ -470,7 +498,7 @@ void sigma_meshrir_h1_kernel(Args a) {
     for (int c = 0; c < 4; ++c) {
         f32x16 acc[NT][4];
         dense<NT, 8, 4, 4>(st, lane, xs, acc);
-        store_h1<NT>(a, acc, n0, lane, c);
+        store_h1<NT, !(DBG & 4)>(a, acc, n0, lane, c, lds + 2 * kChunk + wave * 4096);
     }
 }
 
@@ -533,11 +561,11 @@ int launch_meshrir(const Args& a, hipStream_t st) {
     return check_launch("avr_sigma_fwd");
 }
 
-template <int NT, int WAVES, int OCC>
+template <int NT, int WAVES, int OCC, int DBG = 0>
 int launch_meshrir_h1(const Args& a, hipStream_t st) {
     const int64_t per_block = 32 * NT * WAVES;
     const dim3 grid((unsigned)((a.N + per_block - 1) / per_block));
-    hipLaunchKernelGGL((sigma_meshrir_h1_kernel<NT, WAVES, OCC>), grid, dim3(64 * WAVES), 0, st, a);
+    hipLaunchKernelGGL((sigma_meshrir_h1_kernel<NT, WAVES, OCC, DBG>), grid, dim3(64 * WAVES), 0, st, a);
     return check_launch("avr_sigma_fwd");
 }
 
@@ -602,7 +630,16 @@ extern "C" int avr_sigma_fwd(const avr_sigma_desc* d, const void* wpack, void* b
     a.bias_div = d->bias_div;
     hipStream_t st = as_stream(stream);
     if (h1) {
-        if (d->tile_cfg == 1) return launch_meshrir_h1<1, 8, 1>(a, st);
+        // 0: 4 waves, streaming h1 stores (120 us at config 2); 1: 8 waves;
+        // 2, 3: the same with plain stores (130 us)
+        a.nt_store = d->tile_cfg < 2;
+        if (d->tile_cfg == 1 || d->tile_cfg == 3) return launch_meshrir_h1<1, 8, 1>(a, st);
+        // timing experiments (results are garbage): no barrier / no weight
+        // staging / no h1 stores
+        if (d->tile_cfg == 16) return launch_meshrir_h1<1, 4, 2, 1>(a, st);
+        if (d->tile_cfg == 17) return launch_meshrir_h1<1, 4, 2, 2>(a, st);
+        if (d->tile_cfg == 18) return launch_meshrir_h1<1, 4, 2, 4>(a, st);
+        if (d->tile_cfg == 19) return launch_meshrir_h1<1, 4, 2, 7>(a, st);
         return launch_meshrir_h1<1, 4, 2>(a, st);
     }
     const int cfg = d->tile_cfg;

@@ -159,7 +159,7 @@ def test_sigma_h1_kernel_matches_reference(N, S):
     bias = torch.randn(-(-N // S), 512, device=DEV, generator=g) * 0.3
     packed = sigma.pack_layers(sigma.MESHRIR_H1, ws)
     ra, rh = sigma.reference_fwd(sigma.MESHRIR_H1, ws, inputs, [], N, 0.01, bias=bias, bias_div=S)
-    for cfg in (0, 1):
+    for cfg in (0, 1, 2, 3):
         attn, h1 = sigma.sigma_fwd(sigma.MESHRIR_H1, packed, N, inputs, [], 512, 0.01, tile_cfg=cfg,
                                    bias=bias, bias_div=S)
         torch.cuda.synchronize()

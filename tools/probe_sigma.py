@@ -47,8 +47,12 @@ def main():
         out_w = 256
     flops = 2 * N * sum(M * K for M, K, _, _ in sigma.SCHEDULE[v])
     for cfg in [int(c) for c in a.cfgs.split(",")]:
-        for _ in range(3):
-            sigma.sigma_fwd(v, packed, N, inputs, extras, out_w, 0.01, tile_cfg=cfg, bias=bias, bias_div=S)
+        import time
+        t_end = time.time() + 0.5  # clocks settle before timing
+        while time.time() < t_end:
+            for _ in range(20):
+                sigma.sigma_fwd(v, packed, N, inputs, extras, out_w, 0.01, tile_cfg=cfg, bias=bias, bias_div=S)
+            torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.iters):
