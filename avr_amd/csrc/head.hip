@@ -384,7 +384,14 @@ __global__ __launch_bounds__(kThreads) void head_sort_kernel(avr_render_params p
 // z[t] += sum_k W[t,k] C[k][cnt[t]].  The next block's h rows and W rows are
 // loaded as soon as the current ones are consumed (LDS-only barriers keep
 // them in flight).
-template <typename Th, int KB, int NT, int RPT>
+//
+// SB > 1: each ray's h is loaded SB feature blocks at a time (64 bytes for
+// bf16 with SB = 2), the next such super-block in flight under the current
+// one's SB blocks.  A 128-byte line of a row holds 64 bf16 features: loaded
+// one 32-byte block at a time it is requested 4 times, spread over 4 block
+// iterations, and with ~64 workgroups per XCD each holding 1024 such lines
+// it has left L2 by then (PMC: 1.08 GB fetched for the 268 MB h at config 2).
+template <typename Th, int KB, int NT, int RPT, int SB>
 __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp, int B, int R, int K,
                                                             int KG, const Th* __restrict__ h,
                                                             const Th* __restrict__ W,
@@ -409,15 +416,10 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp
     int ct[NT];
 #pragma unroll
     for (int i = 0; i < NT; ++i) ct[i] = cnt[col * T + min((int)threadIdx.x + kThreads * i, T - 1)];
-    Raw<Th, KB> hv[RPT];
-    load_sorted_rows<Th, KB, RPT>(hv, h, hrow0, hstride, kbeg, own);
     float zacc[NT];
 #pragma unroll
     for (int i = 0; i < NT; ++i) zacc[i] = 0.0f;
-    for (int k0 = kbeg; k0 < kend; k0 += KB) {
-        if (!(dbg & 1)) build_cumsum<Th, KB, RPT>(C, R, own.n, own.spt, own.w, hv, wtotf);
-        if (k0 + KB < kend) load_sorted_rows<Th, KB, RPT>(hv, h, hrow0, hstride, k0 + KB, own);
-        lds_barrier();
+    auto contract = [&](int k0) {
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
             const int t = threadIdx.x + kThreads * i;
@@ -430,6 +432,37 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp
         }
         if (k0 + KB < kend) load_wrows<Th, KB, NT>(wt, W, K, k0 + KB, T);
         lds_barrier();  // C and wtotf are rewritten by the next block
+    };
+    if constexpr (SB == 1) {
+        Raw<Th, KB> hv[RPT];
+        load_sorted_rows<Th, KB, RPT>(hv, h, hrow0, hstride, kbeg, own);
+        for (int k0 = kbeg; k0 < kend; k0 += KB) {
+            if (!(dbg & 1)) build_cumsum<Th, KB, RPT>(C, R, own.n, own.spt, own.w, hv, wtotf);
+            if (k0 + KB < kend) load_sorted_rows<Th, KB, RPT>(hv, h, hrow0, hstride, k0 + KB, own);
+            lds_barrier();
+            contract(k0);
+        }
+    } else {
+        constexpr int ND = Raw<Th, KB>::ND;
+        Raw<Th, KB * SB> nxt[RPT];
+        load_sorted_rows<Th, KB * SB, RPT>(nxt, h, hrow0, hstride, kbeg, own);
+        for (int k0 = kbeg; k0 < kend; k0 += KB * SB) {
+            Raw<Th, KB * SB> big[RPT];
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) big[u] = nxt[u];
+            if (k0 + KB * SB < kend) load_sorted_rows<Th, KB * SB, RPT>(nxt, h, hrow0, hstride, k0 + KB * SB, own);
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) {
+                Raw<Th, KB> hv[RPT];
+#pragma unroll
+                for (int u = 0; u < RPT; ++u)
+#pragma unroll
+                    for (int d = 0; d < ND; ++d) hv[u].d[d] = big[u].d[sb * ND + d];
+                if (!(dbg & 1)) build_cumsum<Th, KB, RPT>(C, R, own.n, own.spt, own.w, hv, wtotf);
+                lds_barrier();
+                contract(k0 + sb * KB);
+            }
+        }
     }
     float* out = zpart + (((int64_t)kg * B + b) * S + s) * T;
 #pragma unroll
@@ -721,14 +754,39 @@ extern "C" int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, co
     hipStream_t st = as_stream(stream);
     const char* dbg_env = getenv("AVR_HEAD_DBG");  // profiling only: skip phases
     const int dbg = dbg_env ? atoi(dbg_env) : 0;
+    // Forward-only block shape for 16-bit h (tools/probe_head.py sweep, MI355X):
+    // feature blocks of <= 8 (C[kb][R+1] of 33 KB: 4 workgroups per CU
+    // instead of 2) and SB blocks per row load (4 while the t slots leave the
+    // registers: NT <= 4, else 2): config 2 0.36 -> 0.24 ms, config 3 0.17 ->
+    // 0.16 ms for the render with the head.  AVR_HEAD_KB / AVR_HEAD_SB
+    // override (experiments).
+    int kbf = hs.kb, sb = 1;
+    if (dtype == AVR_DTYPE_BF16 && hs.rpt <= 8) {
+        kbf = hs.kb > 8 ? 8 : hs.kb;
+        sb = hs.nt <= 4 ? 4 : 2;
+        if (const char* e = getenv("AVR_HEAD_KB")) kbf = atoi(e);
+        if (const char* e = getenv("AVR_HEAD_SB")) sb = atoi(e);
+        if ((kbf != 4 && kbf != 8 && kbf != 16) || kbf > hs.kb) kbf = hs.kb;
+        if ((sb != 1 && sb != 2 && sb != 4) || hs.kg % (sb * kbf) != 0) sb = 1;
+    }
+    HeadShape hf = hs;
+    hf.kb = kbf;
+    hf.lds_c = cumsum_lds_bytes(R, kbf);
     auto go = [&](auto kern, auto hp, auto wp) {
-        allow_lds(kern, hs.lds_c);
-        hipLaunchKernelGGL(kern, grid, dim3(kThreads), hs.lds_c, st, *p, (int)B, R, (int)K, hs.kg, hp, wp,
+        allow_lds(kern, hf.lds_c);
+        hipLaunchKernelGGL(kern, grid, dim3(kThreads), hf.lds_c, st, *p, (int)B, R, (int)K, hf.kg, hp, wp,
                            perm, ws, cnt, zpart, dbg);
     };
 #define AVR_HF(TH, KBV, NTV, RP)                                                                   \
-    if (hs.kb == KBV && hs.nt == NTV && hs.rpt == RP)                                              \
-        go(head_fwd_kernel<TH, KBV, NTV, RP>, (const TH*)h, (const TH*)W);
+    if (hf.kb == KBV && hf.nt == NTV && hf.rpt == RP) {                                            \
+        constexpr bool kSb = sizeof(TH) == 2 && RP <= 8;                                            \
+        if (kSb && sb == 2)                                                                         \
+            go(head_fwd_kernel<TH, KBV, NTV, RP, kSb ? 2 : 1>, (const TH*)h, (const TH*)W);         \
+        else if (kSb && sb == 4)                                                                    \
+            go(head_fwd_kernel<TH, KBV, NTV, RP, kSb ? 4 : 1>, (const TH*)h, (const TH*)W);         \
+        else                                                                                        \
+            go(head_fwd_kernel<TH, KBV, NTV, RP, 1>, (const TH*)h, (const TH*)W);                   \
+    }
 #define AVR_HF_R(TH, KBV, NTV) AVR_HF(TH, KBV, NTV, 4) AVR_HF(TH, KBV, NTV, 8) AVR_HF(TH, KBV, NTV, 16)
 #define AVR_HF_ALL(TH)                                                                             \
     AVR_HF_R(TH, 4, 4) AVR_HF_R(TH, 4, 8) AVR_HF_R(TH, 4, 16) AVR_HF_R(TH, 8, 4) AVR_HF_R(TH, 8, 8) \
