@@ -171,6 +171,16 @@ __device__ __forceinline__ void load_rows(Raw<Th, KB> (&v)[RPT], const Th* __res
         v[u].load(h + hrow0 + (int64_t)min((int)threadIdx.x + kThreads * u, R - 1) * hstride + k0);
 }
 
+// W rows t of feature block k0 / KB from the forward's packed layout
+// Wp[K/KB][T][KB] (avr_head_pack_w): a wave-instruction reads 64 consecutive
+// t, i.e. 64*KB contiguous elements, instead of 64 rows K elements apart.
+template <typename Th, int KB, int NT>
+__device__ __forceinline__ void load_wpacked(Raw<Th, KB> (&v)[NT], const Th* __restrict__ Wp, int k0, int T) {
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+        v[i].load(Wp + ((int64_t)(k0 / KB) * T + min((int)threadIdx.x + kThreads * i, T - 1)) * KB);
+}
+
 template <typename Th, int KB, int NT>
 __device__ __forceinline__ void load_wrows(Raw<Th, KB> (&v)[NT], const Th* __restrict__ W, int K, int k0,
                                            int T) {
@@ -261,40 +271,57 @@ __device__ __forceinline__ int sort_rays(const Rays<RPT>& rays, int lim, int T, 
     return T > 0 ? cnt[T - 1] : 0;
 }
 
-// C[k][p] (row stride R+1) = sum of w h[k] over the first p sorted rays,
-// i.e. P[k][t] = C[k][cnt[t]].  Thread j owns sorted positions
-// j*spt .. j*spt+spt-1; its h rows (hv, already loaded) are summed locally,
-// the per-thread totals scanned across the block.
+// Row stride of C: C[k][j] sits at k*RS + 3 + j, so the slots j = p0+1 ..
+// p0+RPT a thread owns (p0 = tid*RPT) start 16-byte aligned, and a thread
+// whose last owned slot runs past the row's n rays stays inside the row.
+__host__ __device__ constexpr int cs_stride(int R) { return ((R + 22) / 4) * 4; }
+
+// DPP operand of a wave-wide scan step (VALU cross-lane move, no LDS trip)
+template <int CTRL, int ROW_MASK, bool BOUND>
+__device__ __forceinline__ float dpp(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROW_MASK, 0xf, BOUND));
+}
+
+// Inclusive scan over the 64 lanes: row_shr 1,2,4,8 inside each 16-lane row,
+// then row_bcast:15 / row_bcast:31 carry the row totals forward.
+__device__ __forceinline__ float wave_scan_incl(float x) {
+    x += dpp<0x111, 0xf, true>(x);
+    x += dpp<0x112, 0xf, true>(x);
+    x += dpp<0x114, 0xf, true>(x);
+    x += dpp<0x118, 0xf, true>(x);
+    x += dpp<0x142, 0xa, false>(x);
+    x += dpp<0x143, 0xc, false>(x);
+    return x;
+}
+
+// C[k][j] = sum of w h[k] over the first j sorted rays, i.e.
+// P[k][t] = C[k][cnt[t]].  Thread i owns sorted positions i*spt ..
+// i*spt+spt-1; its h rows (hv, already loaded) are summed locally, the
+// per-thread totals scanned across the block (DPP inside a wave, 4 LDS slots
+// across waves).  When a thread owns RPT positions (spt == RPT) its slots are
+// written as 16-byte vectors.
 template <typename Th, int KB, int RPT>
 __device__ __forceinline__ void build_cumsum(float* C, int R, int n, int spt, const float (&wr)[RPT],
                                              const Raw<Th, KB> (&hv)[RPT], float* wtotf) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int RS = cs_stride(R);
     const int p0 = threadIdx.x * spt;
-    float pre[RPT][KB];
+    // local totals first; the local prefixes are recomputed (same fmaf
+    // chain, bit-identical) while C is written, instead of held in RPT*KB
+    // registers across the scan
     float run[KB];
 #pragma unroll
     for (int k = 0; k < KB; ++k) run[k] = 0.0f;
 #pragma unroll
-    for (int u = 0; u < RPT; ++u) {
+    for (int u = 0; u < RPT; ++u)
 #pragma unroll
-        for (int k = 0; k < KB; ++k) {
-            run[k] = fmaf(wr[u], hv[u][k], run[k]);
-            pre[u][k] = run[k];
-        }
-    }
+        for (int k = 0; k < KB; ++k) run[k] = fmaf(wr[u], hv[u][k], run[k]);
     // exclusive scan of run[k] over the 256 threads
     float off[KB];
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
-        float x = run[k];
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const float y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
-        float ex = __shfl_up(x, 1, 64);
-        if (lane == 0) ex = 0.0f;
-        off[k] = ex;
+        const float x = wave_scan_incl(run[k]);
+        off[k] = dpp<0x138, 0xf, true>(x);  // wave_shr:1 (lane 0 reads 0): exclusive
         if (lane == 63) wtotf[wave * KB + k] = x;
     }
     lds_barrier();
@@ -306,13 +333,33 @@ __device__ __forceinline__ void build_cumsum(float* C, int R, int n, int spt, co
     }
     if (threadIdx.x == 0)
 #pragma unroll
-        for (int k = 0; k < KB; ++k) C[k * (R + 1)] = 0.0f;
+        for (int k = 0; k < KB; ++k) C[k * RS + 3] = 0.0f;
+    if (RPT % 4 == 0 && spt == RPT) {
+        if (p0 < n)
 #pragma unroll
-    for (int u = 0; u < RPT; ++u) {
-        const int p = p0 + u;
-        if (u < spt && p < n)
+            for (int k = 0; k < KB; ++k) {
+                float r = 0.0f;
 #pragma unroll
-            for (int k = 0; k < KB; ++k) C[k * (R + 1) + p + 1] = off[k] + pre[u][k];
+                for (int c = 0; c < RPT / 4; ++c) {
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        r = fmaf(wr[4 * c + e], hv[4 * c + e][k], r);
+                        v[e] = off[k] + r;
+                    }
+                    *reinterpret_cast<f32x4*>(C + k * RS + 4 + p0 + 4 * c) = f32x4{v[0], v[1], v[2], v[3]};
+                }
+            }
+    } else {
+#pragma unroll
+        for (int k = 0; k < KB; ++k) {
+            float r = 0.0f;
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                r = fmaf(wr[u], hv[u][k], r);
+                if (u < spt && p0 + u < n) C[k * RS + 4 + p0 + u] = off[k] + r;
+            }
+        }
     }
 }
 
@@ -344,9 +391,9 @@ __device__ __forceinline__ void load_sorted_rows(Raw<Th, KB> (&v)[RPT], const Th
     for (int u = 0; u < RPT; ++u) v[u].load(h + hrow0 + (int64_t)own.ray[u] * hstride + k0);
 }
 
-// LDS of the cumulative-sum kernels: C[KB][R+1] | wave totals
+// LDS of the cumulative-sum kernels: C[KB][cs_stride(R)] | wave totals
 __host__ __device__ constexpr size_t cumsum_lds_bytes(int R, int KB) {
-    return 4 * ((size_t)KB * (R + 1) + 4 * (size_t)KB);
+    return 4 * ((size_t)KB * cs_stride(R) + 4 * (size_t)KB);
 }
 
 // Counting sort of the rays of every column (b, s) by delay (rays with an
@@ -378,6 +425,19 @@ __global__ __launch_bounds__(kThreads) void head_sort_kernel(avr_render_params p
     for (int t = threadIdx.x; t < T; t += kThreads) cnt_out[col * T + t] = cnt[t];
 }
 
+// W [T][K] -> Wp[K/KB][T][KB] (the forward's feature-block-major layout)
+template <typename Th>
+__global__ __launch_bounds__(kThreads) void head_pack_w_kernel(int T, int K, int KB, const Th* __restrict__ W,
+                                                               Th* __restrict__ Wp) {
+    const int64_t n = (int64_t)T * K;
+    for (int64_t i = blockIdx.x * (int64_t)kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+        const int j = (int)(i % KB);
+        const int64_t r = i / KB;  // = kb * T + t
+        const int t = (int)(r % T), kb = (int)(r / T);
+        Wp[i] = W[(int64_t)t * K + kb * KB + j];
+    }
+}
+
 // ------------------------------------------------------------------ forward
 // Per (feature group, s, b): rays counting-sorted by delay once; per feature
 // block, cumulative sums over the sorted rays (no float atomics), then
@@ -391,6 +451,7 @@ __global__ __launch_bounds__(kThreads) void head_sort_kernel(avr_render_params p
 // one 32-byte block at a time it is requested 4 times, spread over 4 block
 // iterations, and with ~64 workgroups per XCD each holding 1024 such lines
 // it has left L2 by then (PMC: 1.08 GB fetched for the 268 MB h at config 2).
+// W here is the packed Wp[K/KB][T][KB] of avr_head_pack_w.
 template <typename Th, int KB, int NT, int RPT, int SB>
 __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp, int B, int R, int K,
                                                             int KG, const Th* __restrict__ h,
@@ -402,15 +463,16 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp
     extern __shared__ float lds_f[];
     const int T = pp.T, S = pp.n_samples;
     const int kg = blockIdx.x, s = blockIdx.y, b = blockIdx.z;
-    float* C = lds_f;                  // [KB][R+1]
-    float* wtotf = C + KB * (R + 1);   // [4][KB]
+    float* C = lds_f;                  // [KB][RS]
+    const int RS = cs_stride(R);
+    float* wtotf = C + KB * RS;        // [4][KB]
     const int lim = tail_limit(pp, s);
     const int64_t col = (int64_t)b * S + s;
     const int64_t hrow0 = ((int64_t)b * R * S + s) * K;
     const int64_t hstride = (int64_t)S * K;
     const int kbeg = kg * KG, kend = kbeg + KG;
     Raw<Th, KB> wt[NT];
-    load_wrows<Th, KB, NT>(wt, W, K, kbeg, T);
+    load_wpacked<Th, KB, NT>(wt, W, kbeg, T);
     Owned<RPT> own;
     own.load(perm + col * R, ws + col * R, cnt + col * T, T);
     int ct[NT];
@@ -426,11 +488,11 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp
             if (t < lim && !(dbg & 4)) {
                 float a = zacc[i];
 #pragma unroll
-                for (int k = 0; k < KB; ++k) a = fmaf(wt[i][k], C[k * (R + 1) + ct[i]], a);
+                for (int k = 0; k < KB; ++k) a = fmaf(wt[i][k], C[k * RS + 3 + ct[i]], a);
                 zacc[i] = a;
             }
         }
-        if (k0 + KB < kend) load_wrows<Th, KB, NT>(wt, W, K, k0 + KB, T);
+        if (k0 + KB < kend) load_wpacked<Th, KB, NT>(wt, W, k0 + KB, T);
         lds_barrier();  // C and wtotf are rewritten by the next block
     };
     if constexpr (SB == 1) {
@@ -445,12 +507,13 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp
     } else {
         constexpr int ND = Raw<Th, KB>::ND;
         Raw<Th, KB * SB> nxt[RPT];
-        load_sorted_rows<Th, KB * SB, RPT>(nxt, h, hrow0, hstride, kbeg, own);
+        auto load_sb = [&](int k0) { load_sorted_rows<Th, KB * SB, RPT>(nxt, h, hrow0, hstride, k0, own); };
+        load_sb(kbeg);
         for (int k0 = kbeg; k0 < kend; k0 += KB * SB) {
             Raw<Th, KB * SB> big[RPT];
 #pragma unroll
             for (int u = 0; u < RPT; ++u) big[u] = nxt[u];
-            if (k0 + KB * SB < kend) load_sorted_rows<Th, KB * SB, RPT>(nxt, h, hrow0, hstride, k0 + KB * SB, own);
+            if (k0 + KB * SB < kend) load_sb(k0 + KB * SB);
 #pragma unroll
             for (int sb = 0; sb < SB; ++sb) {
                 Raw<Th, KB> hv[RPT];
@@ -570,7 +633,8 @@ __global__ __launch_bounds__(kThreads) void head_bwd_w_kernel(avr_render_params 
     const int kb = blockIdx.x, sg = blockIdx.y, b = blockIdx.z;
     const int k0 = kb * KB;
     float* C = lds_f;
-    float* wtotf = C + KB * (R + 1);
+    const int RS = cs_stride(R);
+    float* wtotf = C + KB * RS;
     const int64_t hstride = (int64_t)S * K;
     float acc[NT][KB];
 #pragma unroll
@@ -613,7 +677,7 @@ __global__ __launch_bounds__(kThreads) void head_bwd_w_kernel(avr_render_params 
             const int t = threadIdx.x + kThreads * i;
             if (t < lim) {
 #pragma unroll
-                for (int k = 0; k < KB; ++k) acc[i][k] = fmaf(gc[i], C[k * (R + 1) + cc[i]], acc[i][k]);
+                for (int k = 0; k < KB; ++k) acc[i][k] = fmaf(gc[i], C[k * RS + 3 + cc[i]], acc[i][k]);
             }
         }
     }
@@ -708,7 +772,47 @@ void dw_groups(const HeadShape& hs, int B, int S, int K, int* n_sg, int* s_per) 
     *n_sg = (S + *s_per - 1) / *s_per;
 }
 
+// Forward-only block shape for 16-bit h (tools/probe_head.py sweep, MI355X):
+// feature blocks of <= 8 (C[kb][RS] of 33 KB: 4 workgroups per CU instead of
+// 2) and SB blocks per row load (4 while the t slots leave the registers:
+// NT <= 4, else 2): config 2 0.36 -> 0.24 ms, config 3 0.17 -> 0.16 ms for
+// the render with the head.  AVR_HEAD_KB / AVR_HEAD_SB override (experiments).
+void fwd_block(const HeadShape& hs, int dtype, int* kb, int* sb) {
+    int kbf = hs.kb, s = 1;
+    if (dtype == AVR_DTYPE_BF16 && hs.rpt <= 8) {
+        kbf = hs.kb > 8 ? 8 : hs.kb;
+        s = hs.nt <= 4 ? 4 : 2;
+        if (const char* e = getenv("AVR_HEAD_KB")) kbf = atoi(e);
+        if (const char* e = getenv("AVR_HEAD_SB")) s = atoi(e);
+        if ((kbf != 4 && kbf != 8 && kbf != 16) || kbf > hs.kb) kbf = hs.kb;
+        if ((s != 1 && s != 2 && s != 4) || hs.kg % (s * kbf) != 0) s = 1;
+    }
+    *kb = kbf;
+    *sb = s;
+}
+
 }  // namespace
+
+extern "C" int avr_head_pack_w(const avr_render_params* p, int32_t B, int32_t K, const void* W, int32_t dtype,
+                               void* Wp, void* stream) {
+    if (int e = head_check(p, B, K, W, W, dtype)) return e;
+    AVR_REQUIRE(Wp && reinterpret_cast<uintptr_t>(Wp) % 16 == 0, "avr_head_pack_w: Wp must be 16-byte aligned");
+    HeadShape hs;
+    if (int e = head_shape(*p, B, n_rays(*p), K, dtype == AVR_DTYPE_BF16 ? 2 : 4, &hs)) return e;
+    int kbf, sb;
+    fwd_block(hs, dtype, &kbf, &sb);
+    const int T = p->T;
+    const int64_t n = (int64_t)T * K;
+    const int blocks = (int)std::min<int64_t>((n + kThreads - 1) / kThreads, 4096);
+    hipStream_t st = as_stream(stream);
+    if (dtype == AVR_DTYPE_BF16)
+        hipLaunchKernelGGL(head_pack_w_kernel<__hip_bfloat16>, dim3(blocks), dim3(kThreads), 0, st, T, (int)K, kbf,
+                           (const __hip_bfloat16*)W, (__hip_bfloat16*)Wp);
+    else
+        hipLaunchKernelGGL(head_pack_w_kernel<float>, dim3(blocks), dim3(kThreads), 0, st, T, (int)K, kbf,
+                           (const float*)W, (float*)Wp);
+    return check_launch("avr_head_pack_w");
+}
 
 extern "C" int avr_head_splits(const avr_render_params* p, int32_t B, int32_t K, int32_t dtype,
                                int32_t* n_split) {
@@ -754,21 +858,8 @@ extern "C" int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, co
     hipStream_t st = as_stream(stream);
     const char* dbg_env = getenv("AVR_HEAD_DBG");  // profiling only: skip phases
     const int dbg = dbg_env ? atoi(dbg_env) : 0;
-    // Forward-only block shape for 16-bit h (tools/probe_head.py sweep, MI355X):
-    // feature blocks of <= 8 (C[kb][R+1] of 33 KB: 4 workgroups per CU
-    // instead of 2) and SB blocks per row load (4 while the t slots leave the
-    // registers: NT <= 4, else 2): config 2 0.36 -> 0.24 ms, config 3 0.17 ->
-    // 0.16 ms for the render with the head.  AVR_HEAD_KB / AVR_HEAD_SB
-    // override (experiments).
-    int kbf = hs.kb, sb = 1;
-    if (dtype == AVR_DTYPE_BF16 && hs.rpt <= 8) {
-        kbf = hs.kb > 8 ? 8 : hs.kb;
-        sb = hs.nt <= 4 ? 4 : 2;
-        if (const char* e = getenv("AVR_HEAD_KB")) kbf = atoi(e);
-        if (const char* e = getenv("AVR_HEAD_SB")) sb = atoi(e);
-        if ((kbf != 4 && kbf != 8 && kbf != 16) || kbf > hs.kb) kbf = hs.kb;
-        if ((sb != 1 && sb != 2 && sb != 4) || hs.kg % (sb * kbf) != 0) sb = 1;
-    }
+    int kbf, sb;
+    fwd_block(hs, dtype, &kbf, &sb);
     HeadShape hf = hs;
     hf.kb = kbf;
     hf.lds_c = cumsum_lds_bytes(R, kbf);

@@ -321,7 +321,9 @@ class FusedHeadCore(torch.autograd.Function):
         _lib.call("avr_head_splits", pref, B, K, code, ctypes.byref(ns))
         n_split = ns.value
         part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
-        _lib.call("avr_head_fwd", pref, B, K, _ptr(h), _ptr(W), code, _ptr(perm), _ptr(ws), _ptr(cnt),
+        Wp = torch.empty_like(W)
+        _lib.call("avr_head_pack_w", pref, B, K, _ptr(W), code, _ptr(Wp), st)
+        _lib.call("avr_head_fwd", pref, B, K, _ptr(h), _ptr(Wp), code, _ptr(perm), _ptr(ws), _ptr(cnt),
                   n_split, _ptr(part), st)
         out = _spectrum(p, tables, part, n_split, B, dev, st)
         ctx.p, ctx.tables = p, tables

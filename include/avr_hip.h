@@ -327,6 +327,13 @@ int avr_head_splits(const avr_render_params* p, int32_t B, int32_t K, int32_t dt
  * of kept rays with delay <= t).  Input to avr_head_fwd and avr_head_bwd. */
 int avr_head_sort(const avr_render_params* p, int32_t B, const float* w, const int32_t* delay,
                   int32_t* perm, float* ws, int32_t* cnt, void* stream);
+/* W [T][K] -> Wp (same size) in the forward's feature-block-major layout
+ * [K/kb][T][kb] (kb chosen from p, B, K, dtype as in avr_head_fwd): one
+ * wave-instruction of the forward then reads 64 consecutive t of a block
+ * contiguously.  Wp is avr_head_fwd's W argument. */
+int avr_head_pack_w(const avr_render_params* p, int32_t B, int32_t K, const void* W, int32_t dtype,
+                    void* Wp, void* stream);
+/* W: the packed weight from avr_head_pack_w (same p, B, K, dtype). */
 int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* W,
                  int32_t dtype, const int32_t* perm, const float* ws, const int32_t* cnt,
                  int32_t n_split, float* zpart, void* stream);
