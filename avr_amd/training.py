@@ -6,8 +6,8 @@ the MI355X path, and its checkpoint format (avr_runner.py:136-153, 105-130).
     losses = step(ori_sig, position_rx, position_tx, direction_tx)  # RAF
 
 Per call: render -> Criterion (HIP, all eight terms) -> sum -> backward ->
-clip_grad_norm_(max_norm=1) + NaN/Inf zeroing (one HIP launch for all
-gradients, `avr_scale_sanitize`) -> Adam -> CosineAnnealingLR, the order and
+clip_grad_norm_(max_norm=1) + NaN/Inf zeroing + Adam (one HIP pass over
+p, g, m, v: `avr_adam_step`) -> CosineAnnealingLR, the order and
 hyper-parameters of avr_runner.py:67-73, 181-200.  The reference's
 `torch.isnan(energy_loss).item()` skip (avr_runner.py:183) is kept when
 `nan_check=True` (the default, one host sync per step, as the reference).
@@ -15,6 +15,7 @@ hyper-parameters of avr_runner.py:67-73, 181-200.  The reference's
 from __future__ import annotations
 
 import ctypes
+import math
 
 import torch
 
@@ -24,6 +25,14 @@ from .criterion import Criterion
 
 def _stream(dev):
     return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _clip_coef(grads, max_norm):
+    """clip_grad_norm_'s total norm and clamped coefficient, on the device."""
+    norms = torch._foreach_norm(grads, 2.0)
+    total = torch.linalg.vector_norm(torch.stack([n.float() for n in norms]), 2.0)
+    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    return total, coef
 
 
 def clip_and_sanitize_(params, max_norm=1.0):
@@ -40,9 +49,7 @@ def clip_and_sanitize_(params, max_norm=1.0):
     dev = grads[0].device
     if not grads[0].is_cuda:
         raise RuntimeError("clip_and_sanitize_ needs HIP tensors (no CPU fallback)")
-    norms = torch._foreach_norm(grads, 2.0)
-    total = torch.linalg.vector_norm(torch.stack([n.float() for n in norms]), 2.0)
-    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    total, coef = _clip_coef(grads, max_norm)
     fast = [g for g in grads if g.dtype == torch.float32 and g.is_contiguous() and g.device == dev]
     other = [g for g in grads if not (g.dtype == torch.float32 and g.is_contiguous() and g.device == dev)]
     if fast:
@@ -56,15 +63,84 @@ def clip_and_sanitize_(params, max_norm=1.0):
     return total
 
 
+def _native_adam_ok(optimizer):
+    for group in optimizer.param_groups:
+        if group.get("amsgrad") or group.get("maximize") or group.get("differentiable"):
+            return False
+        for p in group["params"]:
+            if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()):
+                return False
+    return True
+
+
+def clip_sanitize_adam_(optimizer, max_norm=1.0):
+    """clip_and_sanitize_ + optimizer.step() of a torch.optim.Adam
+    (avr_runner.py:190-200) as one HIP pass per parameter (`avr_adam_step`):
+    p, g, m, v read once, p, m, v written once.
+
+    The optimiser state stays in torch.optim.Adam's own (non-fused) layout --
+    `step` a CPU float tensor, `exp_avg`, `exp_avg_sq` -- so state_dict(),
+    load_state_dict(), checkpoints and the LR scheduler are unchanged.  The
+    clipped, sanitised gradient is consumed inside the kernel and not written
+    back to p.grad (the loop zeroes it before the next backward).  Returns the
+    total norm (a device tensor).
+    """
+    params = [p for g in optimizer.param_groups for p in g["params"] if p.grad is not None]
+    if not params:
+        return torch.zeros(())
+    dev = params[0].device
+    total, coef = _clip_coef([p.grad for p in params], max_norm)
+    st_ = _stream(dev)
+    for group in optimizer.param_groups:
+        b1, b2 = group["betas"]
+        lr = float(group["lr"])
+        ps, gs, ms, vs, ns, ss, bs = [], [], [], [], [], [], []
+        for p in group["params"]:
+            if p.grad is None:
+                continue
+            g = p.grad
+            if not (g.dtype == torch.float32 and g.is_contiguous()):
+                raise RuntimeError("clip_sanitize_adam_: gradients must be contiguous fp32")
+            st = optimizer.state[p]
+            if len(st) == 0:
+                st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            if st["step"].is_cuda:  # state loaded from a fused/capturable optimiser
+                st["step"] = st["step"].cpu()
+            st["step"] += 1
+            step = float(st["step"])
+            ps.append(p.data_ptr())
+            gs.append(g.data_ptr())
+            ms.append(st["exp_avg"].data_ptr())
+            vs.append(st["exp_avg_sq"].data_ptr())
+            ns.append(p.numel())
+            ss.append(lr / (1.0 - b1 ** step))
+            bs.append(math.sqrt(1.0 - b2 ** step))
+        if not ps:
+            continue
+        n = len(ps)
+        arr = lambda t, xs: (t * n)(*xs)  # noqa: E731
+        with torch.cuda.device(dev):
+            _lib.call("avr_adam_step", n, arr(ctypes.c_void_p, ps), arr(ctypes.c_void_p, gs),
+                      arr(ctypes.c_void_p, ms), arr(ctypes.c_void_p, vs), arr(ctypes.c_int64, ns),
+                      arr(ctypes.c_float, ss), arr(ctypes.c_float, bs), float(b1), float(b2),
+                      float(group["eps"]), float(group["weight_decay"]), coef.data_ptr(), st_)
+    return total
+
+
 class TrainStep:
     """avr_runner.py's optimiser, scheduler, criterion and inner-loop body."""
 
-    def __init__(self, renderer, train_cfg, render_cfg, fused_adam=True, nan_check=True):
+    def __init__(self, renderer, train_cfg, render_cfg, fused_adam=True, nan_check=True, native_adam=True):
         self.renderer = renderer
         self.criterion = Criterion(train_cfg, render_cfg)
+        # native_adam: clip + sanitize + Adam in one HIP pass (clip_sanitize_adam_);
+        # the Adam object then only holds state (reference's non-fused layout)
         self.optimizer = torch.optim.Adam(renderer.parameters(), lr=float(train_cfg['lr']),
                                           weight_decay=float(train_cfg.get('weight_decay', 0)),
-                                          betas=(0.9, 0.999), fused=fused_adam)
+                                          betas=(0.9, 0.999), fused=fused_adam and not native_adam)
+        self.native_adam = native_adam and _native_adam_ok(self.optimizer)
         self.scheduler = torch.optim.lr_scheduler.CosineAnnealingLR(
             optimizer=self.optimizer, T_max=float(train_cfg['T_max']),
             eta_min=float(train_cfg['eta_min']), last_epoch=-1)
@@ -86,8 +162,11 @@ class TrainStep:
             total = total + x
         self.optimizer.zero_grad(set_to_none=True)
         total.backward()
-        clip_and_sanitize_(self.renderer.parameters(), max_norm=1)
-        self.optimizer.step()
+        if self.native_adam:
+            clip_sanitize_adam_(self.optimizer, max_norm=1)
+        else:
+            clip_and_sanitize_(self.renderer.parameters(), max_norm=1)
+            self.optimizer.step()
         self.scheduler.step()
         self.current_iteration += 1
         return total.detach(), [x.detach() for x in losses[:8]]

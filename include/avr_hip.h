@@ -399,6 +399,19 @@ int avr_das_bwd(int32_t n, const float* steer, const float* angles, const float*
  * launch per 32 tensors. */
 int avr_scale_sanitize(int32_t n_tensors, float* const* ptrs, const int64_t* sizes,
                        const float* coef, void* stream);
+/* The same post-processing fused with torch.optim.Adam's update (amsgrad
+ * off, L2 weight_decay; avr_runner.py:67-69, 190-200), one pass per element:
+ *   g = finite(g*coef) ? g*coef : 0;  g += weight_decay * p;
+ *   m += (1-b1) (g - m);  v = v b2 + (1-b2) g g;
+ *   p -= step_size[i] * (m / (sqrt(v) / bc2_sqrt[i] + eps))
+ * (the fp32 operation order of torch.optim.Adam's default foreach step)
+ * with step_size = lr / (1 - b1^step), bc2_sqrt = sqrt(1 - b2^step) per
+ * tensor (host arrays).  params, grads, exp_avg, exp_avg_sq: HOST arrays of
+ * fp32 device pointers; the gradient is read, not written. */
+int avr_adam_step(int32_t n_tensors, float* const* params, const float* const* grads,
+                  float* const* exp_avg, float* const* exp_avg_sq, const int64_t* sizes,
+                  const float* step_size, const float* bc2_sqrt, double beta1, double beta2,
+                  float eps, float weight_decay, const float* coef, void* stream);
 
 #ifdef __cplusplus
 }

@@ -110,3 +110,38 @@ def test_checkpoint_round_trip(tmp_path):
     torch.manual_seed(1)
     total2, _ = step2(ori, rx, tx, dtx)
     assert abs(float(total2) - float(ref_total)) <= 1e-6 * abs(float(ref_total))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wd", [0.0, 1e-2])
+def test_native_adam_matches_torch_adam(wd):
+    """clip_sanitize_adam_ (avr_adam_step) against clip_and_sanitize_ +
+    torch.optim.Adam over 5 steps, including poisoned (NaN/Inf) gradients and
+    a parameter without a gradient; state_dict layouts interchangeable."""
+    from avr_amd.training import clip_sanitize_adam_
+    g = torch.Generator(device=DEV).manual_seed(3)
+    shapes = [(1000, 3), (7,), (4096, 2), (5, 5)]
+    ref = [torch.randn(s, device=DEV, generator=g).requires_grad_(True) for s in shapes]
+    mine = [p.detach().clone().requires_grad_(True) for p in ref]
+    o_ref = torch.optim.Adam(ref, lr=1e-3, betas=(0.9, 0.999), weight_decay=wd)
+    o_mine = torch.optim.Adam(mine, lr=1e-3, betas=(0.9, 0.999), weight_decay=wd)
+    for it in range(5):
+        for k, (a, b) in enumerate(zip(ref, mine)):
+            if k == 3 and it < 2:  # no gradient for the first two steps
+                a.grad = b.grad = None
+                continue
+            gr = torch.randn(a.shape, device=DEV, generator=g) * (3.0 if it % 2 else 0.1)
+            if k == 0:
+                gr.view(-1)[::97] = float("nan")
+                gr.view(-1)[5] = float("inf")
+            a.grad, b.grad = gr.clone(), gr.clone()
+        clip_and_sanitize_(ref, max_norm=1)
+        o_ref.step()
+        clip_sanitize_adam_(o_mine, max_norm=1)
+        for a, b in zip(ref, mine):
+            torch.testing.assert_close(b.detach(), a.detach(), rtol=2e-6, atol=2e-7)
+    for a, b in zip(ref, mine):
+        sa, sb = o_ref.state[a], o_mine.state[b]
+        assert float(sa["step"]) == float(sb["step"]) and not sb["step"].is_cuda
+        torch.testing.assert_close(sb["exp_avg"], sa["exp_avg"], rtol=2e-6, atol=1e-9)
+        torch.testing.assert_close(sb["exp_avg_sq"], sa["exp_avg_sq"], rtol=2e-6, atol=1e-12)

@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--core-only", action="store_true")
     ap.add_argument("--no-fused", action="store_true", help="materialise the signal (no fused head)")
     ap.add_argument("--foreach-adam", action="store_true", help="torch's default (foreach) Adam")
+    ap.add_argument("--torch-adam", action="store_true", help="torch's fused Adam + avr_scale_sanitize "
+                    "instead of the one-pass avr_adam_step")
     ap.add_argument("--profile", action="store_true", help="torch.profiler table of a few steps")
     ap.add_argument("--loss", default="criterion", choices=["criterion", "l1"])
     ap.add_argument("--nan-check", action="store_true", help="reference's per-step isnan().item()")
@@ -108,7 +110,7 @@ def main():
                      spec_loss_weight=1, amplitude_loss_weight=1, angle_loss_weight=1,
                      time_loss_weight=20, energy_loss_weight=3, multistft_loss_weight=2)
     ts = TrainStep(r, train_cfg, w.render, fused_adam=not args.foreach_adam,
-                   nan_check=args.nan_check)
+                   nan_check=args.nan_check, native_adam=not (args.torch_adam or args.foreach_adam))
     # measured-IR-like target spectrum: decaying noise
     tt = torch.arange(T, device=dev)
     ir = torch.randn(B, T, device=dev, generator=g) * torch.exp(-tt / (0.15 * T)) * 0.05
@@ -140,7 +142,7 @@ def main():
     res["train_ray_samples_per_s"] = w.ray_samples / t
     res["mlp_dtype"] = args.mlp_dtype
     res["fused_head"] = not args.no_fused
-    res["adam"] = "foreach" if args.foreach_adam else "fused"
+    res["adam"] = "foreach" if args.foreach_adam else ("avr_adam_step" if ts.native_adam else "fused")
     res["loss"] = args.loss
     res["nan_check"] = args.nan_check
     print(json.dumps(res))
