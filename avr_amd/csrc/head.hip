@@ -563,7 +563,7 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
         g[i] = t < lim ? v : 0.0f;
     }
     Raw<Th, KB> hv[RPT], wt[NT];
-    load_wrows<Th, KB, NT>(wt, W, K, kbeg, T);
+    load_wpacked<Th, KB, NT>(wt, W, kbeg, T);  // W packed [K/KB][T][KB] by avr_head_bwd
     load_rows<Th, KB, RPT>(hv, h, hrow0, hstride, kbeg, R);
     float gw[RPT];
 #pragma unroll
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
 #pragma unroll
                 for (int k = 0; k < KB; ++k) Q[k * T + t] = g[i] * wt[i][k];
         }
-        if (k0 + KB < kend) load_wrows<Th, KB, NT>(wt, W, K, k0 + KB, T);
+        if (k0 + KB < kend) load_wpacked<Th, KB, NT>(wt, W, k0 + KB, T);
         lds_barrier();
         scan_rows<KB, true>(Q, T);
         lds_barrier();
@@ -901,7 +901,9 @@ extern "C" int avr_head_bwd_workspace(const avr_render_params* p, int32_t B, int
     if (int e = head_shape(*p, B, R, K, dtype == AVR_DTYPE_BF16 ? 2 : 4, &hs)) return e;
     int n_sg, s_per;
     dw_groups(hs, B, S, K, &n_sg, &s_per);
-    *bytes = ((int64_t)hs.n_kg * B * R * S + (int64_t)B * n_sg * T * K) * 4;
+    // fp32 partials, then W packed in the backward's feature blocks (16-B aligned)
+    *bytes = ((int64_t)hs.n_kg * B * R * S + (int64_t)B * n_sg * T * K) * 4 + 16 +
+             (int64_t)T * K * (dtype == AVR_DTYPE_BF16 ? 2 : 4);
     return 0;
 }
 
@@ -920,11 +922,25 @@ extern "C" int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, co
     dw_groups(hs, B, S, K, &n_sg, &s_per);
     const int64_t gw_elems = (int64_t)hs.n_kg * B * R * S;
     const int64_t gW_elems = (int64_t)B * n_sg * T * K;
-    if (workspace_bytes < (gw_elems + gW_elems) * 4)
+    const int64_t es = dtype == AVR_DTYPE_BF16 ? 2 : 4;
+    if (workspace_bytes < (gw_elems + gW_elems) * 4 + 16 + (int64_t)T * K * es)
         return fail(AVR_E_ARG, "avr_head_bwd: workspace too small");
     float* gw_part = workspace;
     float* gW_part = workspace + gw_elems;
+    // W [T][K] -> [K/kb][T][kb]: head_bwd_h then reads 1 KB per wave-instruction
+    char* wp_raw = reinterpret_cast<char*>(gW_part + gW_elems);
+    void* Wb = wp_raw + ((16 - (reinterpret_cast<uintptr_t>(wp_raw) & 15)) & 15);
     hipStream_t st = as_stream(stream);
+    {
+        const int64_t n = (int64_t)T * K;
+        const int blocks = (int)std::min<int64_t>((n + kThreads - 1) / kThreads, 4096);
+        if (dtype == AVR_DTYPE_BF16)
+            hipLaunchKernelGGL(head_pack_w_kernel<__hip_bfloat16>, dim3(blocks), dim3(kThreads), 0, st, T,
+                               (int)K, hs.kb, (const __hip_bfloat16*)W, (__hip_bfloat16*)Wb);
+        else
+            hipLaunchKernelGGL(head_pack_w_kernel<float>, dim3(blocks), dim3(kThreads), 0, st, T, (int)K, hs.kb,
+                               (const float*)W, (float*)Wb);
+    }
     auto go_h = [&](auto kern, auto hp, auto wp, auto gp) {
         allow_lds(kern, hs.lds_q);
         hipLaunchKernelGGL(kern, dim3(hs.n_kg, S, B), dim3(kThreads), hs.lds_q, st, *p, (int)B, R, (int)K,
@@ -937,7 +953,7 @@ extern "C" int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, co
     };
 #define AVR_HB(TH, KBV, NTV, RP)                                                                   \
     if (hs.kb == KBV && hs.nt == NTV && hs.rpt == RP) {                                            \
-        go_h(head_bwd_h_kernel<TH, KBV, NTV, RP>, (const TH*)h, (const TH*)W, (TH*)grad_h);        \
+        go_h(head_bwd_h_kernel<TH, KBV, NTV, RP>, (const TH*)h, (const TH*)Wb, (TH*)grad_h);       \
         go_w(head_bwd_w_kernel<TH, KBV, NTV, RP>, (const TH*)h);                                   \
     }
 #define AVR_HB_R(TH, KBV, NTV) AVR_HB(TH, KBV, NTV, 4) AVR_HB(TH, KBV, NTV, 8) AVR_HB(TH, KBV, NTV, 16)

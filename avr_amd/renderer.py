@@ -291,6 +291,26 @@ class RenderCore(torch.autograd.Function):
                 None, None, None, None, None, None)
 
 
+def _packed_head_weight(w_master, W, cache, pref, shape_key, st):
+    """W in avr_head_fwd's block-major layout (avr_head_pack_w).  With
+    `cache` (no autograd graph recorded) the copy is kept on the master
+    weight until it changes, like wcache.cast_weight."""
+    key = (W.data_ptr(), w_master._version, shape_key)
+    if cache:
+        hit = getattr(w_master, "_avr_headpack", None)
+        if hit is not None and hit[0] == key:
+            return hit[1]
+    B, K, code = shape_key[2], shape_key[3], shape_key[4]
+    Wp = torch.empty_like(W)
+    _lib.call("avr_head_pack_w", pref, B, K, _ptr(W), code, _ptr(Wp), st)
+    if cache:
+        try:
+            w_master._avr_headpack = (key, Wp)
+        except AttributeError:
+            pass
+    return Wp
+
+
 class FusedHeadCore(torch.autograd.Function):
     """Render core with the signal network's last linear layer folded in
     (kernels in csrc/head.hip).
@@ -321,8 +341,7 @@ class FusedHeadCore(torch.autograd.Function):
         _lib.call("avr_head_splits", pref, B, K, code, ctypes.byref(ns))
         n_split = ns.value
         part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
-        Wp = torch.empty_like(W)
-        _lib.call("avr_head_pack_w", pref, B, K, _ptr(W), code, _ptr(Wp), st)
+        Wp = _packed_head_weight(w_master, W, cache, pref, (p.T, R, B, K, code), st)
         _lib.call("avr_head_fwd", pref, B, K, _ptr(h), _ptr(Wp), code, _ptr(perm), _ptr(ws), _ptr(cnt),
                   n_split, _ptr(part), st)
         out = _spectrum(p, tables, part, n_split, B, dev, st)
