@@ -18,6 +18,7 @@ import ctypes
 import math
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import _lib
 from .criterion import Criterion
@@ -119,6 +120,10 @@ def clip_sanitize_adam_(optimizer, max_norm=1.0):
             bs.append(math.sqrt(1.0 - b2 ** step))
         if not ps:
             continue
+        # the kernel writes through raw pointers: bump the version counters as
+        # torch's in-place update would, so version-keyed caches (wcache, the
+        # packed sigma / head weights) see the new values
+        increment_version([p for p in group["params"] if p.grad is not None])
         n = len(ps)
         arr = lambda t, xs: (t * n)(*xs)  # noqa: E731
         with torch.cuda.device(dev):

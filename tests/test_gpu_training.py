@@ -145,3 +145,23 @@ def test_native_adam_matches_torch_adam(wd):
         assert float(sa["step"]) == float(sb["step"]) and not sb["step"].is_cuda
         torch.testing.assert_close(sb["exp_avg"], sa["exp_avg"], rtol=2e-6, atol=1e-9)
         torch.testing.assert_close(sb["exp_avg_sq"], sa["exp_avg_sq"], rtol=2e-6, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_native_adam_invalidates_inference_caches():
+    """The one-pass Adam bumps the parameters' version counters, so weight
+    casts cached at inference (wcache.cast_weight) are rebuilt after a step."""
+    from avr_amd.training import clip_sanitize_adam_
+    from avr_amd.wcache import cast_weight
+    p = torch.nn.Parameter(torch.randn(64, 32, device=DEV))
+    opt = torch.optim.Adam([p], lr=1e-2)
+    with torch.no_grad():
+        c0 = cast_weight(p, torch.bfloat16, True).clone()
+    p.grad = torch.randn_like(p)
+    v0 = p._version
+    clip_sanitize_adam_(opt, max_norm=1)
+    assert p._version > v0
+    with torch.no_grad():
+        c1 = cast_weight(p, torch.bfloat16, True)
+    torch.testing.assert_close(c1, p.detach().to(torch.bfloat16), rtol=0, atol=0)
+    assert not torch.equal(c1, c0)
