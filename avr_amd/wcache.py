@@ -32,7 +32,8 @@ def cast_weight(w: torch.Tensor, dtype: torch.dtype, cache: bool = True) -> torc
 
 
 def clear(module: torch.nn.Module) -> None:
-    """Drop the cached casts of a module's parameters."""
+    """Drop the cached casts (and derived weight copies) of a module's parameters."""
     for p in module.parameters():
-        if hasattr(p, "_avr_cast"):
-            del p._avr_cast
+        for attr in ("_avr_cast", "_avr_bias_cols", "_avr_headpack"):
+            if hasattr(p, attr):
+                delattr(p, attr)
