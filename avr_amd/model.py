@@ -64,6 +64,16 @@ def _wgrad(gy, x):
     batch them (one output tile set per chunk) and sum the fp32 partials."""
     if _hip_wgrad_ok(gy, x):
         return _wgrad_hip(gy, x)
+    M = gy.size(1)
+    if M < 8 and gy.is_cuda and gy.dtype == torch.bfloat16:
+        # a 1-wide output layer (the sigma decoder's last): as a GEMM its
+        # [M, K] output has a few tiles for a K of N = B*R*S rows (86 us at
+        # config 3 for 42 MB of x); zero-padded to 8 rows it runs split-K on
+        # the HIP kernel at the speed of reading x
+        gp = torch.zeros(gy.size(0), 8, dtype=gy.dtype, device=gy.device)
+        gp[:, :M] = gy
+        if _hip_wgrad_ok(gp, x):
+            return _wgrad_hip(gp, x)[:M].contiguous()
     N = gy.size(0)
     k = N // _WGRAD_ROWS
     if k < 2 or gy.size(1) * x.size(1) < _WGRAD_MIN:
@@ -92,7 +102,12 @@ class _Linear(torch.autograd.Function):
     def backward(ctx, gy):
         x, w = ctx.saved_tensors
         gy = gy.contiguous()
-        gx = gy @ w if ctx.needs_input_grad[0] else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            # one output (sigma decoder's last layer): the K = 1 GEMM is an
+            # outer product; the broadcast multiply rounds the same exact
+            # fp32 products once, at write speed (hipBLASLt's K=1 tile: 2 TB/s)
+            gx = gy * w if w.size(0) == 1 else gy @ w
         gw = _wgrad(gy, x) if ctx.needs_input_grad[1] else None
         return gx, gw, None, None
 

@@ -105,3 +105,29 @@ def test_linear_wgrad_kernel_matches_fp32(N, M, K):
     assert err < 5e-5, err
     # deterministic
     assert torch.equal(out, _wgrad_hip(gy, x))
+
+
+@pytest.mark.parametrize("M", [1, 3])
+def test_wgrad_narrow_output_layer(M):
+    """_wgrad of a layer with fewer than 8 outputs (sigma decoder's last):
+    zero-padded onto the HIP kernel, against an fp64 GEMM."""
+    from avr_amd.model import _wgrad
+
+    g = torch.Generator(device=DEV).manual_seed(M)
+    gy = torch.randn(83200, M, device=DEV, generator=g).to(torch.bfloat16)
+    x = torch.randn(83200, 256, device=DEV, generator=g).to(torch.bfloat16)
+    out = _wgrad(gy, x)
+    assert out.shape == (M, 256) and out.dtype == torch.float32 and out.is_contiguous()
+    ref = gy.double().t() @ x.double()
+    err = float((out.double() - ref).norm() / ref.norm())
+    assert err < 5e-5, err
+
+
+def test_one_output_layer_dgrad_is_the_gemm():
+    """_Linear's data gradient for a 1-output layer (broadcast multiply)
+    equals the K = 1 GEMM it replaces, bit for bit, in bf16 and fp32."""
+    g = torch.Generator(device=DEV).manual_seed(5)
+    for dt in (torch.bfloat16, torch.float32):
+        gy = torch.randn(83200, 1, device=DEV, generator=g).to(dt)
+        w = torch.randn(1, 256, device=DEV, generator=g).to(dt)
+        assert torch.equal(gy * w, gy @ w)
