@@ -65,6 +65,17 @@ __device__ __forceinline__ void store_pair<__half>(__half* out, int64_t i, float
     *reinterpret_cast<__half2*>(out + 2 * i) = __floats2half2_rn(v.x, v.y);
 }
 
+// avr_hashgrid_fwd switches to the level-major dispatch from this many points
+// (AVR_HASHGRID_LM_MIN overrides; experiments)
+constexpr int64_t kLevelMajorMinPointsDefault = 16384;
+inline int64_t lm_min_points() {
+    static const int64_t v = [] {
+        const char* e = getenv("AVR_HASHGRID_LM_MIN");
+        return e ? (int64_t)atoll(e) : kLevelMajorMinPointsDefault;
+    }();
+    return v;
+}
+
 struct Corner {
     float pos[3];
     uint32_t grid[3];
@@ -124,7 +135,12 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(int64_t N, int L,
 // instead of all L tables (36 MiB for the MeshRIR position grid) streaming
 // from the Infinity Cache.  out is level-major [L][N][2] (coalesced stores);
 // consumers read feature pair l of point i at out[l*N + i].
-template <typename Tp, typename To>
+//
+// ROW_MAJOR: the same level-major dispatch writing the row-major [N][L][2]
+// output of hashgrid_fwd_kernel (avr_hashgrid_fwd for large N: training's
+// per-sample grids).  The 8-byte stores are strided, but they are 1/8 of the
+// gathered bytes; the gathers are what the L2-resident level saves.
+template <typename Tp, typename To, bool ROW_MAJOR = false>
 __global__ __launch_bounds__(256) void hashgrid_fwd_lm_kernel(int64_t N, const float* __restrict__ x,
                                                               const Tp* __restrict__ params,
                                                               LevelTable lt, To* __restrict__ out) {
@@ -155,7 +171,7 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_lm_kernel(int64_t N, const f
         acc.x = fmaf(wgt, v.x, acc.x);
         acc.y = fmaf(wgt, v.y, acc.y);
     }
-    store_pair(out, (int64_t)l * N + i, acc);
+    store_pair(out, ROW_MAJOR ? i * (int64_t)gridDim.y + l : (int64_t)l * N + i, acc);
 }
 
 // Backward: scatter-add of w_corner * dL/dy into the tables.
@@ -250,6 +266,26 @@ extern "C" int avr_hashgrid_fwd(int64_t N, int32_t n_levels, const float* x, con
     const dim3 grid((unsigned)((work + 255) / 256));
     hipStream_t st = as_stream(stream);
     const int L = n_levels;
+    // many points: level-major dispatch (one level's table L2-resident at a
+    // time), same values and output layout (tools/probe_hashgrid.py)
+    if (N >= lm_min_points()) {
+        const dim3 glm((unsigned)((N + 255) / 256), (unsigned)L);
+        if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F32)
+            hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<float, float, true>), glm, dim3(256), 0, st, N, x,
+                               (const float*)params, lt, (float*)out);
+        else if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F16)
+            hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<float, __half, true>), glm, dim3(256), 0, st, N, x,
+                               (const float*)params, lt, (__half*)out);
+        else if (param_dtype == AVR_DTYPE_F16 && out_dtype == AVR_DTYPE_F16)
+            hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<__half, __half, true>), glm, dim3(256), 0, st, N, x,
+                               (const __half*)params, lt, (__half*)out);
+        else if (param_dtype == AVR_DTYPE_F16 && out_dtype == AVR_DTYPE_F32)
+            hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<__half, float, true>), glm, dim3(256), 0, st, N, x,
+                               (const __half*)params, lt, (float*)out);
+        else
+            return fail(AVR_E_ARG, "avr_hashgrid_fwd: unknown dtype");
+        return check_launch("avr_hashgrid_fwd");
+    }
     if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F32)
         hipLaunchKernelGGL((hashgrid_fwd_kernel<float, float>), grid, dim3(256), 0, st, N, L, x,
                            (const float*)params, lt, (float*)out);
