@@ -18,7 +18,7 @@ step() {  # name, timeout, command...
 }
 for s in "$@"; do
   case $s in
-    tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchq) step bench_q 300 python bench.py --no-cpu-baseline --steps 100 ;;
@@ -48,7 +48,7 @@ for s in "$@"; do
     profcore) step profcore 600 rocprofv3 --kernel-trace --stats -d $OUT/profcore -o run --output-format csv -- python tools/bench_train.py --core-only --steps 20 ;;
     prof5) step prof5 600 rocprofv3 --kernel-trace --stats -d $OUT/prof5 -o run --output-format csv -- python bench.py --workload c5_simu_4096x512x2048 --no-cpu-baseline --steps 10 --warmup 2 --streams 1 --poses 4 ;;
     benchall) for wl in c1_meshrir_plumbing c3_raf_furnished_b4 c4_raf_empty_b4_per_gpu c5_simu_4096x512x2048; do step bench_$wl 300 python bench.py --workload $wl --no-cpu-baseline --steps 50 || exit 1; done ;;
-    prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline --streams 1 ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 3 --streams 1 && step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 20 --warmup 3 --streams 1 ;;
   esac
 done
