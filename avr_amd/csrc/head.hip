@@ -181,13 +181,6 @@ __device__ __forceinline__ void load_wpacked(Raw<Th, KB> (&v)[NT], const Th* __r
         v[i].load(Wp + ((int64_t)(k0 / KB) * T + min((int)threadIdx.x + kThreads * i, T - 1)) * KB);
 }
 
-template <typename Th, int KB, int NT>
-__device__ __forceinline__ void load_wrows(Raw<Th, KB> (&v)[NT], const Th* __restrict__ W, int K, int k0,
-                                           int T) {
-#pragma unroll
-    for (int i = 0; i < NT; ++i) v[i].load(W + (int64_t)min((int)threadIdx.x + kThreads * i, T - 1) * K + k0);
-}
-
 // Runs of equal keys over the lanes of a wavefront (consecutive rays have
 // slowly changing delays): the run's first lane, last lane and whether this
 // lane ends its run.
