@@ -238,6 +238,43 @@ def test_config2_full_size_properties():
     assert rel_l2(s, base) < 1e-5
 
 
+def test_config5_full_size_properties():
+    """Config 5 at full size (4096 rays x 512 samples x T=4094, fp16 storage,
+    17.2 GB of signal): exact linearity (doubling fp16 inputs doubles every
+    product and sum exactly), additivity over 4 ray shards (the multi-GPU
+    decomposition), finite IR.  Golden parity at T=4094 is c5small's."""
+    from avr_amd.parallel import shard_range
+
+    w = WORKLOADS["c5_simu_4096x512x2048"]
+    B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
+    g = torch.Generator(device=DEV).manual_seed(5)
+    attn = (torch.rand(B, R * S, 1, device=DEV, generator=g) * 2).to(torch.float16)
+    sig = torch.randn(B, R * S, T, device=DEV, generator=g, dtype=torch.float16) * 0.1
+    ro = torch.rand(B, 3, device=DEV, generator=g) * 4 - 2
+    tx = torch.rand(B, 3, device=DEV, generator=g) * 4 - 2
+    r = AVRRender(Net(attn, sig), **w.render)
+    with torch.no_grad():
+        torch.manual_seed(0)
+        out, ir = r.render_ir(ro, tx)
+        assert torch.isfinite(out).all() and torch.isfinite(ir).all() and float(out.abs().max()) > 0
+        sig.mul_(2)
+        torch.manual_seed(0)
+        out2 = r(ro, tx)
+        sig.mul_(0.5)
+        torch.testing.assert_close(out2, 2 * out, rtol=0, atol=1e-7 * float(out.abs().max()))
+        total = None
+        for k in range(4):
+            r0, r1 = shard_range(R, k, 4)
+            rk = AVRRender(Net(attn[:, r0 * S:r1 * S], sig[:, r0 * S:r1 * S]), **w.render)
+            rk.ray_range = (r0, r1)
+            torch.manual_seed(0)
+            part = rk(ro, tx)
+            total = part if total is None else total + part
+    assert rel_l2(total.cpu().numpy(), out.cpu().numpy()) < 1e-5
+    del sig, attn
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("n_shards", [2, 3])
 def test_ray_range_shards_sum_to_full(n_shards):
     """Rays split into contiguous ranges (the multi-GPU ray sharding) sum to
