@@ -104,6 +104,7 @@ _SIGS = {
     "avr_sample_rays": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32] + [_vp] * 9),
     "avr_weights_fwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32] + [_vp] * 7),
     "avr_ray_reduce_fwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32, _vp, _vp, _c_i32, _vp, _vp]),
+    "avr_sample_rays_dev": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32] + [_vp] * 9),
     "avr_reduce_splits": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp]),
     "avr_dft_phase_fwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32, _vp, _vp, _vp, _vp, _c_i32, _vp, _vp]),
     "avr_spectrum_finalize": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _vp, _vp, _vp]),

@@ -151,10 +151,10 @@ struct AziJitter {
 constexpr int kSampleThreads = 256;
 
 __global__ __launch_bounds__(kSampleThreads) void sample_rays_kernel(
-    avr_render_params p, int B, AziJitter jit, int r_begin, const float* __restrict__ rays_o,
-    const float* __restrict__ pos_tx, const float* __restrict__ dir_tx, float* __restrict__ dirs,
-    float* __restrict__ net_pts, float* __restrict__ net_view, float* __restrict__ net_tx,
-    float* __restrict__ net_dir_tx) {
+    avr_render_params p, int B, AziJitter jit, const float* __restrict__ jit_dev, int r_begin,
+    const float* __restrict__ rays_o, const float* __restrict__ pos_tx, const float* __restrict__ dir_tx,
+    float* __restrict__ dirs, float* __restrict__ net_pts, float* __restrict__ net_view,
+    float* __restrict__ net_tx, float* __restrict__ net_dir_tx) {
     // directions of the (at most 256/S + 2) rays this block touches, once each
     __shared__ float sdir[kSampleThreads + 1][3];
     const int R = n_rays(p), S = p.n_samples;
@@ -164,7 +164,8 @@ __global__ __launch_bounds__(kSampleThreads) void sample_rays_kernel(
     const int64_t br1 = (min(n, i0 + kSampleThreads) - 1) / S;
     for (int k = threadIdx.x; k <= (int)(br1 - br0); k += kSampleThreads) {
         const int r = r_begin + (int)((br0 + k) % R);
-        ray_direction(p, r < p.n_azi * p.n_ele ? jit.u[r / p.n_ele] : 0.0f, r, sdir[k]);
+        const float u = r < p.n_azi * p.n_ele ? (jit_dev ? jit_dev[r / p.n_ele] : jit.u[r / p.n_ele]) : 0.0f;
+        ray_direction(p, u, r, sdir[k]);
     }
     __syncthreads();
     // stage the block's 256 x 3 outputs per tensor in LDS, then write them
@@ -769,9 +770,30 @@ extern "C" int avr_sample_rays(const avr_render_params* p, int32_t B, const floa
     const int64_t n = (int64_t)B * n_rays(*p) * p->n_samples;
     hipLaunchKernelGGL(sample_rays_kernel, dim3((unsigned)((n + kSampleThreads - 1) / kSampleThreads)),
                        dim3(kSampleThreads), 0,
-                       as_stream(stream), *p, (int)B, jit, (int)ray_begin, rays_o, pos_tx, dir_tx,
-                       dirs, net_pts, net_view, net_tx, dir_tx ? net_dir_tx : nullptr);
+                       as_stream(stream), *p, (int)B, jit, (const float*)nullptr, (int)ray_begin, rays_o,
+                       pos_tx, dir_tx, dirs, net_pts, net_view, net_tx, dir_tx ? net_dir_tx : nullptr);
     return check_launch("avr_sample_rays");
+}
+
+// Same launch with the jitter read from DEVICE memory when the kernel runs
+// (graph replay: avr_amd.graph.GraphedRender refreshes the buffer per pose).
+extern "C" int avr_sample_rays_dev(const avr_render_params* p, int32_t B, const float* u_azi_dev,
+                                   int32_t ray_begin, const float* rays_o, const float* pos_tx,
+                                   const float* dir_tx, float* dirs, float* net_pts, float* net_view,
+                                   float* net_tx, float* net_dir_tx, void* stream) {
+    if (int e = validate(p)) return e;
+    AVR_REQUIRE(B >= 1 && u_azi_dev && rays_o && pos_tx && dirs && net_pts && net_view && net_tx,
+                "avr_sample_rays_dev: bad args");
+    AVR_REQUIRE(!dir_tx || net_dir_tx, "avr_sample_rays_dev: dir_tx given without net_dir_tx");
+    AVR_REQUIRE(ray_begin >= 0 && ray_begin + p->n_rays <= grid_rays(*p),
+                "avr_sample_rays_dev: ray range outside the sphere");
+    AziJitter jit{};
+    const int64_t n = (int64_t)B * n_rays(*p) * p->n_samples;
+    hipLaunchKernelGGL(sample_rays_kernel, dim3((unsigned)((n + kSampleThreads - 1) / kSampleThreads)),
+                       dim3(kSampleThreads), 0,
+                       as_stream(stream), *p, (int)B, jit, u_azi_dev, (int)ray_begin, rays_o, pos_tx, dir_tx,
+                       dirs, net_pts, net_view, net_tx, dir_tx ? net_dir_tx : nullptr);
+    return check_launch("avr_sample_rays_dev");
 }
 
 extern "C" int avr_weights_fwd(const avr_render_params* p, int32_t B, const void* attn,

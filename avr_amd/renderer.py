@@ -431,6 +431,7 @@ class AVRRender(nn.Module):
         # network offers it (avr_amd.model networks; FusedHeadCore)
         self.fused_head = bool(kwargs.get("fused_head", True))
         self._pcache = {}
+        self._jitter_dev = None  # device jitter buffer while a HIP graph is captured (avr_amd.graph)
 
     # -- stages, exposed for tests and for callers that bring their own network
     def _device(self, rays_o):
@@ -451,7 +452,8 @@ class AVRRender(nn.Module):
         """
         dev = self._device(rays_o)
         B = position_tx.size(0)
-        if u_azi is None:
+        u_dev = self._jitter_dev if u_azi is None else None
+        if u_azi is None and u_dev is None:
             u_azi = draw_jitter(self.n_azi, self.n_ele)
         R_all = int(self.n_azi) * int(self.n_ele) + 2
         r0, r1 = self.ray_range if self.ray_range is not None else (0, R_all)
@@ -471,7 +473,13 @@ class AVRRender(nn.Module):
         tx = torch.empty(B, R * S, 3, **f32)
         dtx = torch.empty(B, R * S, 3, **f32) if direction_tx is not None else None
         with _on(dev):
-            if p0.n_azi <= _lib.MAX_AZI:
+            if u_dev is not None:
+                # graph capture: the jitter is read from device memory at replay
+                dirs = torch.empty(R, 3, **f32)
+                _lib.call("avr_sample_rays_dev", pref, B, _ptr(u_dev), r0, _ptr(rays_o),
+                          _ptr(position_tx), _ptr(direction_tx), _ptr(dirs), _ptr(pts), _ptr(view),
+                          _ptr(tx), _ptr(dtx), st)
+            elif p0.n_azi <= _lib.MAX_AZI:
                 # one fused launch; the jitter travels in the kernel arguments
                 u_host = np.ascontiguousarray(u_azi.detach().cpu().numpy(), dtype=np.float32)
                 dirs = torch.empty(R, 3, **f32)

@@ -112,6 +112,12 @@ int avr_sample_rays(const avr_render_params* p, int32_t B, const float* u_azi_ho
                     int32_t ray_begin, const float* rays_o, const float* pos_tx,
                     const float* dir_tx, float* dirs, float* net_pts, float* net_view,
                     float* net_tx, float* net_dir_tx, void* stream);
+/* The same with u_azi_dev a DEVICE pointer to the n_azi jitter draws, read
+ * when the kernel runs (HIP-graph replay; any n_azi). */
+int avr_sample_rays_dev(const avr_render_params* p, int32_t B, const float* u_azi_dev,
+                        int32_t ray_begin, const float* rays_o, const float* pos_tx,
+                        const float* dir_tx, float* dirs, float* net_pts, float* net_view,
+                        float* net_tx, float* net_dir_tx, void* stream);
 
 /* ---- a8 + a11: source delays and compositing weights -------------------
  * attn [B][R*S] (dtype), writes w[B][R][S] fp32 and delay[B][R][S] int32.
