@@ -96,28 +96,52 @@ __device__ __forceinline__ void store_block(Th* p, const float* v) {
     }
 }
 
-// In-place inclusive prefix (or suffix) sums of the KB rows of A[KB][T]:
-// 256/KB threads per row, each a contiguous segment, segment totals combined
-// by a shuffle scan inside the row's lanes (a row's threads share a wave).
+// Row stride of Q[KB][qs] in head_bwd_h: T rounded up to 4 floats, so every
+// thread's scan segment starts 16-byte aligned.
+__host__ __device__ constexpr int q_stride(int T) { return (T + 3) / 4 * 4; }
+
+// In-place inclusive prefix (or suffix) sums of the KB rows of A[KB][qs]:
+// 256/KB threads per row, each a contiguous segment of a multiple of 4
+// floats read and written as 16-byte vectors (lanes 4*seg4/4 words apart:
+// distinct bank quads, conflict-free), segment totals combined by a shuffle
+// scan inside the row's lanes (a row's threads share a wave).
 template <int KB, bool SUFFIX>
 __device__ __forceinline__ void scan_rows(float* A, int T) {
     constexpr int TPR = kThreads / KB;  // 16, 32 or 64 (<= one wave)
     const int row = threadIdx.x / TPR, j = threadIdx.x % TPR;
-    const int seg = (T + TPR - 1) / TPR;
-    float* a = A + row * T;
-    const int lo = j * seg, hi = min(T, lo + seg);
+    const int seg = ((T + TPR - 1) / TPR + 3) / 4 * 4;
+    float* a = A + row * q_stride(T);
+    const int lo = min(T, j * seg), hi = min(T, lo + seg);
+    const int nfull = (hi - lo) / 4;  // whole 16-byte chunks; the tail (< 4) only in the last segment
+    f32x4* a4 = reinterpret_cast<f32x4*>(a + lo);
     float run = 0.0f;
     if (!SUFFIX) {
-#pragma unroll 8
-        for (int t = lo; t < hi; ++t) {
+        for (int c = 0; c < nfull; ++c) {
+            f32x4 v = a4[c];
+            v[0] += run;
+            v[1] += v[0];
+            v[2] += v[1];
+            v[3] += v[2];
+            run = v[3];
+            a4[c] = v;
+        }
+        for (int t = lo + 4 * nfull; t < hi; ++t) {
             run += a[t];
             a[t] = run;
         }
     } else {
-#pragma unroll 8
-        for (int t = hi - 1; t >= lo; --t) {
+        for (int t = hi - 1; t >= lo + 4 * nfull; --t) {
             run += a[t];
             a[t] = run;
+        }
+        for (int c = nfull - 1; c >= 0; --c) {
+            f32x4 v = a4[c];
+            v[3] += run;
+            v[2] += v[3];
+            v[1] += v[2];
+            v[0] += v[1];
+            run = v[0];
+            a4[c] = v;
         }
     }
     // exclusive scan of the segment totals over the TPR lanes of this row
@@ -141,8 +165,15 @@ __device__ __forceinline__ void scan_rows(float* A, int T) {
         if (j == TPR - 1) off = 0.0f;
     }
     if (off != 0.0f) {
-#pragma unroll 8
-        for (int t = lo; t < hi; ++t) a[t] += off;
+        for (int c = 0; c < nfull; ++c) {
+            f32x4 v = a4[c];
+            v[0] += off;
+            v[1] += off;
+            v[2] += off;
+            v[3] += off;
+            a4[c] = v;
+        }
+        for (int t = lo + 4 * nfull; t < hi; ++t) a[t] += off;
     }
 }
 
@@ -538,8 +569,9 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
                                                               const float* __restrict__ gz,
                                                               Th* __restrict__ grad_h,
                                                               float* __restrict__ gw_part) {
-    extern __shared__ float Q[];  // [KB][T]
+    extern __shared__ float Q[];  // [KB][QS]
     const int T = pp.T, S = pp.n_samples;
+    const int QS = q_stride(T);
     const int kg = blockIdx.x, s = blockIdx.y, b = blockIdx.z;
     const int lim = tail_limit(pp, s);
     const int64_t hrow0 = ((int64_t)b * R * S + s) * K;
@@ -569,7 +601,7 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
             const int t = threadIdx.x + kThreads * i;
             if (t < T)
 #pragma unroll
-                for (int k = 0; k < KB; ++k) Q[k * T + t] = g[i] * wt[i][k];
+                for (int k = 0; k < KB; ++k) Q[k * QS + t] = g[i] * wt[i][k];
         }
         if (k0 + KB < kend) load_wpacked<Th, KB, NT>(wt, W, k0 + KB, T);
         lds_barrier();
@@ -586,7 +618,7 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
                     float acc = gw[u];
 #pragma unroll
                     for (int k = 0; k < KB; ++k) {
-                        const float q = Q[k * T + d];
+                        const float q = Q[k * QS + d];
                         gh[k] = wr * q;
                         acc = fmaf(hv[u][k], q, acc);
                     }
@@ -708,7 +740,7 @@ struct HeadShape {
     int kb;             // features per block (4, 8 or 16)
     int n_kg;           // forward feature groups = DFT partials (power of two <= 16)
     int kg;             // features per group
-    size_t lds_q;       // head_bwd_h: Q[kb][T]
+    size_t lds_q;       // head_bwd_h: Q[kb][q_stride(T)]
     size_t lds_c;       // head_fwd / head_bwd_w: C[kb][R+1]
     size_t lds_sort;    // head_sort: cnt[T], perm[R], ws[R]
 };
@@ -721,9 +753,10 @@ int head_shape(const avr_render_params& p, int B, int R, int K, int es, HeadShap
     // feature block: prefetched W rows in registers (kb*nt <= 64), and the
     // backward's Q[kb][T] in <= 80 KiB of LDS (two workgroups per CU)
     int kb = 16;
-    while (kb > 4 && ((size_t)kb * T * 4 > 80 * 1024 || kb * nt > 64)) kb /= 2;
+    while (kb > 4 && ((size_t)kb * q_stride(T) * 4 > 80 * 1024 || kb * nt > 64)) kb /= 2;
     const size_t lds_sort = 4 * ((size_t)T + 2 * (size_t)R + 4);
-    if ((size_t)kb * T * 4 > 150 * 1024 || cumsum_lds_bytes(R, kb) > 150 * 1024 || lds_sort > 150 * 1024)
+    if ((size_t)kb * q_stride(T) * 4 > 150 * 1024 || cumsum_lds_bytes(R, kb) > 150 * 1024 ||
+        lds_sort > 150 * 1024)
         return fail(AVR_E_CONFIG, "fused head: T x rays too large for LDS");
     if (K % kb != 0 || (kb * es) % 8 != 0)
         return fail(AVR_E_CONFIG, "fused head: hidden width must be a multiple of the feature block");
@@ -735,7 +768,7 @@ int head_shape(const avr_render_params& p, int B, int R, int K, int es, HeadShap
     hs->kb = kb;
     hs->n_kg = n;
     hs->kg = K / n;
-    hs->lds_q = (size_t)kb * T * 4;
+    hs->lds_q = (size_t)kb * q_stride(T) * 4;
     hs->lds_c = cumsum_lds_bytes(R, kb);
     hs->lds_sort = lds_sort;
     return 0;
