@@ -560,7 +560,10 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp
 }
 
 // ------------------------------------------------- backward: dL/dh, dL/dw
-template <typename Th, int KB, int NT, int RPT>
+// SB > 1 (bf16): each ray's h is loaded and its grad_h stored SB feature
+// blocks at a time (32 bytes per row for SB = 2) instead of 16 bytes per
+// block; the grad_h of the SB blocks waits packed in registers.
+template <typename Th, int KB, int NT, int RPT, int SB = 1>
 __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params pp, int B, int R, int K,
                                                               int KG, const Th* __restrict__ h,
                                                               const Th* __restrict__ W,
@@ -587,15 +590,14 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
         const float v = gzr[min(t, T - 1)];
         g[i] = t < lim ? v : 0.0f;
     }
-    Raw<Th, KB> hv[RPT], wt[NT];
+    Raw<Th, KB> wt[NT];
     load_wpacked<Th, KB, NT>(wt, W, kbeg, T);  // W packed [K/KB][T][KB] by avr_head_bwd
-    load_rows<Th, KB, RPT>(hv, h, hrow0, hstride, kbeg, R);
     float gw[RPT];
 #pragma unroll
     for (int u = 0; u < RPT; ++u) gw[u] = 0.0f;
-    for (int k0 = kbeg; k0 < kend; k0 += KB) {
+    // Q[k][t] = suffix sum over t of gz[t] W[t][k] for feature block kk
+    auto build_q = [&](int kk) {
         lds_barrier();
-        // u[k][t] = gz[t] W[t][k], then the suffix sum over t
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
             const int t = threadIdx.x + kThreads * i;
@@ -603,34 +605,83 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
 #pragma unroll
                 for (int k = 0; k < KB; ++k) Q[k * QS + t] = g[i] * wt[i][k];
         }
-        if (k0 + KB < kend) load_wpacked<Th, KB, NT>(wt, W, k0 + KB, T);
+        if (kk + KB < kend) load_wpacked<Th, KB, NT>(wt, W, kk + KB, T);
         lds_barrier();
         scan_rows<KB, true>(Q, T);
         lds_barrier();
+    };
+    if constexpr (SB == 1) {
+        Raw<Th, KB> hv[RPT];
+        load_rows<Th, KB, RPT>(hv, h, hrow0, hstride, kbeg, R);
+        for (int k0 = kbeg; k0 < kend; k0 += KB) {
+            build_q(k0);
 #pragma unroll
-        for (int u = 0; u < RPT; ++u) {
-            const int r = threadIdx.x + kThreads * u;
-            if (r < R) {
-                const int d = rays.d[u];
-                float gh[KB];
-                if (d < lim) {
+            for (int u = 0; u < RPT; ++u) {
+                const int r = threadIdx.x + kThreads * u;
+                if (r < R) {
+                    const int d = rays.d[u];
+                    float gh[KB];
+                    if (d < lim) {
+                        const float wr = rays.w[u];
+                        float acc = gw[u];
+#pragma unroll
+                        for (int k = 0; k < KB; ++k) {
+                            const float q = Q[k * QS + d];
+                            gh[k] = wr * q;
+                            acc = fmaf(hv[u][k], q, acc);
+                        }
+                        gw[u] = acc;
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < KB; ++k) gh[k] = 0.0f;
+                    }
+                    store_block<Th, KB>(grad_h + hrow0 + (int64_t)r * hstride + k0, gh);
+                }
+            }
+            if (k0 + KB < kend) load_rows<Th, KB, RPT>(hv, h, hrow0, hstride, k0 + KB, R);
+        }
+    } else {
+        static_assert(sizeof(Th) == 2, "super-blocks are for 16-bit h");
+        constexpr int NDW = KB * SB / 2;  // dwords of SB blocks of one row
+        Raw<Th, KB * SB> hv[RPT];
+        load_rows<Th, KB * SB, RPT>(hv, h, hrow0, hstride, kbeg, R);
+        for (int k0 = kbeg; k0 < kend; k0 += KB * SB) {
+            uint32_t ghp[RPT][NDW];
+#pragma unroll
+            for (int sb = 0; sb < SB; ++sb) {
+                build_q(k0 + sb * KB);
+#pragma unroll
+                for (int u = 0; u < RPT; ++u) {
+                    const int d = rays.d[u];
+                    const bool live = d < lim && (int)threadIdx.x + kThreads * u < R;
                     const float wr = rays.w[u];
                     float acc = gw[u];
 #pragma unroll
-                    for (int k = 0; k < KB; ++k) {
-                        const float q = Q[k * QS + d];
-                        gh[k] = wr * q;
-                        acc = fmaf(hv[u][k], q, acc);
+                    for (int k = 0; k < KB; k += 2) {
+                        const float q0 = live ? Q[k * QS + d] : 0.0f;
+                        const float q1 = live ? Q[(k + 1) * QS + d] : 0.0f;
+                        acc = fmaf(hv[u][sb * KB + k], q0, acc);
+                        acc = fmaf(hv[u][sb * KB + k + 1], q1, acc);
+                        const __hip_bfloat16 a0 = __float2bfloat16(live ? wr * q0 : 0.0f);
+                        const __hip_bfloat16 a1 = __float2bfloat16(live ? wr * q1 : 0.0f);
+                        ghp[u][sb * KB / 2 + k / 2] = (uint32_t)(*reinterpret_cast<const uint16_t*>(&a0)) |
+                                                      ((uint32_t)(*reinterpret_cast<const uint16_t*>(&a1)) << 16);
                     }
-                    gw[u] = acc;
-                } else {
-#pragma unroll
-                    for (int k = 0; k < KB; ++k) gh[k] = 0.0f;
+                    if (live) gw[u] = acc;
                 }
-                store_block<Th, KB>(grad_h + hrow0 + (int64_t)r * hstride + k0, gh);
             }
+#pragma unroll
+            for (int u = 0; u < RPT; ++u) {
+                const int r = threadIdx.x + kThreads * u;
+                if (r < R) {
+                    u32x4* dst = reinterpret_cast<u32x4*>(grad_h + hrow0 + (int64_t)r * hstride + k0);
+#pragma unroll
+                    for (int c = 0; c < NDW / 4; ++c)
+                        dst[c] = u32x4{ghp[u][4 * c], ghp[u][4 * c + 1], ghp[u][4 * c + 2], ghp[u][4 * c + 3]};
+                }
+            }
+            if (k0 + KB * SB < kend) load_rows<Th, KB * SB, RPT>(hv, h, hrow0, hstride, k0 + KB * SB, R);
         }
-        if (k0 + KB < kend) load_rows<Th, KB, RPT>(hv, h, hrow0, hstride, k0 + KB, R);
     }
 #pragma unroll
     for (int u = 0; u < RPT; ++u) {
@@ -967,6 +1018,10 @@ extern "C" int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, co
             hipLaunchKernelGGL(head_pack_w_kernel<float>, dim3(blocks), dim3(kThreads), 0, st, T, (int)K, hs.kb,
                                (const float*)W, (float*)Wb);
     }
+    // 16-bit h: h loads / grad_h stores 2 feature blocks (32 B) per row
+    // (AVR_HEAD_BSB=1 restores one block; experiments)
+    int bsb = (dtype == AVR_DTYPE_BF16 && hs.kg % (2 * hs.kb) == 0) ? 2 : 1;
+    if (const char* e = getenv("AVR_HEAD_BSB")) bsb = (atoi(e) == 2 && hs.kg % (2 * hs.kb) == 0) ? 2 : 1;
     auto go_h = [&](auto kern, auto hp, auto wp, auto gp) {
         allow_lds(kern, hs.lds_q);
         hipLaunchKernelGGL(kern, dim3(hs.n_kg, S, B), dim3(kThreads), hs.lds_q, st, *p, (int)B, R, (int)K,
@@ -979,7 +1034,14 @@ extern "C" int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, co
     };
 #define AVR_HB(TH, KBV, NTV, RP)                                                                   \
     if (hs.kb == KBV && hs.nt == NTV && hs.rpt == RP) {                                            \
-        go_h(head_bwd_h_kernel<TH, KBV, NTV, RP>, (const TH*)h, (const TH*)Wb, (TH*)grad_h);       \
+        if constexpr (sizeof(TH) == 2 && RP <= 8) {                                                \
+            if (bsb == 2)                                                                           \
+                go_h(head_bwd_h_kernel<TH, KBV, NTV, RP, 2>, (const TH*)h, (const TH*)Wb, (TH*)grad_h); \
+            else                                                                                    \
+                go_h(head_bwd_h_kernel<TH, KBV, NTV, RP, 1>, (const TH*)h, (const TH*)Wb, (TH*)grad_h); \
+        } else {                                                                                    \
+            go_h(head_bwd_h_kernel<TH, KBV, NTV, RP, 1>, (const TH*)h, (const TH*)Wb, (TH*)grad_h);   \
+        }                                                                                           \
         go_w(head_bwd_w_kernel<TH, KBV, NTV, RP>, (const TH*)h);                                   \
     }
 #define AVR_HB_R(TH, KBV, NTV) AVR_HB(TH, KBV, NTV, 4) AVR_HB(TH, KBV, NTV, 8) AVR_HB(TH, KBV, NTV, 16)
