@@ -26,11 +26,12 @@ def _points(n, seed):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
-def test_forward_matches_restatement(dtype):
+@pytest.mark.parametrize("n", [4096, 20000])  # 20000: the level-major dispatch (>= 16384 points)
+def test_forward_matches_restatement(dtype, n):
     enc = HashGridEncoding(3, CFG, dtype=dtype, seed=5).to(DEV)
     with torch.no_grad():
         enc.params.uniform_(-1, 1)
-    x = _points(4096, 0)
+    x = _points(n, 0)
     out = enc(torch.from_numpy(x).to(DEV)).detach().float().cpu().numpy()
     # fp16 encodings read fp16 tables (tcnn's param precision), fp32 ones fp32
     table = enc.params.detach().to(enc.param_dtype).float().cpu().numpy()
@@ -67,7 +68,7 @@ def test_level_major_forward_is_transposed_forward(dtype):
     enc = HashGridEncoding(3, CFG, dtype=dtype, seed=7).to(DEV)
     with torch.no_grad():
         enc.params.uniform_(-1, 1)
-        for n in (8, 255, 4097):
+        for n in (8, 255, 4097, 16384, 20001):
             x = torch.from_numpy(_points(n, 1)).to(DEV)
             a = enc(x)
             b = enc.forward_level_major(x)

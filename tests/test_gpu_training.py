@@ -165,3 +165,25 @@ def test_native_adam_invalidates_inference_caches():
         c1 = cast_weight(p, torch.bfloat16, True)
     torch.testing.assert_close(c1, p.detach().to(torch.bfloat16), rtol=0, atol=0)
     assert not torch.equal(c1, c0)
+
+
+@pytest.mark.gpu
+def test_native_adam_many_tensors_and_empty():
+    """More tensors than one kernel-argument table holds (32), an empty one,
+    odd sizes (scalar tail), against clip_and_sanitize_ + torch Adam."""
+    from avr_amd.training import clip_sanitize_adam_
+    g = torch.Generator(device=DEV).manual_seed(9)
+    shapes = [(0,)] + [(37 + 5 * k,) for k in range(40)] + [(3, 7)]
+    ref = [torch.randn(s, device=DEV, generator=g).requires_grad_(True) for s in shapes]
+    mine = [p.detach().clone().requires_grad_(True) for p in ref]
+    o_ref = torch.optim.Adam(ref, lr=3e-3)
+    o_mine = torch.optim.Adam(mine, lr=3e-3)
+    for _ in range(3):
+        for a, b in zip(ref, mine):
+            gr = torch.randn(a.shape, device=DEV, generator=g)
+            a.grad, b.grad = gr.clone(), gr.clone()
+        clip_and_sanitize_(ref, max_norm=1)
+        o_ref.step()
+        clip_sanitize_adam_(o_mine, max_norm=1)
+    for a, b in zip(ref, mine):
+        torch.testing.assert_close(b.detach(), a.detach(), rtol=2e-6, atol=2e-7)
