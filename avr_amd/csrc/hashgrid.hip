@@ -352,3 +352,132 @@ extern "C" int avr_hashgrid_fwd_lm(int64_t N, int32_t n_levels, const float* x, 
         return fail(AVR_E_ARG, "avr_hashgrid_fwd_lm: unknown dtype");
     return check_launch("avr_hashgrid_fwd_lm");
 }
+
+// ----------------------------------------------------------------------------
+// Per-ray / per-pose first-layer bias of AVRModel's signal network at
+// inference (avr_amd/model.py _trunk_fused_h1): for every ray of every pose
+//
+//   e_dir = bf16(enc_dtype(dir_grid((view[b, r*S] + 1) / 2)))     [2*Ld]
+//   e_tx  = bf16(enc_dtype(tx_grid((tx[b, 0] + 1) / 2)))           [2*Lt]
+//   bias[b*R + r][o] = sum_k e_dir[k] w_dir[k][o] + sum_k e_tx[k] w_tx[k][o]
+//
+// (the view direction repeats over a ray's samples and tx over a pose's,
+// model.py:221 concatenates both to every sample).  One launch instead of
+// the ~12 small torch kernels of the same arithmetic: the row selection, the
+// [0, 1] map, two small grids, the fp16 -> bf16 -> fp32 casts, two skinny
+// GEMMs and their sum.  Each workgroup does kBiasRays rays: encodings into
+// LDS, then each thread walks k for its outputs with the rays' sums in
+// registers (k ascending: a fixed order).
+namespace {
+
+constexpr int kBiasRays = 16;
+
+template <typename Tp>
+__device__ __forceinline__ float2 encode_point_level(const float* xi, const Tp* params, const LevelTable& lt, int l) {
+    const Corner c = locate(xi, lt.scale[l]);
+    const uint32_t size = (uint32_t)(lt.offset[l + 1] - lt.offset[l]);
+    const uint32_t res = lt.res[l];
+    const Tp* table = params + 2 * lt.offset[l];
+    float2 acc = make_float2(0.0f, 0.0f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        float wgt = 1.0f;
+        uint32_t g[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            if (k & (1 << d)) {
+                wgt *= c.pos[d];
+                g[d] = c.grid[d] + 1;
+            } else {
+                wgt *= 1.0f - c.pos[d];
+                g[d] = c.grid[d];
+            }
+        }
+        const float2 v = load_pair(table, grid_index(size, res, g[0], g[1], g[2]));
+        acc.x = fmaf(wgt, v.x, acc.x);
+        acc.y = fmaf(wgt, v.y, acc.y);
+    }
+    return acc;
+}
+
+__device__ __forceinline__ float round_feature(float v, bool f16) {
+    if (f16) v = __half2float(__float2half(v));          // the encoding's output dtype
+    return __bfloat162float(__float2bfloat16(v));         // the MLP's bf16 input
+}
+
+template <typename Tp>
+__global__ __launch_bounds__(256) void ray_pose_bias_kernel(int B, int R, int S, const float* __restrict__ view,
+                                                            const float* __restrict__ tx, const Tp* __restrict__ dp,
+                                                            LevelTable dl, int dL, const Tp* __restrict__ tp,
+                                                            LevelTable tl, int tL, int f16,
+                                                            const float* __restrict__ wd,
+                                                            const float* __restrict__ wt, int nout,
+                                                            float* __restrict__ bias) {
+    __shared__ float e[kBiasRays][2][2 * kMaxLevels];
+    const int64_t g0 = (int64_t)blockIdx.x * kBiasRays;
+    const int nr = (int)min((int64_t)kBiasRays, (int64_t)B * R - g0);
+    for (int q = threadIdx.x; q < kBiasRays * 2 * kMaxLevels; q += 256) {
+        const int j = q / (2 * kMaxLevels), rem = q % (2 * kMaxLevels);
+        const int which = rem / kMaxLevels, l = rem % kMaxLevels;
+        if (j >= nr || l >= (which ? tL : dL)) continue;
+        const int64_t gr = g0 + j;
+        const int64_t b = gr / R, r = gr % R;
+        const float* src = which ? tx + b * R * S * 3 : view + (b * R * S + r * S) * 3;
+        const float xi[3] = {(src[0] + 1.0f) / 2.0f, (src[1] + 1.0f) / 2.0f, (src[2] + 1.0f) / 2.0f};
+        const float2 v = which ? encode_point_level(xi, tp, tl, l) : encode_point_level(xi, dp, dl, l);
+        e[j][which][2 * l] = round_feature(v.x, f16);
+        e[j][which][2 * l + 1] = round_feature(v.y, f16);
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < nout; o += 256) {
+        float sd[kBiasRays], st[kBiasRays];
+#pragma unroll
+        for (int j = 0; j < kBiasRays; ++j) sd[j] = st[j] = 0.0f;
+        for (int k = 0; k < 2 * dL; ++k) {
+            const float w = wd[(int64_t)k * nout + o];
+#pragma unroll
+            for (int j = 0; j < kBiasRays; ++j) sd[j] = fmaf(e[j][0][k], w, sd[j]);
+        }
+        for (int k = 0; k < 2 * tL; ++k) {
+            const float w = wt[(int64_t)k * nout + o];
+#pragma unroll
+            for (int j = 0; j < kBiasRays; ++j) st[j] = fmaf(e[j][1][k], w, st[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < kBiasRays; ++j)
+            if (j < nr) bias[(g0 + j) * nout + o] = sd[j] + st[j];
+    }
+}
+
+}  // namespace
+
+extern "C" int avr_ray_pose_bias(int32_t B, int32_t R, int32_t S, const float* view, const float* tx,
+                                 int32_t dir_levels, const void* dir_params, const int64_t* dir_offset,
+                                 const float* dir_scale, const int32_t* dir_res, int32_t tx_levels,
+                                 const void* tx_params, const int64_t* tx_offset, const float* tx_scale,
+                                 const int32_t* tx_res, int32_t param_dtype, int32_t enc_dtype,
+                                 const float* w_dir, const float* w_tx, int32_t n_out, float* bias,
+                                 void* stream) {
+    AVR_REQUIRE(B >= 1 && R >= 1 && S >= 1 && view && tx && dir_params && tx_params && w_dir && w_tx && bias &&
+                    n_out >= 1,
+                "avr_ray_pose_bias: bad args");
+    AVR_REQUIRE(enc_dtype == AVR_DTYPE_F16 || enc_dtype == AVR_DTYPE_F32, "avr_ray_pose_bias: enc dtype");
+    LevelTable dl, tl;
+    if (int e = make_table(dir_levels, dir_offset, dir_scale, dir_res, &dl)) return e;
+    if (int e = make_table(tx_levels, tx_offset, tx_scale, tx_res, &tl)) return e;
+    const int64_t rays = (int64_t)B * R;
+    const dim3 grid((unsigned)((rays + kBiasRays - 1) / kBiasRays));
+    const int f16 = enc_dtype == AVR_DTYPE_F16;
+    hipStream_t st = as_stream(stream);
+    if (param_dtype == AVR_DTYPE_F16)
+        hipLaunchKernelGGL(ray_pose_bias_kernel<__half>, grid, dim3(256), 0, st, (int)B, (int)R, (int)S, view, tx,
+                           (const __half*)dir_params, dl, (int)dir_levels, (const __half*)tx_params, tl,
+                           (int)tx_levels, f16, w_dir, w_tx, (int)n_out, bias);
+    else if (param_dtype == AVR_DTYPE_F32)
+        hipLaunchKernelGGL(ray_pose_bias_kernel<float>, grid, dim3(256), 0, st, (int)B, (int)R, (int)S, view, tx,
+                           (const float*)dir_params, dl, (int)dir_levels, (const float*)tx_params, tl,
+                           (int)tx_levels, f16, w_dir, w_tx, (int)n_out, bias);
+    else
+        return fail(AVR_E_ARG, "avr_ray_pose_bias: unknown param dtype");
+    return check_launch("avr_ray_pose_bias");
+}

@@ -281,6 +281,32 @@ def _bias_columns(w1):
     return cols
 
 
+def _ray_pose_bias(dir_enc, tx_enc, view, tx, wd, wt, layout):
+    """The first-layer bias of every ray in one launch (`avr_ray_pose_bias`):
+    the per-ray direction and per-pose tx encodings, rounded as the unfused
+    path rounds them, times their weight columns.  None when the grids do
+    not fit the kernel (the caller then runs the torch ops)."""
+    B, R, S = layout
+    if not (view.is_cuda and dir_enc.dtype == tx_enc.dtype and dir_enc.param_dtype == tx_enc.param_dtype
+            and dir_enc.n_levels <= 32 and tx_enc.n_levels <= 32
+            and wd.size(0) == dir_enc.n_output_dims and wt.size(0) == tx_enc.n_output_dims):
+        return None
+    from . import _lib
+    from .encoding import _code
+    v = view.reshape(B, R * S, 3).float().contiguous()
+    t = tx.reshape(B, R * S, 3).float().contiguous()
+    cache = not torch.is_grad_enabled()
+    dtab, ttab = dir_enc.table(cache), tx_enc.table(cache)
+    bias = torch.empty(B * R, wd.size(1), dtype=torch.float32, device=view.device)
+    st = torch.cuda.current_stream(view.device).cuda_stream
+    _lib.call("avr_ray_pose_bias", B, R, S, v.data_ptr(), t.data_ptr(),
+              dir_enc.n_levels, dtab.data_ptr(), dir_enc._off.ctypes.data, dir_enc._scale.ctypes.data,
+              dir_enc._res.ctypes.data, tx_enc.n_levels, ttab.data_ptr(), tx_enc._off.ctypes.data,
+              tx_enc._scale.ctypes.data, tx_enc._res.ctypes.data, _code(dtab.dtype), _code(dir_enc.dtype),
+              wd.data_ptr(), wt.data_ptr(), wd.size(1), bias.data_ptr(), st)
+    return bias
+
+
 def _sigma_params(model):
     return _sigma.network_layers(model._model_encoder_sigma) + _sigma.network_layers(model._model_decoder_sigma)
 
@@ -364,13 +390,15 @@ class AVRModel(nn.Module):
         B, R, S = L
         bs, n = pts.size(0), pts.size(1)
         pos_enc = self._pos_encoding.forward_level_major((pts.reshape(-1, 3) + 1) / 2)
-        dir_e = self._dir_encoding((_per_ray(view.reshape(-1, 3), L) + 1) / 2)
-        tx_e = self._tx_encoding((_per_pose(tx.reshape(-1, 3), L) + 1) / 2)
         w1 = self._model_signal.layers[0].weight
         wd, wt = _bias_columns(w1)
-        bias = dir_e.to(torch.bfloat16).float() @ wd
-        bias = (bias.view(B, R, -1) + (tx_e.to(torch.bfloat16).float() @ wt).view(B, 1, -1))
-        bias = bias.reshape(B * R, -1).contiguous()
+        bias = _ray_pose_bias(self._dir_encoding, self._tx_encoding, view, tx, wd, wt, L)
+        if bias is None:
+            dir_e = self._dir_encoding((_per_ray(view.reshape(-1, 3), L) + 1) / 2)
+            tx_e = self._tx_encoding((_per_pose(tx.reshape(-1, 3), L) + 1) / 2)
+            bias = dir_e.to(torch.bfloat16).float() @ wd
+            bias = (bias.view(B, R, -1) + (tx_e.to(torch.bfloat16).float() @ wt).view(B, 1, -1))
+            bias = bias.reshape(B * R, -1).contiguous()
         params = _sigma_params(self) + [w1[:, :128]]
         packed = self._sigma_pack.get(_sigma.MESHRIR_H1, params)
         attn, h1 = _sigma.sigma_fwd(_sigma.MESHRIR_H1, packed, bs * n, [(pos_enc, 1)], [], 512, 0.01,

@@ -225,6 +225,23 @@ int avr_hashgrid_fwd_lm(int64_t N, int32_t n_levels, const float* x, const void*
                         int32_t param_dtype, const int64_t* level_offset, const float* level_scale,
                         const int32_t* level_res, void* out, int32_t out_dtype, void* stream);
 
+/* AVRModel inference: the signal network's first-layer bias of every ray,
+ * from the per-ray view direction and the per-pose tx position (model.py:221
+ * concatenates both encodings to every sample):
+ *   e_dir = bf16(enc(dir_grid((view[b][r*S] + 1) / 2))), e_tx likewise from
+ *   tx[b][0];  bias[b*R + r][o] = sum_k e_dir[k] w_dir[k][o] + sum_k e_tx[k] w_tx[k][o]
+ * view, tx [B][R*S][3] fp32 (network inputs in [-1, 1]); both grids' tables
+ * in param_dtype; enc_dtype (F16/F32) the encodings' output rounding;
+ * w_dir [2*dir_levels][n_out], w_tx [2*tx_levels][n_out] fp32; bias
+ * [B*R][n_out] fp32.  Level arrays are HOST pointers as above. */
+int avr_ray_pose_bias(int32_t B, int32_t R, int32_t S, const float* view, const float* tx,
+                      int32_t dir_levels, const void* dir_params, const int64_t* dir_offset,
+                      const float* dir_scale, const int32_t* dir_res, int32_t tx_levels,
+                      const void* tx_params, const int64_t* tx_offset, const float* tx_scale,
+                      const int32_t* tx_res, int32_t param_dtype, int32_t enc_dtype,
+                      const float* w_dir, const float* w_tx, int32_t n_out, float* bias,
+                      void* stream);
+
 /* grad_out[N][L*2] -> grad_params (fp32, accumulated with atomics; zero it
  * first). */
 int avr_hashgrid_bwd(int64_t N, int32_t n_levels, const float* x, const void* grad_out,

@@ -131,3 +131,34 @@ def test_one_output_layer_dgrad_is_the_gemm():
         gy = torch.randn(83200, 1, device=DEV, generator=g).to(dt)
         w = torch.randn(1, 256, device=DEV, generator=g).to(dt)
         assert torch.equal(gy * w, gy @ w)
+
+
+@pytest.mark.parametrize("enc_dtype", [torch.float16, torch.float32])
+def test_ray_pose_bias_kernel_matches_torch_ops(enc_dtype):
+    """avr_ray_pose_bias against the torch ops it replaces in the fused
+    inference trunk: per-ray / per-pose selection, (x + 1) / 2, the dir and tx
+    grids, fp16 -> bf16 -> fp32 rounding, two skinny fp32 GEMMs and their sum
+    (only the GEMMs' fp32 summation order differs)."""
+    from avr_amd.model import _bias_columns, _per_pose, _per_ray, _ray_pose_bias
+
+    w = WORKLOADS["c2_meshrir_1024x256x512"]
+    cfg = dict(MESHRIR_MODEL, signal_output_dim=w.T)
+    model = AVRModel(cfg, mlp_dtype=torch.bfloat16, enc_dtype=enc_dtype).to(DEV)
+    with torch.no_grad():
+        for enc in (model._dir_encoding, model._tx_encoding):
+            enc.params.uniform_(-1, 1)
+    B = 2
+    r = AVRRender(model, **w.render)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    pts, view, tx, _, geom = r.sample(torch.rand(B, 3, device=DEV, generator=g) * 4 - 2,
+                                      torch.rand(B, 3, device=DEV, generator=g) * 4 - 2)
+    L = (B, geom["n_rays"], w.n_samples)
+    wd, wt = _bias_columns(model._model_signal.layers[0].weight)
+    with torch.no_grad():
+        got = _ray_pose_bias(model._dir_encoding, model._tx_encoding, view, tx, wd, wt, L)
+        dir_e = model._dir_encoding((_per_ray(view.reshape(-1, 3), L) + 1) / 2)
+        tx_e = model._tx_encoding((_per_pose(tx.reshape(-1, 3), L) + 1) / 2)
+        ref = dir_e.to(torch.bfloat16).float() @ wd
+        ref = (ref.view(B, L[1], -1) + (tx_e.to(torch.bfloat16).float() @ wt).view(B, 1, -1)).reshape(B * L[1], -1)
+    assert got is not None and got.shape == ref.shape
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
