@@ -251,6 +251,16 @@ def _concat_ok(pts, layout):
     return layout is not None and pts.is_cuda and os.environ.get("AVR_GROUPED_CONCAT", "1") != "0"
 
 
+_HALF = torch.tensor(0.5)
+
+
+def _unit(x):
+    """(x + 1) / 2 (model.py:187-189) as ONE elementwise kernel: 0.5 + 0.5 x.
+    Halving is exact, so round(0.5 x + 0.5) == round(x + 1) / 2 bit for bit
+    (tests/test_gpu_model.py::test_unit_map_is_bit_identical)."""
+    return torch.add(_HALF, x, alpha=0.5)
+
+
 def _per_ray(x, layout):
     """The first sample's row of each ray.  Callers select before mapping
     to [0, 1] ((x + 1) / 2 is elementwise): the map then runs on B*R rows."""
@@ -350,18 +360,18 @@ class AVRModel(nn.Module):
         L = ray_layout
         if _fused_sigma_ok(self, pts, L, _sigma.MESHRIR):
             return self._trunk_fused(pts, view, tx, L)
-        pos_enc = self._pos_encoding((pts.reshape(-1, 3) + 1) / 2)
+        pos_enc = self._pos_encoding(_unit(pts.reshape(-1, 3)))
         sigma_feat = self._model_encoder_sigma(pos_enc)
         attn = self._model_decoder_sigma(F.relu(sigma_feat))
         if _concat_ok(pts, L):
             B, R, S = L
-            dir_e = self._dir_encoding((_per_ray(view.reshape(-1, 3), L) + 1) / 2)
-            tx_e = self._tx_encoding((_per_pose(tx.reshape(-1, 3), L) + 1) / 2)
+            dir_e = self._dir_encoding(_unit(_per_ray(view.reshape(-1, 3), L)))
+            tx_e = self._tx_encoding(_unit(_per_pose(tx.reshape(-1, 3), L)))
             base = grouped_concat([(sigma_feat, 1), (dir_e, S), (tx_e, R * S)], bs * n, sigma_feat.dtype,
                                   splits=[1, 1, R])
             return torch.abs(F.leaky_relu(attn)).view(bs, n, 1), base
-        dir_enc = _grouped(self._dir_encoding, (view.reshape(-1, 3) + 1) / 2, L, "ray")
-        tx_enc = _grouped(self._tx_encoding, (tx.reshape(-1, 3) + 1) / 2, L, "pose")
+        dir_enc = _grouped(self._dir_encoding, _unit(view.reshape(-1, 3)), L, "ray")
+        tx_enc = _grouped(self._tx_encoding, _unit(tx.reshape(-1, 3)), L, "pose")
         dt = sigma_feat.dtype
         sf = sigma_feat if L is None else sigma_feat.view(*L, -1)
         base = _cat_features([sf, dir_enc.to(dt), tx_enc.to(dt)], L)
@@ -373,9 +383,9 @@ class AVRModel(nn.Module):
         attn [B, N, 1] and the signal network's input [N, 208] (bf16)."""
         B, R, S = L
         bs, n = pts.size(0), pts.size(1)
-        pos_enc = self._pos_encoding.forward_level_major((pts.reshape(-1, 3) + 1) / 2)
-        dir_e = self._dir_encoding((_per_ray(view.reshape(-1, 3), L) + 1) / 2)
-        tx_e = self._tx_encoding((_per_pose(tx.reshape(-1, 3), L) + 1) / 2)
+        pos_enc = self._pos_encoding.forward_level_major(_unit(pts.reshape(-1, 3)))
+        dir_e = self._dir_encoding(_unit(_per_ray(view.reshape(-1, 3), L)))
+        tx_e = self._tx_encoding(_unit(_per_pose(tx.reshape(-1, 3), L)))
         packed = self._sigma_pack.get(_sigma.MESHRIR, _sigma_params(self))
         attn, base = _sigma.sigma_fwd(_sigma.MESHRIR, packed, bs * n, [(pos_enc, 1)],
                                       [(dir_e, S), (tx_e, R * S)], 128, 0.01)
@@ -389,13 +399,13 @@ class AVRModel(nn.Module):
         and h1 = relu(layer 1) [N, 512] bf16."""
         B, R, S = L
         bs, n = pts.size(0), pts.size(1)
-        pos_enc = self._pos_encoding.forward_level_major((pts.reshape(-1, 3) + 1) / 2)
+        pos_enc = self._pos_encoding.forward_level_major(_unit(pts.reshape(-1, 3)))
         w1 = self._model_signal.layers[0].weight
         wd, wt = _bias_columns(w1)
         bias = _ray_pose_bias(self._dir_encoding, self._tx_encoding, view, tx, wd, wt, L)
         if bias is None:
-            dir_e = self._dir_encoding((_per_ray(view.reshape(-1, 3), L) + 1) / 2)
-            tx_e = self._tx_encoding((_per_pose(tx.reshape(-1, 3), L) + 1) / 2)
+            dir_e = self._dir_encoding(_unit(_per_ray(view.reshape(-1, 3), L)))
+            tx_e = self._tx_encoding(_unit(_per_pose(tx.reshape(-1, 3), L)))
             bias = dir_e.to(torch.bfloat16).float() @ wd
             bias = (bias.view(B, R, -1) + (tx_e.to(torch.bfloat16).float() @ wt).view(B, 1, -1))
             bias = bias.reshape(B * R, -1).contiguous()
@@ -474,10 +484,10 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
         L = ray_layout
         if _fused_sigma_ok(self, pts, L, _sigma.RAF):
             return self._trunk_fused(pts, view, tx, tx_view, L)
-        pts = (pts.reshape(-1, 3) + 1) / 2
-        view = (view.reshape(-1, 3) + 1) / 2
-        tx = (tx.reshape(-1, 3) + 1) / 2
-        tx_view = (tx_view.reshape(-1, 3) + 1) / 2
+        pts = _unit(pts.reshape(-1, 3))
+        view = _unit(view.reshape(-1, 3))
+        tx = _unit(tx.reshape(-1, 3))
+        tx_view = _unit(tx_view.reshape(-1, 3))
         if _concat_ok(pts, L):
             return self._trunk_grouped(pts, view, tx, tx_view, L)
         pos_e = _grouped(self._pos_encoding, pts, L, "sample")
@@ -519,10 +529,10 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
         launch: attn [B, N, 1] and the signal network's input [N, 416]."""
         B, R, S = L
         bs, n = pts.size(0), pts.size(1)
-        p = (pts.reshape(-1, 3) + 1) / 2
-        t = (_per_pose(tx.reshape(-1, 3), L) + 1) / 2
-        v = (_per_ray(view.reshape(-1, 3), L) + 1) / 2
-        tv = (_per_pose(tx_view.reshape(-1, 3), L) + 1) / 2
+        p = _unit(pts.reshape(-1, 3))
+        t = _unit(_per_pose(tx.reshape(-1, 3), L))
+        v = _unit(_per_ray(view.reshape(-1, 3), L))
+        tv = _unit(_per_pose(tx_view.reshape(-1, 3), L))
         packed = self._sigma_pack.get(_sigma.RAF, _sigma_params(self))
         attn, base = _sigma.sigma_fwd(
             _sigma.RAF, packed, bs * n,

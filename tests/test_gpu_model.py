@@ -162,3 +162,12 @@ def test_ray_pose_bias_kernel_matches_torch_ops(enc_dtype):
         ref = (ref.view(B, L[1], -1) + (tx_e.to(torch.bfloat16).float() @ wt).view(B, 1, -1)).reshape(B * L[1], -1)
     assert got is not None and got.shape == ref.shape
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
+
+
+def test_unit_map_is_bit_identical():
+    from avr_amd.model import _unit
+
+    g = torch.Generator(device=DEV).manual_seed(6)
+    x = torch.rand(1 << 20, 3, device=DEV, generator=g) * 2 - 1
+    x[:4, 0] = torch.tensor([-1.0, 1.0, 0.0, -1 + 2 ** -24], device=DEV)
+    assert torch.equal(_unit(x), (x + 1) / 2)
