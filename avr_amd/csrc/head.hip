@@ -23,8 +23,9 @@
 //   dL/dW[t,k]     = sum_{b,s} gz[b,s,t] P[b,s,k,t]
 // The first two come from head_bwd_h (per (b, s, feature group)), the last
 // from head_bwd_w (per (feature block, s group, b), accumulating over its
-// samples in registers).  Scatter-adds into LDS are float atomics: the
-// summation order, and so the last bits, can vary from run to run.
+// samples in registers).  Every sum runs in a fixed order (rays sorted by
+// the total order (delay, ray); no float atomics), so renders and gradients
+// are bitwise reproducible.
 #include "common.h"
 
 using namespace avr;
@@ -233,9 +234,9 @@ __device__ __forceinline__ Run lane_run(int key) {
     return r;
 }
 
-// In-place exclusive prefix sum of cnt[0..T) (ints): contiguous segments per
+// In-place inclusive prefix sum of cnt[0..T) (ints): contiguous segments per
 // thread, segment totals scanned through the wavefronts and 4 LDS slots.
-__device__ __forceinline__ void block_exclusive_scan(int* cnt, int T, int* wtot) {
+__device__ __forceinline__ void block_inclusive_scan(int* cnt, int T, int* wtot) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int seg = (T + kThreads - 1) / kThreads;
     const int lo = threadIdx.x * seg, hi = min(T, lo + seg);
@@ -252,46 +253,62 @@ __device__ __forceinline__ void block_exclusive_scan(int* cnt, int T, int* wtot)
     int off = x - tot;  // exact for ints
     for (int w = 0; w < wave; ++w) off += wtot[w];
     for (int t = lo; t < hi; ++t) {
-        const int c = cnt[t];
+        off += cnt[t];
         cnt[t] = off;
-        off += c;
     }
 }
 
-// Rays of column (b, s) with a non-empty window (d < lim), counting-sorted
-// by delay into LDS: perm[p] = ray, ws[p] = its weight, and afterwards
-// cnt[t] = number of those rays with delay <= t.  Returns that number.
-template <int RPT>
-__device__ __forceinline__ int sort_rays(const Rays<RPT>& rays, int lim, int T, int* cnt, int* perm,
-                                         float* ws, int* wtot) {
-    const int lane = threadIdx.x & 63;
-    for (int t = threadIdx.x; t < T; t += kThreads) cnt[t] = 0;
-    lds_barrier();
-#pragma unroll
-    for (int u = 0; u < RPT; ++u) {
-        const int d = rays.d[u];
-        const bool live = d < lim;
-        const Run run = lane_run(live ? d : -1);
-        if (run.tail && live) atomicAdd(&cnt[d], run.last - run.first + 1);
-    }
-    lds_barrier();
-    block_exclusive_scan(cnt, T, wtot);
-    lds_barrier();
-#pragma unroll
-    for (int u = 0; u < RPT; ++u) {
-        const int d = rays.d[u];
-        const bool live = d < lim;
-        const Run run = lane_run(live ? d : -1);
-        int base = 0;
-        if (run.tail && live) base = atomicAdd(&cnt[d], run.last - run.first + 1);
-        base = __shfl(base, run.last, 64);
-        if (live) {
-            const int pos = base + lane - run.first;
-            perm[pos] = threadIdx.x + kThreads * u;
-            ws[pos] = rays.w[u];
+// Smallest power of two >= R (the bitonic sort's key array)
+__host__ __device__ constexpr int pow2_ceil(int R) {
+    int n = 1;
+    while (n < R) n <<= 1;
+    return n;
+}
+
+// Ascending bitonic sort of keys[0..n) (n a power of two) in LDS.  The keys
+// are distinct, so the result (and everything summed in its order) does not
+// depend on how the waves are scheduled.
+__device__ __forceinline__ void bitonic_sort(uint32_t* keys, int n) {
+    for (int k = 2; k <= n; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < (n >> 1); i += kThreads) {
+                const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
+                const int hi = lo + j;
+                const uint32_t a = keys[lo], c = keys[hi];
+                if ((a > c) == ((lo & k) == 0)) {
+                    keys[lo] = c;
+                    keys[hi] = a;
+                }
+            }
+            lds_barrier();
         }
     }
+}
+
+// Rays of column (b, s) with a non-empty window (d < lim), sorted by
+// (delay, ray) -- a total order, so the sort is deterministic: keys
+// (d << 12 | r) in LDS through a bitonic sort; afterwards cnt[t] = number of
+// live rays with delay <= t (integer histogram + scan, order-free) and
+// keys[p] & 0xfff is the p-th ray.  Returns the number of live rays.
+template <int RPT>
+__device__ __forceinline__ int sort_rays(const Rays<RPT>& rays, int lim, int T, int R, int* cnt, float* wr,
+                                         uint32_t* keys, int nk, int* wtot) {
+    for (int t = threadIdx.x; t < T; t += kThreads) cnt[t] = 0;
+    for (int i = threadIdx.x; i < nk; i += kThreads) keys[i] = 0xffffffffu;
     lds_barrier();
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+        const int r = threadIdx.x + kThreads * u;
+        const int d = rays.d[u];
+        const bool live = d < lim;
+        if (r < R) wr[r] = rays.w[u];
+        if (live) keys[r] = ((uint32_t)d << 12) | (uint32_t)r;
+        const Run run = lane_run(live ? d : -1);
+        if (run.tail && live) atomicAdd(&cnt[d], run.last - run.first + 1);  // integer: order-free
+    }
+    lds_barrier();
+    block_inclusive_scan(cnt, T, wtot);
+    bitonic_sort(keys, nk);
     return T > 0 ? cnt[T - 1] : 0;
 }
 
@@ -434,17 +451,19 @@ __global__ __launch_bounds__(kThreads) void head_sort_kernel(avr_render_params p
     extern __shared__ float lds_f[];
     const int T = pp.T, S = pp.n_samples;
     const int s = blockIdx.x, b = blockIdx.y;
+    const int nk = pow2_ceil(R);
     int* cnt = reinterpret_cast<int*>(lds_f);
-    int* perm = cnt + T;
-    float* ws = reinterpret_cast<float*>(perm + R);
-    int* wtot = reinterpret_cast<int*>(ws + R);
+    float* wr = reinterpret_cast<float*>(cnt + T);
+    uint32_t* keys = reinterpret_cast<uint32_t*>(wr + R);
+    int* wtot = reinterpret_cast<int*>(keys + nk);
     Rays<RPT> rays;
     rays.load(w, delay, b, s, R, S);
-    const int n = sort_rays<RPT>(rays, tail_limit(pp, s), T, cnt, perm, ws, wtot);
+    const int n = sort_rays<RPT>(rays, tail_limit(pp, s), T, R, cnt, wr, keys, nk, wtot);
     const int64_t col = (int64_t)b * S + s;
     for (int p = threadIdx.x; p < R; p += kThreads) {
-        perm_out[col * R + p] = p < n ? perm[p] : 0;
-        ws_out[col * R + p] = p < n ? ws[p] : 0.0f;
+        const int r = p < n ? (int)(keys[p] & 0xfffu) : 0;
+        perm_out[col * R + p] = r;
+        ws_out[col * R + p] = p < n ? wr[r] : 0.0f;
     }
     for (int t = threadIdx.x; t < T; t += kThreads) cnt_out[col * T + t] = cnt[t];
 }
@@ -793,7 +812,7 @@ struct HeadShape {
     int kg;             // features per group
     size_t lds_q;       // head_bwd_h: Q[kb][q_stride(T)]
     size_t lds_c;       // head_fwd / head_bwd_w: C[kb][R+1]
-    size_t lds_sort;    // head_sort: cnt[T], perm[R], ws[R]
+    size_t lds_sort;    // head_sort: cnt[T], wr[R], keys[pow2_ceil(R)]
 };
 
 int head_shape(const avr_render_params& p, int B, int R, int K, int es, HeadShape* hs) {
@@ -805,7 +824,7 @@ int head_shape(const avr_render_params& p, int B, int R, int K, int es, HeadShap
     // backward's Q[kb][T] in <= 80 KiB of LDS (two workgroups per CU)
     int kb = 16;
     while (kb > 4 && ((size_t)kb * q_stride(T) * 4 > 80 * 1024 || kb * nt > 64)) kb /= 2;
-    const size_t lds_sort = 4 * ((size_t)T + 2 * (size_t)R + 4);
+    const size_t lds_sort = 4 * ((size_t)T + (size_t)R + (size_t)pow2_ceil(R) + 4);
     if ((size_t)kb * q_stride(T) * 4 > 150 * 1024 || cumsum_lds_bytes(R, kb) > 150 * 1024 ||
         lds_sort > 150 * 1024)
         return fail(AVR_E_CONFIG, "fused head: T x rays too large for LDS");

@@ -1,13 +1,17 @@
-"""GPU: the fused signal head (csrc/head.hip) against
-the plain render of signal = h @ W^T.
+"""GPU: the fused signal head (csrc/head.hip).
 
 The fused path never materialises the signal; by linearity it must equal the
-unfused render of the same network output, forward and backward (grads to
-attn, h and W).  The reference for each case is the plain HIP path on the
-fp32 product of the same operands (the plain path itself is pinned to the
-reference's golden vectors in test_gpu_render.py)."""
+reference render of signal = h @ W^T.  Checked two ways on the same operands:
+* against the CPU oracle (oracle/avr_oracle.py, pinned bit-identical to
+  renderer_cpu.py) on signal = h.float() @ W.T computed on the host, forward
+  (1e-4, the north-star bar) and backward through oracle autograd (grads to
+  attn, h = grad_signal @ W and W = grad_signal^T @ h);
+* against the plain HIP render of the same product (tighter: 2e-5).
+Renders and gradients are bitwise reproducible run to run."""
 import pytest
 import torch
+
+from oracle import avr_oracle as orc
 
 from avr_amd import AVRRender
 from avr_amd.model import AVRModel_complex
@@ -31,21 +35,82 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_fused_head_matches_plain_render(case, dtype):
+def _operands(case, dtype):
     name, base, n_azi, n_ele, S, T, K, B = case
     cfg = dict(base, n_azi=n_azi, n_ele=n_ele, n_samples=S)
-    r = AVRRender(None, **cfg)
     R = n_azi * n_ele + 2
     g = torch.Generator(device=DEV).manual_seed(sum(map(ord, name)))
     ro = torch.rand(B, 3, device=DEV, generator=g) * 2 - 1
     tx = torch.rand(B, 3, device=DEV, generator=g) * 2 - 1
-    torch.manual_seed(5)
-    _, _, _, _, geom = r.sample(ro, tx)
     attn = (torch.rand(B, R * S, 1, device=DEV, generator=g) * 2)
     h = torch.relu(torch.randn(B, R * S, K, device=DEV, generator=g)).to(dtype)
     W = (torch.randn(T, K, device=DEV, generator=g) / K ** 0.5)
+    go = torch.randn(B, T // 2 + 1, 2, device=DEV, generator=g)
+    return cfg, ro, tx, attn, h, W, go
+
+
+def _fused(case, dtype, ops=None):
+    """Fused render + backward; returns (out, grad_attn, grad_h, grad_W)."""
+    cfg, ro, tx, attn, h, W, go = ops or _operands(case, dtype)
+    r = AVRRender(None, **cfg)
+    torch.manual_seed(5)
+    _, _, _, _, geom = r.sample(ro, tx)
+    a1 = attn.clone().requires_grad_(True)
+    h1 = h.clone().requires_grad_(True)
+    W1 = W.clone().requires_grad_(True)
+    out = r.render_from_hidden(a1, h1, W1, dtype, geom)
+    (out * go).sum().backward()
+    return out.detach(), a1.grad, h1.grad, W1.grad
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_fused_head_matches_oracle(case, dtype):
+    """Fused head against the CPU oracle (the reference's algorithm) on
+    signal = h @ W^T with the dtype-rounded operands, forward and backward."""
+    name = case[0]
+    ops = _operands(case, dtype)
+    cfg, ro, tx, attn, h, W, go = ops
+    out_f, ga_f, gh_f, gW_f = _fused(case, dtype, ops)
+
+    hc = h.float().cpu()
+    Wc = W.to(dtype).float().cpu().double()
+    ac = attn.cpu().requires_grad_(True)
+    sig = (hc.double() @ Wc.t()).float().requires_grad_(True)
+    torch.manual_seed(5)  # the jitter draw the fused render consumed
+    ref = orc.render_spectrum(orc.RenderConfig.from_kwargs(**cfg), orc.StubNetwork(ac, sig),
+                              ro.cpu(), tx.cpu())
+    (ref * go.cpu()).sum().backward()
+    gs = sig.grad.double()
+    gh_ref = gs @ Wc  # dL/dh = dL/dsignal @ W
+    gW_ref = torch.einsum("brt,brk->tk", gs, hc.double())  # dL/dW = sum over rows
+
+    assert _rel(out_f.cpu(), ref) < 1e-4, (name, _rel(out_f.cpu(), ref))
+    tol_h = 1e-3 if dtype == torch.float32 else 6e-3  # grad_h is stored in the h dtype
+    assert _rel(ga_f.cpu(), ac.grad) < 1e-3, (name, "attn", _rel(ga_f.cpu(), ac.grad))
+    assert _rel(gh_f.float().cpu(), gh_ref) < tol_h, (name, "h", _rel(gh_f.float().cpu(), gh_ref))
+    assert _rel(gW_f.cpu(), gW_ref) < 1e-3, (name, "W", _rel(gW_f.cpu(), gW_ref))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_fused_head_bitwise_reproducible(case, dtype):
+    """Two renders (forward + backward) of the same operands are identical."""
+    ops = _operands(case, dtype)
+    a = _fused(case, dtype, ops)
+    b = _fused(case, dtype, ops)
+    for x, y, what in zip(a, b, ("out", "grad_attn", "grad_h", "grad_W")):
+        assert torch.equal(x, y), (case[0], what)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_fused_head_matches_plain_render(case, dtype):
+    name, base, n_azi, n_ele, S, T, K, B = case
+    cfg, ro, tx, attn, h, W, go = _operands(case, dtype)
+    r = AVRRender(None, **cfg)
+    torch.manual_seed(5)
+    _, _, _, _, geom = r.sample(ro, tx)
 
     a1 = attn.clone().requires_grad_(True)
     h1 = h.clone().requires_grad_(True)
@@ -61,7 +126,6 @@ def test_fused_head_matches_plain_render(case, dtype):
     out_u = r.render_from_network_output(a2, sig, geom)
 
     assert _rel(out_f, out_u) < 2e-5, (name, _rel(out_f, out_u))
-    go = torch.randn(out_f.shape, device=DEV, generator=g)
     (out_f * go).sum().backward()
     (out_u * go).sum().backward()
     tol_h = 2e-4 if dtype == torch.float32 else 6e-3  # grad_h is stored in the h dtype

@@ -42,12 +42,8 @@ def test_oracle_forward_matches_reference(name):
     np.testing.assert_allclose(rec["dirs"].numpy(), case["dirs"], rtol=0, atol=2e-7)
     np.testing.assert_array_equal(rec["shift"].numpy(), case["shift"])
     digest_check(case, "weights", rec["weights"].numpy(), rtol=1e-5, atol=1e-9)
-    d = rec["delay"].numpy()
-    if case.has("delay"):
-        assert (d == case["delay"]).mean() > 0.999
-    else:
-        assert (d.reshape(-1)[case["delay_idx"]] == case["delay_at"]).mean() > 0.999
-        assert abs(float(d.astype(np.float64).sum()) - float(case["delay_sum"])) <= 0.001 * d.size
+    # integer work is bit-exact: every delay of every fixture
+    np.testing.assert_array_equal(rec["delay"].numpy().astype(np.int16), case["delay"])
     for k in ("pts", "view", "tx", "dir_tx"):
         if case.has("net_" + k + "_sum"):
             digest_check(case, "net_" + k, rec[k].numpy(), rtol=1e-6, atol=1e-6)
