@@ -18,7 +18,12 @@ With the same seed the replay equals the eager render bit for bit
 
 The network is captured too, so it must be graph-safe (no host syncs, same
 tensors every call): the stub network of bench.py, and the package's own
-models at inference.  The returned tensors are the graph's static outputs,
+models at inference.  The package's weight caches (bf16 casts, packed
+head/sigma weights, bias columns) are bypassed while a graph is captured
+(wcache.capturing), so every replay derives them from the master weights it
+reads by pointer: an optimizer step (in place) between replays is seen, and
+a parameter whose storage was replaced (load_state_dict with assign, .to())
+starts a new capture (graphs are keyed on the parameters' data pointers).  The returned tensors are the graph's static outputs,
 overwritten by the next replay of the same graph: clone them to keep them.
 """
 from __future__ import annotations
@@ -70,7 +75,8 @@ class GraphedRender:
         replayed; the tensors are the graph's static outputs."""
         r = self.renderer
         dev = r._device(rays_o)
-        key = (int(position_tx.size(0)), direction_tx is None, dev)
+        key = (int(position_tx.size(0)), direction_tx is None, dev,
+               tuple(p.data_ptr() for p in r.parameters()))
         g = self._graphs.get(key)
         if g is None:
             g = self._graphs[key] = self._capture(dev, rays_o, position_tx, direction_tx)

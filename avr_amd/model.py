@@ -18,7 +18,7 @@ import torch.nn.functional as F
 from . import sigma as _sigma
 from .concat import grouped_concat
 from .encoding import HashGridEncoding
-from .wcache import cast_weight
+from .wcache import cache_lookup, cache_store, capturing, cast_weight
 
 
 import os
@@ -279,16 +279,12 @@ def _bias_columns(w1):
     the unfused GEMM reads them, in fp32 and transposed; kept on the weight
     until it changes (version counter), like wcache.cast_weight."""
     key = (w1.data_ptr(), w1._version)
-    hit = getattr(w1, "_avr_bias_cols", None)
-    if hit is not None and hit[0] == key:
-        return hit[1]
+    hit = None if capturing() else cache_lookup(w1, "_avr_bias_cols", key)
+    if hit is not None:
+        return hit
     wb = cast_weight(w1, torch.bfloat16, True).float()
     cols = (wb[:, 128:168].t().contiguous(), wb[:, 168:208].t().contiguous())
-    try:
-        w1._avr_bias_cols = (key, cols)
-    except AttributeError:
-        pass
-    return cols
+    return cols if capturing() else cache_store(w1, "_avr_bias_cols", key, cols)
 
 
 def _ray_pose_bias(dir_enc, tx_enc, view, tx, wd, wt, layout):

@@ -13,7 +13,14 @@ independent:
   all-reduce (F*8 bytes per pose: 4 KiB at config 2) sums them.  The azimuth
   jitter is drawn on every rank (keeping each rank's CPU generator in the
   same state as the reference's) and rank 0's draw is broadcast, so all
-  shards see one sphere.
+  shards see one sphere.  Over RCCL the broadcast stays on the device and the
+  sampling kernel reads the jitter there (no host synchronisation per pose).
+
+  Training through a ray-sharded render: the loss on the all-reduced
+  spectrum is replicated, so each rank's parameter gradient covers only its
+  own rays and the true gradient is their SUM.  Call
+  `allreduce_grads_sum(module.parameters())` after backward (do not wrap the
+  module in DDP, which would average).
 """
 from __future__ import annotations
 
@@ -53,14 +60,37 @@ def allreduce_spectrum(partial: torch.Tensor, group=None) -> torch.Tensor:
     return _AllReduceSum.apply(partial, group)
 
 
-def broadcast_jitter(u_azi: torch.Tensor, group=None, device=None) -> torch.Tensor:
-    """Rank 0's azimuth draw to every rank (n_azi floats)."""
+def broadcast_jitter(u_azi: torch.Tensor, group=None, device=None, keep_on_device=False) -> torch.Tensor:
+    """Rank 0's azimuth draw to every rank (n_azi floats).
+
+    With `keep_on_device` (RCCL) the result stays a device tensor, which
+    `AVRRender.sample` reads in its sampling kernel without a host copy."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return u_azi
     backend = dist.get_backend(group)
     t = u_azi.to(device) if (backend == "nccl" and device is not None) else u_azi.clone()
     dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
-    return t.cpu()
+    return t if (keep_on_device and t.is_cuda) else t.cpu()
+
+
+def allreduce_grads_sum(params, group=None):
+    """SUM-all-reduce of parameter gradients after a ray-sharded backward
+    (each rank's gradient covers its own rays; the full-pose gradient is
+    their sum).  One flat buffer per dtype/device, one collective each."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    buckets = {}
+    for p in params:
+        if p.grad is not None:
+            buckets.setdefault((p.grad.device, p.grad.dtype), []).append(p.grad)
+    for grads in buckets.values():
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+        off = 0
+        for g in grads:
+            n = g.numel()
+            g.copy_(flat[off:off + n].view_as(g))
+            off += n
 
 
 class RayShardedRender(nn.Module):
@@ -82,7 +112,8 @@ class RayShardedRender(nn.Module):
         R = int(r.n_azi) * int(r.n_ele) + 2
         r.ray_range = shard_range(R, rank, world)
         try:
-            u = broadcast_jitter(draw_jitter(r.n_azi, r.n_ele), self.group, rays_o.device)
+            u = broadcast_jitter(draw_jitter(r.n_azi, r.n_ele), self.group, rays_o.device,
+                                 keep_on_device=rays_o.is_cuda)
             pts, view, tx, dtx, geom = r.sample(rays_o, position_tx, direction_tx, u_azi=u)
             kw = {} if ch_idx is None else {"ch_idx": ch_idx}
             if dtx is not None:

@@ -29,11 +29,8 @@ import torch.nn as nn
 
 from . import _lib
 from ._lib import DTYPE_BF16, DTYPE_F16, DTYPE_F32, render_params
-from .wcache import cast_weight
+from .wcache import cache_lookup, cache_store, capturing, cast_weight
 
-# Optional instrumentation for bench.py: an object with begin(stream) / end(stream)
-# called around the dominant kernel (the ray-reduction stream).  None in normal use.
-KERNEL_TIMER = None
 
 _RENDER_KEYS = ("n_samples", "near", "far", "n_azi", "n_ele", "speed", "fs", "pathloss",
                 "xyz_min", "xyz_max")
@@ -114,11 +111,14 @@ class Tables:
         key = (p.n_rays, B, sig_code, os.environ.get("AVR_NSPLIT"), os.environ.get("AVR_KSPLIT"))
         v = self._layouts.get(key)
         if v is None:
-            off = (ctypes.c_int64 * 5)()
-            sp = (ctypes.c_int32 * 2)()
-            _lib.call("avr_render_core_layout", ctypes_ref(p), B, sig_code, off, sp)
-            v = (tuple(off), int(sp[0]), int(sp[1]))
-            self._layouts[key] = v
+            with _TABLE_LOCK:
+                v = self._layouts.get(key)
+                if v is None:
+                    off = (ctypes.c_int64 * 5)()
+                    sp = (ctypes.c_int32 * 2)()
+                    _lib.call("avr_render_core_layout", ctypes_ref(p), B, sig_code, off, sp)
+                    v = (tuple(off), int(sp[0]), int(sp[1]))
+                    self._layouts[key] = v
         return v
 
 
@@ -129,7 +129,7 @@ def ctypes_ref(p):
 
 
 _TABLE_CACHE: dict = {}
-_TABLE_LOCK = threading.Lock()
+_TABLE_LOCK = threading.RLock()
 
 
 def get_tables(p, device) -> Tables:
@@ -230,8 +230,12 @@ def _grad_attn(p, tables, attn, grad_w, st):
     return grad_attn
 
 
-def _render_core_fwd(attn, signal, p, tables, rays_o, position_tx, dirs, ir_out):
-    """avr_render_core_fwd -> (out [B, F, 2], workspace, layout offsets)."""
+def _render_core_fwd(attn, signal, p, tables, rays_o, position_tx, dirs, ir_out, timer=None):
+    """avr_render_core_fwd -> (out [B, F, 2], workspace, layout offsets).
+
+    `timer` (bench.py / tools/tune.py instrumentation, normally None) hands
+    out a pair of hipEvent_t the library records around the ray-reduction
+    launch on its stream."""
     dev = signal.device
     B = signal.size(0)
     F = p.T // 2 + 1
@@ -240,7 +244,6 @@ def _render_core_fwd(attn, signal, p, tables, rays_o, position_tx, dirs, ir_out)
     ws = torch.empty(off[4], dtype=torch.uint8, device=dev)
     out = torch.empty(B, F, 2, dtype=torch.float32, device=dev)
     ev0 = ev1 = None
-    timer = KERNEL_TIMER
     if timer is not None:
         R, S = p.n_rays, p.n_samples
         delay = ws[off[1]:off[1] + B * R * S * 4].view(torch.int32).view(B, R, S)
@@ -261,11 +264,11 @@ class RenderCore(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, attn, signal, p, tables, rays_o, position_tx, dirs, ir_out=None):
+    def forward(ctx, attn, signal, p, tables, rays_o, position_tx, dirs, ir_out=None, timer=None):
         """One native call (avr_render_core_fwd): weights, ray reduction, DFT
         + phase, finalize, and the irfft into `ir_out` [B, 2(F-1)] when given
         (forward only, as spectrum_to_ir)."""
-        out, ws, off = _render_core_fwd(attn, signal, p, tables, rays_o, position_tx, dirs, ir_out)
+        out, ws, off = _render_core_fwd(attn, signal, p, tables, rays_o, position_tx, dirs, ir_out, timer)
         B, R, S = signal.size(0), p.n_rays, p.n_samples
         w = ws[off[0]:off[0] + B * R * S * 4].view(torch.float32).view(B, R, S)
         delay = ws[off[1]:off[1] + B * R * S * 4].view(torch.int32).view(B, R, S)
@@ -288,7 +291,7 @@ class RenderCore(torch.autograd.Function):
                   _ptr(gz), _ptr(w), _ptr(delay), _ptr(grad_signal), _ptr(grad_w), st)
         grad_attn = _grad_attn(p, tables, attn, grad_w, st) if ctx.needs_input_grad[0] else None
         return (grad_attn, grad_signal if ctx.needs_input_grad[1] else None,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 def _packed_head_weight(w_master, W, cache, pref, shape_key, st):
@@ -296,19 +299,15 @@ def _packed_head_weight(w_master, W, cache, pref, shape_key, st):
     `cache` (no autograd graph recorded) the copy is kept on the master
     weight until it changes, like wcache.cast_weight."""
     key = (W.data_ptr(), w_master._version, shape_key)
+    cache = cache and not capturing()
     if cache:
-        hit = getattr(w_master, "_avr_headpack", None)
-        if hit is not None and hit[0] == key:
-            return hit[1]
+        hit = cache_lookup(w_master, "_avr_headpack", key)
+        if hit is not None:
+            return hit
     B, K, code = shape_key[2], shape_key[3], shape_key[4]
     Wp = torch.empty_like(W)
     _lib.call("avr_head_pack_w", pref, B, K, _ptr(W), code, _ptr(Wp), st)
-    if cache:
-        try:
-            w_master._avr_headpack = (key, Wp)
-        except AttributeError:
-            pass
-    return Wp
+    return cache_store(w_master, "_avr_headpack", key, Wp) if cache else Wp
 
 
 class FusedHeadCore(torch.autograd.Function):
@@ -374,6 +373,19 @@ class FusedHeadCore(torch.autograd.Function):
                 grad_W if ctx.needs_input_grad[2] else None, None, None, None, None, None, None, None)
 
 
+def _poison_nonfinite(out, tensors, ir_out=None):
+    """out + NaN where any element of `tensors` is non-finite, else out + 0
+    (the reference's NaN propagation through its masks; no host sync)."""
+    bad = torch.zeros((), dtype=torch.bool, device=out.device)
+    for t in tensors:
+        bad = bad | ~torch.isfinite(t).all()
+    poison = torch.where(bad, torch.tensor(float("nan"), device=out.device),
+                         torch.tensor(0.0, device=out.device))
+    if ir_out is not None:
+        ir_out.add_(poison)
+    return out + poison
+
+
 # --------------------------------------------------------------------------
 # reference-named helpers (renderer.py:127-165)
 # --------------------------------------------------------------------------
@@ -430,8 +442,21 @@ class AVRRender(nn.Module):
         # fold the signal network's last layer into the render when the
         # network offers it (avr_amd.model networks; FusedHeadCore)
         self.fused_head = bool(kwargs.get("fused_head", True))
+        # Non-finite network outputs: the ray reduction never loads a 16-byte
+        # chunk whose elements are all masked, so a NaN/Inf confined to masked
+        # elements does not reach the spectrum here, whereas the reference's
+        # `signal * mask` turns it into NaN (renderer.py:82,89) and its runner
+        # then skips the step (avr_runner.py:183-185).  With
+        # propagate_nonfinite=True any non-finite attn/signal element poisons
+        # the output exactly like the reference (one extra read of the
+        # network output, no host synchronisation).
+        self.propagate_nonfinite = bool(kwargs.get("propagate_nonfinite", False))
         self._pcache = {}
+        self._pcache_lock = threading.Lock()
         self._jitter_dev = None  # device jitter buffer while a HIP graph is captured (avr_amd.graph)
+        # bench/tuning instrumentation: an object whose events(...) returns the
+        # hipEvent_t pair recorded around the ray reduction (bench.KernelTimer)
+        self.kernel_timer = None
 
     # -- stages, exposed for tests and for callers that bring their own network
     def _device(self, rays_o):
@@ -453,6 +478,10 @@ class AVRRender(nn.Module):
         dev = self._device(rays_o)
         B = position_tx.size(0)
         u_dev = self._jitter_dev if u_azi is None else None
+        if u_azi is not None and u_azi.is_cuda:
+            # jitter already on the device (RCCL broadcast by RayShardedRender):
+            # the sampling kernel reads it there, no host round trip
+            u_dev, u_azi = u_azi.to(dev, torch.float32).contiguous(), None
         if u_azi is None and u_dev is None:
             u_azi = draw_jitter(self.n_azi, self.n_ele)
         R_all = int(self.n_azi) * int(self.n_ele) + 2
@@ -505,8 +534,11 @@ class AVRRender(nn.Module):
         key = (T, R)
         p = self._pcache.get(key)
         if p is None:
-            p = render_params(self._cfg, T, n_rays=R)
-            self._pcache[key] = p
+            with self._pcache_lock:  # nn.DataParallel threads share the module
+                p = self._pcache.get(key)
+                if p is None:
+                    p = render_params(self._cfg, T, n_rays=R)
+                    self._pcache[key] = p
         return p
 
     def render_from_network_output(self, attn, signal, geom, ir_out=None):
@@ -532,10 +564,14 @@ class AVRRender(nn.Module):
             check_config(p, tables)
             if not (torch.is_grad_enabled() and (attn.requires_grad or signal.requires_grad)):
                 # inference: the same native call without the autograd node
-                return _render_core_fwd(attn, signal, p, tables, geom["rays_o"],
-                                        geom["position_tx"], geom["dirs"], ir_out)[0]
-            return RenderCore.apply(attn, signal, p, tables, geom["rays_o"], geom["position_tx"],
-                                    geom["dirs"], ir_out)
+                out = _render_core_fwd(attn, signal, p, tables, geom["rays_o"],
+                                       geom["position_tx"], geom["dirs"], ir_out, self.kernel_timer)[0]
+            else:
+                out = RenderCore.apply(attn, signal, p, tables, geom["rays_o"], geom["position_tx"],
+                                       geom["dirs"], ir_out, self.kernel_timer)
+            if self.propagate_nonfinite:
+                out = _poison_nonfinite(out, (attn, signal), ir_out)
+            return out
 
     def _head_supported(self, geom, h, weight, dtype):
         """Whether the fused-head kernels take this shape (T <= 4096, <= 4096
@@ -646,5 +682,7 @@ def _ir_twiddle(n, dev):
                 tw = torch.empty(n, 2, dtype=torch.float32, device=dev)
                 with torch.cuda.device(dev):
                     _lib.call("avr_ir_twiddle", n, _ptr(tw), _stream(dev))
+                    # other host threads read it on their own streams
+                    torch.cuda.current_stream(dev).synchronize()
                 _IRTW[key] = tw
     return tw

@@ -24,6 +24,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .wcache import cache_lookup, cache_store, capturing
 
 MESHRIR = 0  # AVR_SIGMA_MESHRIR
 RAF = 1      # AVR_SIGMA_RAF
@@ -73,6 +74,26 @@ def fragment_index(M, K, first):
     return o, k, valid
 
 
+_INDEX: dict = {}
+
+
+def _gather_index(M, K, first, device):
+    """Device (row, col) gather indices of fragment_index, invalid slots
+    pointing at the zero corner; kept per shape and device, so repacking
+    (every optimizer step, or inside a captured HIP graph) does no host copy."""
+    key = (M, K, first, device)
+    v = _INDEX.get(key)
+    if v is None:
+        o, k, valid = fragment_index(M, K, first)
+        OT, KS = o.shape[:2]
+        v = (torch.from_numpy(np.where(valid, o, OT * 32)).to(device),
+             torch.from_numpy(np.where(valid, k, KS * 16)).to(device))
+        if device.type == "cuda":
+            torch.cuda.current_stream(device).synchronize()  # shared across streams
+        _INDEX[key] = v
+    return v
+
+
 def pack_layers(variant, weights):
     """Weights (fp32 [M, K] tensors, in SCHEDULE order) -> packed bf16
     fragments, one 32 KB chunk per LDS stage (zero padded), as a flat
@@ -84,13 +105,10 @@ def pack_layers(variant, weights):
     for w, (M, K, first, co) in zip(weights, sched):
         if tuple(w.shape) != (M, K):
             raise ValueError(f"layer shape {tuple(w.shape)} != {(M, K)}")
-        o, k, valid = fragment_index(M, K, first)
-        OT, KS = o.shape[:2]
+        oi, ki = _gather_index(M, K, first, w.device)
+        OT, KS = oi.shape[:2]
         wp = torch.zeros(OT * 32 + 1, KS * 16 + 1, dtype=torch.float32, device=w.device)
         wp[:M, :K] = w.detach().float()
-        # invalid slots read the zero corner
-        oi = torch.from_numpy(np.where(valid, o, OT * 32)).to(w.device)
-        ki = torch.from_numpy(np.where(valid, k, KS * 16)).to(w.device)
         frags = wp[oi, ki].to(torch.bfloat16)  # [OT, KS, 64, 8]
         for c in range(OT // co):
             part = frags[c * co:(c + 1) * co].reshape(-1)
@@ -136,16 +154,14 @@ class SigmaWeights:
     """Packed fragments of a model's sigma networks, repacked when any weight
     changes (parameter version counters)."""
 
-    def __init__(self):
-        self.key = None
-        self.packed = None
-
     def get(self, variant, params):
+        if capturing():  # a captured graph repacks at every replay
+            return pack_layers(variant, params)
         key = (variant,) + tuple((p.data_ptr(), p._version) for p in params)
-        if key != self.key:
-            self.packed = pack_layers(variant, params)
-            self.key = key
-        return self.packed
+        hit = cache_lookup(self, "_entry", key)
+        if hit is not None:
+            return hit
+        return cache_store(self, "_entry", key, pack_layers(variant, params))
 
 
 def _src(t, rows_div):

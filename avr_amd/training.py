@@ -169,6 +169,9 @@ class TrainStep:
         total.backward()
         if self.native_adam:
             clip_sanitize_adam_(self.optimizer, max_norm=1)
+            # the Adam update ran natively: tell the LR scheduler that this
+            # step's optimizer.step() happened (its order check reads the flag)
+            self.optimizer._opt_called = True
         else:
             clip_and_sanitize_(self.renderer.parameters(), max_norm=1)
             self.optimizer.step()

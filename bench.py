@@ -1,22 +1,38 @@
-"""Benchmark: MeshRIR single-listener render (config 2) through the IR.
+"""Benchmark: the acoustic volume render path on MI355X.
 
-One step = one pass of the hot path over one pose of synthetic input with the
-network output already resident in HBM (stub network, as the reference's own
-CPU timing does): ray generation + sampling (network inputs) -> weights ->
-ray-reduction stream -> MFMA DFT + phase -> spectrum -> irfft IR.
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode MODE] [--workload NAME]
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+Modes (a "step" is one pass of the hot path over one unit of synthetic input):
 
-For N > 1 launch with torch.distributed.run (one process per GPU); each rank
-renders its own poses (weak scaling, no data-path collective), rank 0 prints
-one JSON line with the whole-job ray-samples/s.
+* `pose` (default, the BASELINE metric): MeshRIR single-listener render,
+  config 2 (1024 rays x 256 samples x 512 bins).  One step = one pose through
+  the IR with the network output already resident in HBM (stub network, as
+  the reference's own CPU timing does): ray generation + sampling -> weights
+  -> ray-reduction stream -> MFMA DFT + phase -> spectrum -> irfft IR.  With
+  N ranks every rank renders its own poses (weak scaling, no data-path
+  collective: poses are independent).
+* `ray-shard`: config 5 (4096 x 512 x 2048 bins, fp16 signal), ONE pose whose
+  rays are split over the N ranks (avr_amd.parallel.RayShardedRender) with the
+  spectrum all-reduce over RCCL inside the timed region, then the IR (strong
+  scaling: the pose is fixed, each rank holds 17.2 GB / N of signal).
+* `ddp-train`: config 4 (RAF-Empty, 4 poses per rank), the full training step
+  (avr_runner_ddp.py:131-137 body: AVRModel_complex -> render -> criterion ->
+  backward with DDP's bucketed RCCL gradient all-reduce -> clip + Adam ->
+  scheduler) (weak scaling).
+
+`--gpus N` with N > 1 outside torchrun re-launches this script under
+`torch.distributed.run` (one process per GPU) before any GPU call; under
+torchrun the world size comes from the environment and must equal --gpus.
+Rank 0 prints ONE JSON line; `value` is the whole-job throughput = units all
+ranks processed / max-over-ranks time of the K timed steps.
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -25,11 +41,13 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from avr_amd import AVRRender  # noqa: E402
-from avr_amd import renderer as rmod  # noqa: E402
-from avr_amd.workloads import WORKLOADS  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "ray-samples/sec/GPU (1024 rays×256 samp×512 freq) + IR render ms/pose"
+MODES = {  # mode -> default workload (avr_amd.workloads.WORKLOADS)
+    "pose": "c2_meshrir_1024x256x512",
+    "ray-shard": "c5_simu_4096x512x2048",
+    "ddp-train": "c4_raf_empty_b4_per_gpu",
+}
 
 
 class StubNet(torch.nn.Module):
@@ -42,7 +60,8 @@ class StubNet(torch.nn.Module):
 
 
 class KernelTimer:
-    """HIP events around the ray-reduction kernel on the stream it runs on.
+    """HIP events around the ray-reduction kernel on the stream it runs on
+    (set as `AVRRender.kernel_timer`).
 
     Events are created up front (creating one inside the timed loop costs
     more host time than the render issues).  Also keeps each launch's delay
@@ -86,6 +105,105 @@ class KernelTimer:
         return tot / max(1, len(self.rows))
 
 
+# ----------------------------------------------------------------------------
+# launcher (no GPU call before the ranks exist)
+# ----------------------------------------------------------------------------
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: WORLD_SIZE under torchrun, else 1")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--mode", default="pose", choices=sorted(MODES))
+    ap.add_argument("--workload", default=None, help="default: the mode's workload")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--poses", type=int, default=16,
+                    help="distinct synthetic poses cycled over the steps")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="pose mode: HIP streams the independent per-pose renders are issued on "
+                         "round-robin, each with its own signal buffer (1 = strictly serial)")
+    ap.add_argument("--mlp-dtype", default="bf16", choices=["bf16", "fp16", "fp32"],
+                    help="ddp-train mode: MLP compute dtype")
+    args = ap.parse_args(argv)
+    if args.workload is None:
+        args.workload = MODES[args.mode]
+    return args
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_command(n, argv, port, script=None):
+    """The torch.distributed.run command that starts n ranks of this script."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}",
+            script or os.path.abspath(__file__), *argv]
+
+
+def resolve_world(args, env=None, device_count=None):
+    """('launch', n) to start n ranks, ('run', world) to run as one of them.
+
+    Raises SystemExit with a clear message when the request cannot be met:
+    --gpus disagreeing with a torchrun world, or more GPUs than visible."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} "
+                             "(launch with --nproc-per-node equal to --gpus)")
+        return "run", world
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if n == 1:
+        return "run", 1
+    # counting devices does not initialise the GPU on this image
+    have = torch.cuda.device_count() if device_count is None else device_count
+    if have < n:
+        raise SystemExit(f"bench.py: --gpus {n} requested but only {have} GPU(s) visible")
+    return "launch", n
+
+
+def timed(run, world, dev):
+    """Barrier + synchronize on both sides of run(); max over ranks (s).
+    (`dev` may be the CPU: the gloo tests of this logic.)"""
+    import torch.distributed as dist
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    run()
+    t_issue = time.perf_counter() - t0
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, t_issue
+
+
+def whole_job_rate(units_per_rank, world, steps, elapsed_max):
+    """value: units every rank processed over the slowest rank's time."""
+    return units_per_rank * world * steps / elapsed_max
+
+
+# ----------------------------------------------------------------------------
+# measurement helpers
+# ----------------------------------------------------------------------------
 def pmc_traffic(workload, dtype_name):
     """HBM bytes per launch of the reduction kernel from the newest committed
     rocprofv3 --pmc summary for this workload (tools/pmc_summary.py; the
@@ -104,6 +222,41 @@ def pmc_traffic(workload, dtype_name):
             if k.startswith("void ray_reduce_fwd_kernel<" + dtype_name):
                 return v["hbm_bytes"], os.path.relpath(path, ROOT)
     return None, None
+
+
+def roofline(w, timer, dt):
+    """Roofline object for the ray-reduction kernel from the live HIP events."""
+    B, S, T = w.batch, w.n_samples, w.T
+    k_ms = timer.mean_ms()
+    es = 2 if dt == torch.float16 else 4
+    n_split = timer.n_split or 1
+    # algorithmic bytes: the live signal elements (each read once), w + delay
+    # (8 B per ray-sample), the fp32 partials written; the dense tensor is
+    # reported beside it (SURVEY.md §8d's basis; the kernel never reads the
+    # masked elements, so only the live basis bounds it)
+    live = timer.mean_live_elements(T)
+    # ray-samples one launch covers (this rank's shard in ray-shard mode)
+    rows = timer.rows[0][0].numel() if timer.rows else w.ray_samples
+    alg_bytes = live * es + rows * 8 + n_split * B * S * T * 4
+    dense_bytes = rows * (T * es + 8) + n_split * B * S * T * 4
+    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(w.name, "__half" if dt == torch.float16 else "float")
+    return {
+        "kernel": "ray_reduce_fwd_kernel",
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic,
+        "traffic_source": traffic_src,
+        "alg_bytes_per_launch": alg_bytes,
+        "dense_bytes_per_launch": dense_bytes,
+        "dense_frac": dense_bytes / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+        "live_fraction": live / (rows * T) if rows else 0.0,
+        "avg_launch_ms": k_ms,
+        "measured": "HIP events around each launch, roofline phase of K steps on one stream",
+    }
 
 
 def cpu_baseline(w, budget_s=15.0):
@@ -144,164 +297,244 @@ def cpu_baseline(w, budget_s=15.0):
     }
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="c2_meshrir_1024x256x512")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
-    ap.add_argument("--poses", type=int, default=16,
-                    help="distinct synthetic poses cycled over the steps")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="HIP streams the independent per-pose renders are issued on "
-                         "round-robin (1 = strictly serial)")
-    args = ap.parse_args()
+def _poses(w, P, dev, gen):
+    rays_o = torch.rand(P, w.batch, 3, device=dev, generator=gen) * 4 - 2
+    tx = torch.rand(P, w.batch, 3, device=dev, generator=gen) * 4 - 2
+    dtx = (torch.nn.functional.normalize(torch.randn(P, w.batch, 3, device=dev, generator=gen), dim=-1)
+           if w.with_dir_tx else [None] * P)
+    return rays_o, tx, dtx
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
-    torch.cuda.set_device(dev)
+def _base_result(args, w, world, value, elapsed, dtype):
+    return {
+        "metric": METRIC,
+        "value": value,
+        "unit": "ray-samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "per_gpu_value": value / world,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": dtype,
+        "data": "synthetic (stub network, outputs resident in HBM; seeded torch RNG)",
+    }
 
-    w = WORKLOADS[args.workload]
+
+# ----------------------------------------------------------------------------
+# modes
+# ----------------------------------------------------------------------------
+def bench_pose(args, w, world, rank, dev):
+    from avr_amd import AVRRender
+
     B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
     dt = torch.float16 if w.signal_dtype == "float16" else torch.float32
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    attn = (torch.rand(B, R * S, 1, device=dev, generator=gen) * 2).to(dt)
-    signal = (torch.randn(B, R * S, T, device=dev, generator=gen) * 0.1).to(dt)
+    n_streams = max(1, args.streams)
+    # one network output per stream, so concurrent renders never share
+    # addresses (no cross-stream cache reuse can inflate the rate)
+    renderers = []
+    for _ in range(n_streams):
+        attn = (torch.rand(B, R * S, 1, device=dev, generator=gen) * 2).to(dt)
+        signal = (torch.randn(B, R * S, T, device=dev, generator=gen) * 0.1).to(dt)
+        renderers.append(AVRRender(StubNet(attn, signal), **w.render))
     # a fixed set of listener/source poses, cycled: the live window of each
     # row (and so the bytes the reduction reads) depends on the geometry
     P = args.poses
-    rays_o = torch.rand(P, B, 3, device=dev, generator=gen) * 4 - 2
-    tx = torch.rand(P, B, 3, device=dev, generator=gen) * 4 - 2
-    dtx = (torch.nn.functional.normalize(torch.randn(P, B, 3, device=dev, generator=gen), dim=-1)
-           if w.with_dir_tx else [None] * P)
-    renderer = AVRRender(StubNet(attn, signal), **w.render)
+    rays_o, tx, dtx = _poses(w, P, dev, gen)
     timer = KernelTimer(args.steps)
-    rmod.KERNEL_TIMER = timer
+    renderers[0].kernel_timer = timer
     pose = [0]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_streams - 1)]
 
-    def step():
+    def step(k):
         i = pose[0] % P
         pose[0] += 1
         with torch.no_grad():
-            return renderer.render_ir(rays_o[i], tx[i], dtx[i])
+            return renderers[k].render_ir(rays_o[i], tx[i], dtx[i])
 
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
-
-    def run(n, n_streams):
+    def run(n, ns):
         for i in range(n):
-            with torch.cuda.stream(streams[i % n_streams]):
-                step()
+            with torch.cuda.stream(streams[i % ns]):
+                step(i % ns)
 
     torch.manual_seed(rank)
-    run(args.warmup, args.streams)
+    run(args.warmup, n_streams)
     torch.cuda.synchronize()
-
-    def barrier():
-        if world > 1:
-            import torch.distributed as dist
-
-            dist.barrier()
 
     # latency: one pose at a time on one stream (IR render ms/pose)
     n_lat = max(5, min(args.steps, 20))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(n_lat):
-        step()
+        step(0)
         torch.cuda.synchronize()
     latency_ms = (time.perf_counter() - t0) * 1e3 / n_lat
 
     # roofline phase: K launches on ONE stream with HIP events around the
     # dominant kernel on its stream, so no other kernel overlaps it and the
     # events bracket exactly the kernel (a rocprofv3 trace of this command
-    # gives the same average; events inside the 2-stream phase would also
-    # count the wait for the other stream and slow its issue down)
+    # gives the same average)
     timer.enabled = True
     run(args.steps, 1)
     torch.cuda.synchronize()
     timer.enabled = False
 
     # throughput (the reported value): K independent single-pose renders
-    barrier()
+    elapsed, t_issue = timed(lambda: run(args.steps, n_streams), world, dev)
+    value = whole_job_rate(w.ray_samples, world, args.steps, elapsed)
+    res = _base_result(args, w, world, value, elapsed, "f32" if dt == torch.float32 else "f16-storage/f32-math")
+    res.update({
+        "ir_render_ms_per_pose": latency_ms / B,
+        "host_issue_ms_per_step": t_issue * 1e3 / args.steps,
+        "streams": n_streams,
+        "config": {"workload": w.name, "mode": "pose", "rays": R, "samples": S, "T": T, "freq_bins": w.F,
+                   "poses_per_step": B, "distinct_poses": P,
+                   "parallelism": f"poses x{world} (no data-path collective)",
+                   "pipelining": f"{n_streams} HIP streams, consecutive poses round-robin, "
+                                 "one signal buffer per stream"},
+        "roofline": roofline(w, timer, dt),
+    })
+    return res
+
+
+def bench_ray_shard(args, w, world, rank, dev):
+    from avr_amd import AVRRender, spectrum_to_ir
+    from avr_amd.parallel import RayShardedRender, shard_range
+
+    B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
+    dt = torch.float16 if w.signal_dtype == "float16" else torch.float32
+    r0, r1 = shard_range(R, rank, world)
+    Rl = r1 - r0
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    attn = (torch.rand(B, Rl * S, 1, device=dev, generator=gen) * 2).to(dt)
+    signal = (torch.randn(B, Rl * S, T, device=dev, generator=gen) * 0.1).to(dt)
+    # every rank renders the same poses (one pose, its rays split)
+    pg = torch.Generator(device=dev).manual_seed(4321)
+    P = args.poses
+    rays_o, tx, dtx = _poses(w, P, dev, pg)
+    renderer = AVRRender(StubNet(attn, signal), **w.render)
+    timer = KernelTimer(args.steps)
+    renderer.kernel_timer = timer
+    sharded = RayShardedRender(renderer)
+    pose = [0]
+
+    def step():
+        i = pose[0] % P
+        pose[0] += 1
+        with torch.no_grad():
+            out = sharded(rays_o[i], tx[i], dtx[i])
+            return out, spectrum_to_ir(out)
+
+    def run(n):
+        for _ in range(n):
+            step()
+
+    torch.manual_seed(7)  # same CPU jitter stream on every rank
+    run(args.warmup)
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps, args.streams)
-    t_issue = time.perf_counter() - t0
+    timer.enabled = True
+    run(args.steps)
     torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
+    timer.enabled = False
+    elapsed, t_issue = timed(lambda: run(args.steps), world, dev)
+    value = whole_job_rate(w.ray_samples, 1, args.steps, elapsed)  # one pose per step, all ranks
+    res = _base_result(args, w, world, value, elapsed, "f32" if dt == torch.float32 else "f16-storage/f32-math")
+    rf = roofline(w, timer, dt)
+    res.update({
+        "scaling": "strong",
+        "ir_render_ms_per_pose": elapsed * 1e3 / args.steps,
+        "host_issue_ms_per_step": t_issue * 1e3 / args.steps,
+        "config": {"workload": w.name, "mode": "ray-shard", "rays": R, "rays_per_rank": Rl, "samples": S,
+                   "T": T, "freq_bins": w.F, "poses_per_step": B,
+                   "parallelism": f"rays x{world}, one RCCL all-reduce of the [B,F,2] spectrum per pose"},
+        "roofline": rf,
+    })
+    return res
+
+
+def bench_ddp_train(args, w, world, rank, dev):
+    from avr_amd import AVRRender
+    from avr_amd.model import AVRModel_complex
+    from avr_amd.parallel import ddp
+    from avr_amd.training import TrainStep
+    from avr_amd.workloads import RAF_MODEL
+
+    B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
+    mlp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.mlp_dtype]
+    torch.manual_seed(0)  # identical initial weights on every rank (DDP also broadcasts them)
+    model = AVRModel_complex(dict(RAF_MODEL, signal_output_dim=T), mlp_dtype=mlp_dtype).to(dev)
+    r = AVRRender(model, **w.render).to(dev)
+    net = ddp(r, dev) if world > 1 else r
+    # RAF training config (config_files/avr_raf_*.yml:24-40)
+    train_cfg = dict(lr=2e-4, weight_decay=0, T_max=300000, eta_min=8e-5,
+                     spec_loss_weight=1, amplitude_loss_weight=1, angle_loss_weight=1,
+                     time_loss_weight=20, energy_loss_weight=3, multistft_loss_weight=2)
+    ts = TrainStep(net, train_cfg, w.render)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)  # each rank its own pose shard
+    P = max(1, min(args.poses, 4))
+    rays_o, tx, dtx = _poses(w, P, dev, g)
+    tt = torch.arange(T, device=dev)
+    targets = [torch.fft.rfft(torch.randn(B, T, device=dev, generator=g) * torch.exp(-tt / (0.15 * T)) * 0.05)
+               for _ in range(P)]
+    it = [0]
+
+    def step():
+        i = it[0] % P
+        it[0] += 1
+        ts(targets[i], rays_o[i], tx[i], dtx[i])
+
+    def run(n):
+        for _ in range(n):
+            step()
+
+    torch.manual_seed(rank)
+    run(args.warmup)
+    torch.cuda.synchronize()
+    elapsed, t_issue = timed(lambda: run(args.steps), world, dev)
+    value = whole_job_rate(w.ray_samples, world, args.steps, elapsed)
+    n_params = sum(p.numel() for p in r.parameters())
+    res = _base_result(args, w, world, value, elapsed, args.mlp_dtype + " MLP / f32 render")
+    res.update({
+        "data": "synthetic poses and decaying-noise target IRs; random-init AVRModel_complex (RAF widths)",
+        "host_issue_ms_per_step": t_issue * 1e3 / args.steps,
+        "config": {"workload": w.name, "mode": "ddp-train", "rays": R, "samples": S, "T": T,
+                   "freq_bins": w.F, "poses_per_rank": B, "global_batch": B * world,
+                   "model": "AVRModel_complex (6 hash grids, RAF MLP widths)",
+                   "params": n_params, "grad_allreduce_bytes": 4 * n_params if world > 1 else 0,
+                   "parallelism": f"dp{world} (DDP, RCCL bucketed gradient all-reduce)"},
+        "roofline": None,
+    })
+    return res
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    what, n = resolve_world(args)
+    if what == "launch":
+        # start the ranks as children (never exec from this process)
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        return subprocess.call(launch_command(n, argv, free_port()), env=env)
+    world = n
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
 
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        dist.init_process_group("nccl", device_id=dev)
+        world = dist.get_world_size()
 
-    ms_per_step = elapsed * 1e3 / args.steps
-    total_rs = world * w.ray_samples * args.steps
-    value = total_rs / elapsed
+    from avr_amd.workloads import WORKLOADS
 
-    # roofline for the dominant kernel (ray-reduction stream)
-    k_ms = timer.mean_ms()
-    es = 2 if dt == torch.float16 else 4
-    n_split = timer.n_split or 1
-    # algorithmic bytes: the live signal elements (each read once), w + delay
-    # (8 B per ray-sample), the fp32 partials written; the dense tensor is
-    # reported beside it
-    live = timer.mean_live_elements(T)
-    alg_bytes = live * es + w.ray_samples * 8 + n_split * B * S * T * 4
-    dense_bytes = w.ray_samples * (T * es + 8) + n_split * B * S * T * 4
-    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
-
-    traffic, traffic_src = pmc_traffic(w.name, "__half" if dt == torch.float16 else "float")
-
-    result = {
-        "metric": "ray-samples/sec/GPU (1024 rays×256 samp×512 freq) + IR render ms/pose",
-        "value": value,
-        "unit": "ray-samples/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": ms_per_step,
-        "ir_render_ms_per_pose": latency_ms / B,
-        "host_issue_ms_per_step": t_issue * 1e3 / args.steps,
-        "streams": args.streams,
-        "per_gpu_value": value / world,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32" if dt == torch.float32 else "f16-storage/f32-math",
-        "data": "synthetic (stub network, outputs resident in HBM; seeded torch RNG)",
-        "config": {"workload": w.name, "rays": R, "samples": S, "T": T, "freq_bins": w.F,
-                   "poses_per_step": B, "distinct_poses": P, "parallelism": f"poses x{world} (no data-path collective)",
-                   "pipelining": f"{args.streams} HIP streams, consecutive poses round-robin"},
-        "roofline": {
-            "kernel": "ray_reduce_fwd_kernel",
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "traffic_source": traffic_src,
-            "alg_bytes_per_launch": alg_bytes,
-            "dense_bytes_per_launch": dense_bytes,
-            "live_fraction": live / (w.ray_samples * T),
-            "avg_launch_ms": k_ms,
-            "measured": "HIP events around each launch, roofline phase of K steps on one stream",
-        },
-
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    w = WORKLOADS[args.workload]
+    fn = {"pose": bench_pose, "ray-shard": bench_ray_shard, "ddp-train": bench_ddp_train}[args.mode]
+    result = fn(args, w, world, rank, dev)
+    if rank == 0 and world == 1 and args.mode == "pose" and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(w, args.cpu_budget)
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -309,7 +542,8 @@ def main():
         import torch.distributed as dist
 
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from avr_amd.parallel import allreduce_spectrum, broadcast_jitter, shard_range
+from avr_amd.parallel import allreduce_grads_sum, allreduce_spectrum, broadcast_jitter, shard_range
 from avr_amd.workloads import WORKLOADS, make_inputs
 
 
@@ -137,3 +137,63 @@ def test_ddp_helper_allreduces_pose_shard_grads_gloo():
     # DDP averages over ranks: mean of the two shard gradients
     for g in out.values():
         torch.testing.assert_close(torch.tensor(g), ref.weight.grad / 2, rtol=1e-5, atol=1e-6)
+
+
+def _ray_grad_worker(rank, world, port, q):
+    """Ray-sharded TRAINING: parameter gradients summed over ranks equal the
+    unsharded render's gradient (the loss on the all-reduced spectrum is
+    replicated; each rank's backward covers only its own rays)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from oracle import avr_oracle as orc
+
+        w = WORKLOADS["c1_meshrir_plumbing"]
+        inp = make_inputs(w, 1)
+        R, S, T = w.n_rays, w.n_samples, w.T
+        cfg = orc.RenderConfig.from_kwargs(**w.render)
+        base = torch.from_numpy(inp["signal"]).reshape(1, R, S, T)
+        attn0 = torch.from_numpy(inp["attn"])
+        g = torch.randn(1, T // 2 + 1, 2, generator=torch.Generator().manual_seed(5))
+
+        def loss_and_grads(mask_rays):
+            scale = torch.nn.Parameter(torch.linspace(0.5, 1.5, T))
+            gain = torch.nn.Parameter(torch.tensor(1.25))
+            sig = base * scale * mask_rays.view(1, R, 1, 1)
+            torch.manual_seed(1)
+            out = orc.render_spectrum(cfg, orc.StubNetwork(attn0 * gain, sig.reshape(1, R * S, T)),
+                                      torch.from_numpy(inp["rays_o"]), torch.from_numpy(inp["position_tx"]))
+            return out, (scale, gain)
+
+        r0, r1 = shard_range(R, rank, world)
+        m = torch.zeros(R)
+        m[r0:r1] = 1
+        part, params = loss_and_grads(m)
+        full = allreduce_spectrum(part)
+        (full * g).sum().backward()
+        allreduce_grads_sum(params)
+        ref, rparams = loss_and_grads(torch.ones(R))
+        (ref * g).sum().backward()
+        q.put((rank, [float((p.grad - rp.grad).abs().max() / rp.grad.abs().max().clamp(min=1e-30))
+                      for p, rp in zip(params, rparams)]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ray_sharded_param_grads_sum_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ray_grad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, errs in out.items():
+        assert max(errs) < 1e-5, (rank, errs)

@@ -44,3 +44,42 @@ def test_graph_replay_equals_eager(name):
         assert torch.equal(out_g, out_e), k
         assert torch.equal(ir_g, ir_e), k
     assert len(gr._graphs) == 1
+
+
+@pytest.mark.parametrize("mlp_dtype", [torch.bfloat16, torch.float32])
+def test_graph_replay_sees_optimizer_step_avrmodel(mlp_dtype):
+    """The package's own network captured (cast/packed-weight caches bypassed
+    while capturing): after an in-place Adam step the replay renders with the
+    NEW weights, equal to the eager render, and no re-capture happens."""
+    from avr_amd.model import AVRModel
+    from avr_amd.workloads import MESHRIR, MESHRIR_MODEL
+
+    cfg = dict(MESHRIR, n_azi=16, n_ele=8, n_samples=64)
+    torch.manual_seed(0)
+    m = AVRModel(dict(MESHRIR_MODEL, signal_output_dim=1022), mlp_dtype=mlp_dtype).to(DEV)
+    r = AVRRender(m, **cfg).to(DEV)
+    gr = GraphedRender(r)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    ro = torch.rand(1, 3, device=DEV, generator=g) * 2 - 1
+    tx = ro + 0.5  # close source: live windows inside T
+
+    def both(seed):
+        with torch.no_grad():
+            torch.manual_seed(seed)
+            e = r.render_ir(ro, tx)[0].clone()
+            torch.manual_seed(seed)
+            gg = gr.render_ir(ro, tx)[0].clone()
+        torch.cuda.synchronize()
+        return e, gg
+
+    e0, g0 = both(5)
+    assert e0.abs().max() > 0
+    torch.testing.assert_close(g0, e0, rtol=1e-5, atol=1e-6)
+    opt = torch.optim.Adam(r.parameters(), lr=1e-2)
+    torch.manual_seed(5)
+    r(ro, tx).square().sum().backward()
+    opt.step()
+    e1, g1 = both(5)
+    assert (e1 - e0).abs().max() > 1e-4 * e0.abs().max()  # the step changed the render
+    torch.testing.assert_close(g1, e1, rtol=1e-5, atol=1e-6)
+    assert len(gr._graphs) == 1

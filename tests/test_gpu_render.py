@@ -349,3 +349,46 @@ def test_reduced_precision_storage_matches_oracle_on_rounded_inputs(dtype):
     gs, gs32 = sgn.grad.float().cpu().numpy(), s32.grad.cpu().numpy()
     tol = 2e-2 if dtype == torch.bfloat16 else 3e-3
     assert rel_l2(gs, gs32) < tol
+
+
+def _nan_render(inp, w, seed, edit=None, **kw):
+    sig = torch.from_numpy(inp["signal"]).to(DEV).clone()
+    attn = torch.from_numpy(inp["attn"]).to(DEV).clone()
+    if edit is not None:
+        edit(attn, sig)
+    r = AVRRender(Net(attn, sig), **w.render, **kw)
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        return r(torch.from_numpy(inp["rays_o"]).to(DEV), torch.from_numpy(inp["position_tx"]).to(DEV))
+
+
+def test_nonfinite_semantics():
+    """Masked-region NaN/Inf (whole 16-byte chunks outside [delay, T-1-shift))
+    is never loaded: the spectrum is exactly the clean one (the reference
+    would give NaN, renderer.py:82,89).  A NaN in the live window gives NaN as
+    in the reference.  propagate_nonfinite=True reproduces the reference in
+    both cases ('Non-finite network outputs')."""
+    case = Case("c1_s1")
+    w, inp = case.workload, case.inputs()
+    R, S, T = w.n_rays, w.n_samples, w.T
+    delay, shift = case["delay"][0].astype(int), case["shift"].astype(int)
+    assert delay.min() >= 4 and (shift >= 4).any()
+    s_tail = int(np.nonzero(shift >= 4)[0][0])
+    live = [(r, s) for r in range(R) for s in range(S) if delay[r, s] < T - 1 - shift[s]]
+    assert live
+    r_live, s_live = live[len(live) // 2]
+
+    def masked(attn, sig):
+        sig[0, 5 * S + 7, 0] = float("nan")          # t=0 < delay: a fully masked chunk
+        sig[0, 9 * S + s_tail, T - 1] = float("inf")  # t >= T-1-shift: fully masked tail chunk
+
+    def live_nan(attn, sig):
+        sig[0, r_live * S + s_live, delay[r_live, s_live]] = float("nan")
+
+    clean = _nan_render(inp, w, case.seed)
+    assert torch.isfinite(clean).all()
+    assert torch.equal(_nan_render(inp, w, case.seed, masked), clean)
+    assert torch.isnan(_nan_render(inp, w, case.seed, live_nan)).any()
+    strict = _nan_render(inp, w, case.seed, masked, propagate_nonfinite=True)
+    assert torch.isnan(strict).all()
+    assert torch.equal(_nan_render(inp, w, case.seed, None, propagate_nonfinite=True), clean)

@@ -21,6 +21,10 @@ for s in "$@"; do
     tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
+    modes) step bench_rayshard 300 python bench.py --mode ray-shard --steps 20 --warmup 3 --poses 4 \
+           && step bench_ddp 300 python bench.py --mode ddp-train --steps 10 --warmup 3 \
+           && step bench_gpus2 120 python bench.py --gpus 2 --steps 5 ;;
+    newtests) step pytest_new 600 python -u -m pytest tests/test_gpu_dist2.py tests/test_gpu_reentrancy.py tests/test_gpu_graph.py "tests/test_gpu_render.py::test_nonfinite_semantics" -q -rf --timeout 120 --timeout-method thread ;;
     benchq) step bench_q 300 python bench.py --no-cpu-baseline --steps 100 ;;
     streams) step bench_s1 200 python bench.py --no-cpu-baseline --steps 200 --streams 1 && step bench_s2 200 python bench.py --no-cpu-baseline --steps 200 --streams 2 && step bench_s3 200 python bench.py --no-cpu-baseline --steps 200 --streams 3 ;;
     tune) step tune 600 python tools/tune.py ;;

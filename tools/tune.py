@@ -19,7 +19,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from avr_amd import AVRRender, spectrum_to_ir  # noqa: E402
-from avr_amd import renderer as rmod  # noqa: E402
 from avr_amd.workloads import WORKLOADS  # noqa: E402
 from bench import KernelTimer, StubNet  # noqa: E402
 
@@ -63,7 +62,7 @@ def main():
     dtx = torch.nn.functional.normalize(torch.randn(B, 3, device=dev, generator=g), dim=-1) if w.with_dir_tx else None
     r = AVRRender(StubNet(attn, sig), **w.render)
     timer = KernelTimer(args.steps)
-    rmod.KERNEL_TIMER = timer
+    r.kernel_timer = timer
     combos = list(itertools.product(args.variants.split(","), [int(x) for x in args.nsplit.split(",")],
                                     [int(x) for x in args.ksplit.split(",")]))
     res = {c: {"step": [], "reduce": []} for c in combos}
