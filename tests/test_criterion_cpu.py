@@ -2,10 +2,13 @@
 independent numpy statement of the same transforms, and the product
 criterion's host-side contract (no compute without a GPU).
 
-The restatement cannot be pinned to the running reference (criterion.py
-imports auraloss, absent here): these tests pin its reading of torch.stft's
-conventions (centre reflect padding, a short window centred in n_fft, hop
-defaults, one-sided bins) and of the loss formulas instead."""
+Every term except the MR-STFT one (and the gradient of their sum) is
+pinned to golden vectors of the reference's own utils/criterion.py
+(tests/golden/criterion, tools/gen_criterion_golden.py).  The MR-STFT term
+cannot be (auraloss is absent here): for it these tests pin the
+restatement's reading of torch.stft's conventions (centre reflect padding, a
+short window centred in n_fft, hop defaults, one-sided bins) and of the loss
+formulas."""
 import numpy as np
 import pytest
 import torch
@@ -112,3 +115,30 @@ def test_product_criterion_refuses_cpu_tensors():
     x = torch.zeros(1, 257, dtype=torch.complex64)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         crit(x, x)
+
+
+@pytest.mark.parametrize("name", [c[0] for c in __import__("criterion_cases").CASES])
+def test_oracle_matches_reference_criterion_golden(name):
+    """The restatement against golden vectors of the reference's own
+    utils/criterion.py (tools/gen_criterion_golden.py): every term except the
+    auraloss MR-STFT one, and the gradient of their sum."""
+    import os
+
+    from criterion_cases import CASES, RENDER, spectra
+
+    case = {c[0]: c for c in CASES}[name]
+    _, B, F, weights, seed = case
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "criterion",
+                             f"crit_{name}.npz"))
+    pred, ori = spectra(B, F, seed)
+    p = pred.clone().requires_grad_(True)
+    o = co.criterion(p, ori, weights)
+    terms = list(o[:5]) + list(co.das_losses(p, ori, RENDER["fs"], RENDER["speed"],
+                                             weights.get("das_reg_loss_weight", 0.0),
+                                             weights.get("das_ce_loss_weight", 0.0),
+                                             weights.get("beta", 100.0)))
+    np.testing.assert_allclose([float(x) for x in terms], z["losses"], rtol=1e-6, atol=1e-9)
+    np.testing.assert_array_equal(o[6].numpy(), z["ori_time"])
+    np.testing.assert_array_equal(o[7].detach().numpy(), z["pred_time"])
+    sum(terms).backward()
+    np.testing.assert_allclose(torch.view_as_real(p.grad).numpy(), z["grad"], rtol=1e-5, atol=1e-9)
