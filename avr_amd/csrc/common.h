@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 #include <hip/hip_bf16.h>
+#include <type_traits>
 #include <stdint.h>
 #include <string>
 
@@ -47,6 +48,29 @@ __device__ __forceinline__ void store_f(__hip_bfloat16* p, int64_t i, float v) {
 // bf16 pair packed in a dword -> two floats (exact)
 __device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+// fp16 pair packed in a dword -> two floats (exact)
+__device__ __forceinline__ float f16_lo(uint32_t u) { return __half2float(__ushort_as_half((unsigned short)(u & 0xffffu))); }
+__device__ __forceinline__ float f16_hi(uint32_t u) { return __half2float(__ushort_as_half((unsigned short)(u >> 16))); }
+
+// element k of a dword-packed row of 16-bit values of type T (fp16 or bf16)
+template <typename T>
+__device__ __forceinline__ float unpack16(uint32_t u, int hi) {
+    if constexpr (std::is_same<T, __half>::value)
+        return hi ? f16_hi(u) : f16_lo(u);
+    else
+        return hi ? bf16_hi(u) : bf16_lo(u);
+}
+// two floats -> a dword of two 16-bit values of type T (round to nearest even)
+template <typename T>
+__device__ __forceinline__ uint32_t pack16(float a, float b) {
+    if constexpr (std::is_same<T, __half>::value) {
+        return (uint32_t)__half_as_ushort(__float2half(a)) | ((uint32_t)__half_as_ushort(__float2half(b)) << 16);
+    } else {
+        const __hip_bfloat16 x = __float2bfloat16(a), y = __float2bfloat16(b);
+        return (uint32_t)(*reinterpret_cast<const uint16_t*>(&x)) |
+               ((uint32_t)(*reinterpret_cast<const uint16_t*>(&y)) << 16);
+    }
+}
 
 // 16-byte vectors of signal elements as floats: 4 x fp32 or 8 x fp16/bf16.
 // load() is non-temporal (the signal is streamed once per pass and should

@@ -66,7 +66,7 @@ struct Raw {
     }
     __device__ __forceinline__ float operator[](int k) const {
         if constexpr (sizeof(Th) == 2)
-            return (k & 1) ? bf16_hi(d[k >> 1]) : bf16_lo(d[k >> 1]);
+            return unpack16<Th>(d[k >> 1], k & 1);
         else
             return __uint_as_float(d[k]);
     }
@@ -77,12 +77,7 @@ __device__ __forceinline__ void store_block(Th* p, const float* v) {
     if constexpr (sizeof(Th) == 2) {
         uint32_t u[KB / 2];
 #pragma unroll
-        for (int i = 0; i < KB / 2; ++i) {
-            const __hip_bfloat16 a = __float2bfloat16(v[2 * i]);
-            const __hip_bfloat16 b = __float2bfloat16(v[2 * i + 1]);
-            u[i] = (uint32_t)(*reinterpret_cast<const uint16_t*>(&a)) |
-                   ((uint32_t)(*reinterpret_cast<const uint16_t*>(&b)) << 16);
-        }
+        for (int i = 0; i < KB / 2; ++i) u[i] = pack16<Th>(v[2 * i], v[2 * i + 1]);
         if constexpr (KB >= 8) {
 #pragma unroll
             for (int c = 0; c < KB / 8; ++c)
@@ -489,8 +484,8 @@ __global__ __launch_bounds__(kThreads) void head_pack_w_kernel(int T, int K, int
 // them in flight).
 //
 // SB > 1: each ray's h is loaded SB feature blocks at a time (64 bytes for
-// bf16 with SB = 2), the next such super-block in flight under the current
-// one's SB blocks.  A 128-byte line of a row holds 64 bf16 features: loaded
+// 16-bit h with SB = 2), the next such super-block in flight under the current
+// one's SB blocks.  A 128-byte line of a row holds 64 16-bit features: loaded
 // one 32-byte block at a time it is requested 4 times, spread over 4 block
 // iterations, and with ~64 workgroups per XCD each holding 1024 such lines
 // it has left L2 by then (PMC: 1.08 GB fetched for the 268 MB h at config 2).
@@ -579,7 +574,7 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp
 }
 
 // ------------------------------------------------- backward: dL/dh, dL/dw
-// SB > 1 (bf16): each ray's h is loaded and its grad_h stored SB feature
+// SB > 1 (16-bit h): each ray's h is loaded and its grad_h stored SB feature
 // blocks at a time (32 bytes per row for SB = 2) instead of 16 bytes per
 // block; the grad_h of the SB blocks waits packed in registers.
 template <typename Th, int KB, int NT, int RPT, int SB = 1>
@@ -681,10 +676,7 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
                         const float q1 = live ? Q[(k + 1) * QS + d] : 0.0f;
                         acc = fmaf(hv[u][sb * KB + k], q0, acc);
                         acc = fmaf(hv[u][sb * KB + k + 1], q1, acc);
-                        const __hip_bfloat16 a0 = __float2bfloat16(live ? wr * q0 : 0.0f);
-                        const __hip_bfloat16 a1 = __float2bfloat16(live ? wr * q1 : 0.0f);
-                        ghp[u][sb * KB / 2 + k / 2] = (uint32_t)(*reinterpret_cast<const uint16_t*>(&a0)) |
-                                                      ((uint32_t)(*reinterpret_cast<const uint16_t*>(&a1)) << 16);
+                        ghp[u][sb * KB / 2 + k / 2] = pack16<Th>(live ? wr * q0 : 0.0f, live ? wr * q1 : 0.0f);
                     }
                     if (live) gw[u] = acc;
                 }
@@ -850,10 +842,12 @@ void allow_lds(Kern k, size_t lds) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
 }
 
+int elem_size(int dtype) { return dtype == AVR_DTYPE_F32 ? 4 : 2; }
+
 int head_check(const avr_render_params* p, int B, int K, const void* h, const void* W, int dtype) {
     AVR_REQUIRE(p && B >= 1 && K >= 4 && h && W, "fused head: bad args");
-    AVR_REQUIRE(dtype == AVR_DTYPE_F32 || dtype == AVR_DTYPE_BF16,
-                "fused head: h/W must be fp32 or bf16");
+    AVR_REQUIRE(dtype == AVR_DTYPE_F32 || dtype == AVR_DTYPE_BF16 || dtype == AVR_DTYPE_F16,
+                "fused head: h/W must be fp32, bf16 or fp16");
     AVR_REQUIRE(reinterpret_cast<uintptr_t>(h) % 16 == 0 && reinterpret_cast<uintptr_t>(W) % 16 == 0,
                 "fused head: h and W must be 16-byte aligned");
     return 0;
@@ -875,7 +869,7 @@ void dw_groups(const HeadShape& hs, int B, int S, int K, int* n_sg, int* s_per) 
 // the render with the head.  AVR_HEAD_KB / AVR_HEAD_SB override (experiments).
 void fwd_block(const HeadShape& hs, int dtype, int* kb, int* sb) {
     int kbf = hs.kb, s = 1;
-    if (dtype == AVR_DTYPE_BF16 && hs.rpt <= 8) {
+    if (elem_size(dtype) == 2 && hs.rpt <= 8) {
         kbf = hs.kb > 8 ? 8 : hs.kb;
         s = hs.nt <= 4 ? 4 : 2;
         if (const char* e = getenv("AVR_HEAD_KB")) kbf = atoi(e);
@@ -894,7 +888,7 @@ extern "C" int avr_head_pack_w(const avr_render_params* p, int32_t B, int32_t K,
     if (int e = head_check(p, B, K, W, W, dtype)) return e;
     AVR_REQUIRE(Wp && reinterpret_cast<uintptr_t>(Wp) % 16 == 0, "avr_head_pack_w: Wp must be 16-byte aligned");
     HeadShape hs;
-    if (int e = head_shape(*p, B, n_rays(*p), K, dtype == AVR_DTYPE_BF16 ? 2 : 4, &hs)) return e;
+    if (int e = head_shape(*p, B, n_rays(*p), K, elem_size(dtype), &hs)) return e;
     int kbf, sb;
     fwd_block(hs, dtype, &kbf, &sb);
     const int T = p->T;
@@ -904,6 +898,9 @@ extern "C" int avr_head_pack_w(const avr_render_params* p, int32_t B, int32_t K,
     if (dtype == AVR_DTYPE_BF16)
         hipLaunchKernelGGL(head_pack_w_kernel<__hip_bfloat16>, dim3(blocks), dim3(kThreads), 0, st, T, (int)K, kbf,
                            (const __hip_bfloat16*)W, (__hip_bfloat16*)Wp);
+    else if (dtype == AVR_DTYPE_F16)
+        hipLaunchKernelGGL(head_pack_w_kernel<__half>, dim3(blocks), dim3(kThreads), 0, st, T, (int)K, kbf,
+                           (const __half*)W, (__half*)Wp);
     else
         hipLaunchKernelGGL(head_pack_w_kernel<float>, dim3(blocks), dim3(kThreads), 0, st, T, (int)K, kbf,
                            (const float*)W, (float*)Wp);
@@ -914,7 +911,7 @@ extern "C" int avr_head_splits(const avr_render_params* p, int32_t B, int32_t K,
                                int32_t* n_split) {
     AVR_REQUIRE(p && n_split, "avr_head_splits: bad args");
     HeadShape hs;
-    const int es = dtype == AVR_DTYPE_BF16 ? 2 : 4;
+    const int es = elem_size(dtype);
     if (int e = head_shape(*p, B, n_rays(*p), K, es, &hs)) return e;
     *n_split = hs.n_kg;
     return 0;
@@ -948,7 +945,7 @@ extern "C" int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, co
     AVR_REQUIRE(perm && ws && cnt && zpart, "avr_head_fwd: bad args");
     const int R = n_rays(*p);
     HeadShape hs;
-    if (int e = head_shape(*p, B, R, K, dtype == AVR_DTYPE_BF16 ? 2 : 4, &hs)) return e;
+    if (int e = head_shape(*p, B, R, K, elem_size(dtype), &hs)) return e;
     AVR_REQUIRE(n_split == hs.n_kg, "avr_head_fwd: n_split must come from avr_head_splits");
     const dim3 grid(hs.n_kg, p->n_samples, B);
     hipStream_t st = as_stream(stream);
@@ -980,6 +977,8 @@ extern "C" int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, co
     AVR_HF_R(TH, 16, 4)
     if (dtype == AVR_DTYPE_BF16) {
         AVR_HF_ALL(__hip_bfloat16)
+    } else if (dtype == AVR_DTYPE_F16) {
+        AVR_HF_ALL(__half)
     } else {
         AVR_HF_ALL(float)
     }
@@ -994,12 +993,12 @@ extern "C" int avr_head_bwd_workspace(const avr_render_params* p, int32_t B, int
     AVR_REQUIRE(p && bytes, "avr_head_bwd_workspace: bad args");
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
     HeadShape hs;
-    if (int e = head_shape(*p, B, R, K, dtype == AVR_DTYPE_BF16 ? 2 : 4, &hs)) return e;
+    if (int e = head_shape(*p, B, R, K, elem_size(dtype), &hs)) return e;
     int n_sg, s_per;
     dw_groups(hs, B, S, K, &n_sg, &s_per);
     // fp32 partials, then W packed in the backward's feature blocks (16-B aligned)
     *bytes = ((int64_t)hs.n_kg * B * R * S + (int64_t)B * n_sg * T * K) * 4 + 16 +
-             (int64_t)T * K * (dtype == AVR_DTYPE_BF16 ? 2 : 4);
+             (int64_t)T * K * (elem_size(dtype));
     return 0;
 }
 
@@ -1013,12 +1012,12 @@ extern "C" int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, co
                 "avr_head_bwd: bad args");
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
     HeadShape hs;
-    if (int e = head_shape(*p, B, R, K, dtype == AVR_DTYPE_BF16 ? 2 : 4, &hs)) return e;
+    if (int e = head_shape(*p, B, R, K, elem_size(dtype), &hs)) return e;
     int n_sg, s_per;
     dw_groups(hs, B, S, K, &n_sg, &s_per);
     const int64_t gw_elems = (int64_t)hs.n_kg * B * R * S;
     const int64_t gW_elems = (int64_t)B * n_sg * T * K;
-    const int64_t es = dtype == AVR_DTYPE_BF16 ? 2 : 4;
+    const int64_t es = elem_size(dtype);
     if (workspace_bytes < (gw_elems + gW_elems) * 4 + 16 + (int64_t)T * K * es)
         return fail(AVR_E_ARG, "avr_head_bwd: workspace too small");
     float* gw_part = workspace;
@@ -1033,13 +1032,16 @@ extern "C" int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, co
         if (dtype == AVR_DTYPE_BF16)
             hipLaunchKernelGGL(head_pack_w_kernel<__hip_bfloat16>, dim3(blocks), dim3(kThreads), 0, st, T,
                                (int)K, hs.kb, (const __hip_bfloat16*)W, (__hip_bfloat16*)Wb);
+        else if (dtype == AVR_DTYPE_F16)
+            hipLaunchKernelGGL(head_pack_w_kernel<__half>, dim3(blocks), dim3(kThreads), 0, st, T,
+                               (int)K, hs.kb, (const __half*)W, (__half*)Wb);
         else
             hipLaunchKernelGGL(head_pack_w_kernel<float>, dim3(blocks), dim3(kThreads), 0, st, T, (int)K, hs.kb,
                                (const float*)W, (float*)Wb);
     }
     // 16-bit h: h loads / grad_h stores 2 feature blocks (32 B) per row
     // (AVR_HEAD_BSB=1 restores one block; experiments)
-    int bsb = (dtype == AVR_DTYPE_BF16 && hs.kg % (2 * hs.kb) == 0) ? 2 : 1;
+    int bsb = (elem_size(dtype) == 2 && hs.kg % (2 * hs.kb) == 0) ? 2 : 1;
     if (const char* e = getenv("AVR_HEAD_BSB")) bsb = (atoi(e) == 2 && hs.kg % (2 * hs.kb) == 0) ? 2 : 1;
     auto go_h = [&](auto kern, auto hp, auto wp, auto gp) {
         allow_lds(kern, hs.lds_q);
@@ -1069,6 +1071,8 @@ extern "C" int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, co
     AVR_HB_R(TH, 16, 4)
     if (dtype == AVR_DTYPE_BF16) {
         AVR_HB_ALL(__hip_bfloat16)
+    } else if (dtype == AVR_DTYPE_F16) {
+        AVR_HB_ALL(__half)
     } else {
         AVR_HB_ALL(float)
     }

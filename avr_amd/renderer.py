@@ -575,12 +575,12 @@ class AVRRender(nn.Module):
 
     def _head_supported(self, geom, h, weight, dtype):
         """Whether the fused-head kernels take this shape (T <= 4096, <= 4096
-        rays per shard, the LDS budget, fp32/bf16); otherwise the network
+        rays per shard, the LDS budget, fp32/bf16/fp16); otherwise the network
         applies its last layer and the plain path renders."""
-        if dtype not in (torch.float32, torch.bfloat16):
+        if dtype not in (torch.float32, torch.bfloat16, torch.float16):
             return False
         p = render_params(self._cfg, weight.size(0), n_rays=geom["n_rays"])
-        code = DTYPE_BF16 if dtype == torch.bfloat16 else DTYPE_F32
+        code = {torch.bfloat16: DTYPE_BF16, torch.float16: DTYPE_F16}.get(dtype, DTYPE_F32)
         n = ctypes.c_int32(0)
         return _lib.load().avr_head_splits(ctypes_ref(p), geom["B"], h.size(-1), code,
                                            ctypes.byref(n)) == 0

@@ -63,7 +63,7 @@ def _fused(case, dtype, ops=None):
     return out.detach(), a1.grad, h1.grad, W1.grad
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
 def test_fused_head_matches_oracle(case, dtype):
     """Fused head against the CPU oracle (the reference's algorithm) on
@@ -92,7 +92,7 @@ def test_fused_head_matches_oracle(case, dtype):
     assert _rel(gW_f.cpu(), gW_ref) < 1e-3, (name, "W", _rel(gW_f.cpu(), gW_ref))
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
 def test_fused_head_bitwise_reproducible(case, dtype):
     """Two renders (forward + backward) of the same operands are identical."""
@@ -103,7 +103,7 @@ def test_fused_head_bitwise_reproducible(case, dtype):
         assert torch.equal(x, y), (case[0], what)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
 def test_fused_head_matches_plain_render(case, dtype):
     name, base, n_azi, n_ele, S, T, K, B = case
@@ -174,3 +174,33 @@ def test_fused_head_falls_back_when_unsupported():
     torch.manual_seed(0)
     b = AVRRender(model, fused_head=False, **cfg)(ro, tx, dtx)
     assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("mlp_dtype", [torch.float16, torch.bfloat16])
+def test_fused_head_model_reference_precision(mlp_dtype):
+    """AVRModel_complex with 16-bit MLPs (fp16 is tcnn's precision,
+    model.py:21-31) stays on the fused path and equals the plain render of
+    the layer's exact product h @ W^T on the same 16-bit operands (fp32
+    accumulation, as the fused head sums; rounding that product back to
+    16 bits, as the unfused layer does, would only lose precision)."""
+    cfg = dict(RAF, n_azi=6, n_ele=5, n_samples=32)
+    torch.manual_seed(2)
+    model = AVRModel_complex(dict(RAF_MODEL, signal_output_dim=800), mlp_dtype=mlp_dtype).to(DEV)
+    B = 2
+    g = torch.Generator(device=DEV).manual_seed(12)
+    ro = torch.rand(B, 3, device=DEV, generator=g) * 2 - 1
+    tx = torch.rand(B, 3, device=DEV, generator=g) * 2 - 1
+    dtx = torch.nn.functional.normalize(torch.randn(B, 3, device=DEV, generator=g), dim=-1)
+    r = AVRRender(model, **cfg)
+    with torch.no_grad():
+        torch.manual_seed(3)
+        pts, view, txn, dtxn, geom = r.sample(ro, tx, dtx)
+        attn, h, weight, dtype = model.forward_fused(pts, view, txn, dtxn)
+        assert dtype == mlp_dtype and h.dtype == mlp_dtype and r._head_supported(geom, h, weight, dtype)
+        fused = r.render_from_hidden(attn, h, weight, dtype, geom)
+        sig = h.float() @ weight.to(dtype).float().t()
+        plain = r.render_from_network_output(attn, sig, geom)
+        torch.manual_seed(3)
+        end_to_end = r(ro, tx, dtx)  # the module's forward takes the fused path
+    assert _rel(fused, plain) < 2e-5, _rel(fused, plain)
+    assert torch.equal(end_to_end, fused)
