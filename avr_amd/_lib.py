@@ -51,7 +51,12 @@ class RenderParams(ctypes.Structure):
     ]
 
     def key(self):
-        return tuple(getattr(self, f) for f, _ in self._fields_)
+        """Hashable value of every field (computed once: render_params builds
+        a fresh object and nothing mutates it afterwards)."""
+        k = self.__dict__.get("_key")
+        if k is None:
+            k = self._key = tuple(getattr(self, f) for f, _ in self._fields_)
+        return k
 
 
 def _f32(x) -> float:

@@ -23,7 +23,6 @@ import math
 import os
 import threading
 
-import numpy as np
 import torch
 import torch.nn as nn
 
@@ -59,6 +58,14 @@ def _on(dev):
     """torch.cuda.device(dev), skipped when dev is already current (the
     common case: entering the guard costs more host time than a launch)."""
     return _NO_GUARD if torch.cuda.current_device() == dev.index else torch.cuda.device(dev)
+
+
+def _f32_on(t, dev):
+    """t as a contiguous fp32 tensor on dev (no-op calls skipped: each costs
+    host time on the latency path)."""
+    if t.device != dev or t.dtype != torch.float32:
+        t = t.to(dev, torch.float32)
+    return t if t.is_contiguous() else t.contiguous()
 
 
 def _dtype_code(t):
@@ -491,10 +498,10 @@ class AVRRender(nn.Module):
         p0 = self._params(2, r1 - r0)
         R, S = r1 - r0, p0.n_samples
         f32 = dict(dtype=torch.float32, device=dev)
-        rays_o = rays_o.to(dev, torch.float32).contiguous()
-        position_tx = position_tx.to(dev, torch.float32).contiguous()
+        rays_o = _f32_on(rays_o, dev)
+        position_tx = _f32_on(position_tx, dev)
         if direction_tx is not None:
-            direction_tx = direction_tx.to(dev, torch.float32).contiguous()
+            direction_tx = _f32_on(direction_tx, dev)
         st = _stream(dev)
         pref = ctypes_ref(p0)
         pts = torch.empty(B, R * S, 3, **f32)
@@ -510,9 +517,11 @@ class AVRRender(nn.Module):
                           _ptr(tx), _ptr(dtx), st)
             elif p0.n_azi <= _lib.MAX_AZI:
                 # one fused launch; the jitter travels in the kernel arguments
-                u_host = np.ascontiguousarray(u_azi.detach().cpu().numpy(), dtype=np.float32)
+                u_host = u_azi.detach()
+                if u_host.device.type != "cpu" or u_host.dtype != torch.float32 or not u_host.is_contiguous():
+                    u_host = u_host.to("cpu", torch.float32).contiguous()
                 dirs = torch.empty(R, 3, **f32)
-                _lib.call("avr_sample_rays", pref, B, u_host.ctypes.data, r0, _ptr(rays_o),
+                _lib.call("avr_sample_rays", pref, B, u_host.data_ptr(), r0, _ptr(rays_o),
                           _ptr(position_tx), _ptr(direction_tx), _ptr(dirs), _ptr(pts), _ptr(view),
                           _ptr(tx), _ptr(dtx), st)
             else:
@@ -551,9 +560,17 @@ class AVRRender(nn.Module):
             attn = attn.float()
         if signal.dtype not in native:
             signal = signal.float()
-        attn = attn.to(dev).reshape(B, -1).contiguous()
+        if attn.device != dev:
+            attn = attn.to(dev)
+        attn = attn.reshape(B, -1)
+        if not attn.is_contiguous():
+            attn = attn.contiguous()
         T = signal.size(-1)
-        signal = signal.to(dev).reshape(B, -1, T).contiguous()
+        if signal.device != dev:
+            signal = signal.to(dev)
+        signal = signal.reshape(B, -1, T)
+        if not signal.is_contiguous():
+            signal = signal.contiguous()
         R = geom["n_rays"]
         if attn.size(1) != R * S or signal.size(1) != R * S:
             raise ValueError(f"network output has {signal.size(1)} ray-samples, expected "
@@ -579,7 +596,7 @@ class AVRRender(nn.Module):
         applies its last layer and the plain path renders."""
         if dtype not in (torch.float32, torch.bfloat16, torch.float16):
             return False
-        p = render_params(self._cfg, weight.size(0), n_rays=geom["n_rays"])
+        p = self._params(weight.size(0), geom["n_rays"])
         code = {torch.bfloat16: DTYPE_BF16, torch.float16: DTYPE_F16}.get(dtype, DTYPE_F32)
         n = ctypes.c_int32(0)
         return _lib.load().avr_head_splits(ctypes_ref(p), geom["B"], h.size(-1), code,
@@ -600,8 +617,8 @@ class AVRRender(nn.Module):
         R = geom["n_rays"]
         if attn.size(1) != R * S or h.size(1) != R * S:
             raise ValueError(f"network output has {h.size(1)} ray-samples, expected {R}x{S}={R * S}")
-        p = render_params(self._cfg, T, n_rays=R)
-        with torch.cuda.device(dev):
+        p = self._params(T, R)
+        with _on(dev):
             tables = get_tables(p, dev)
             check_config(p, tables)
             return FusedHeadCore.apply(attn, h, weight, dtype, p, tables, geom["rays_o"],
