@@ -400,16 +400,17 @@ __device__ __forceinline__ float2 encode_point_level(const float* xi, const Tp* 
     return acc;
 }
 
-__device__ __forceinline__ float round_feature(float v, bool f16) {
-    if (f16) v = __half2float(__float2half(v));          // the encoding's output dtype
-    return __bfloat162float(__float2bfloat16(v));         // the MLP's bf16 input
+__device__ __forceinline__ float round_feature(float v, bool f16, bool mlp_f16) {
+    if (f16) v = __half2float(__float2half(v));               // the encoding's output dtype
+    return mlp_f16 ? __half2float(__float2half(v))            // the MLP's 16-bit input
+                   : __bfloat162float(__float2bfloat16(v));
 }
 
 template <typename Tp>
 __global__ __launch_bounds__(256) void ray_pose_bias_kernel(int B, int R, int S, const float* __restrict__ view,
                                                             const float* __restrict__ tx, const Tp* __restrict__ dp,
                                                             LevelTable dl, int dL, const Tp* __restrict__ tp,
-                                                            LevelTable tl, int tL, int f16,
+                                                            LevelTable tl, int tL, int f16, int mlp_f16,
                                                             const float* __restrict__ wd,
                                                             const float* __restrict__ wt, int nout,
                                                             float* __restrict__ bias) {
@@ -425,8 +426,8 @@ __global__ __launch_bounds__(256) void ray_pose_bias_kernel(int B, int R, int S,
         const float* src = which ? tx + b * R * S * 3 : view + (b * R * S + r * S) * 3;
         const float xi[3] = {(src[0] + 1.0f) / 2.0f, (src[1] + 1.0f) / 2.0f, (src[2] + 1.0f) / 2.0f};
         const float2 v = which ? encode_point_level(xi, tp, tl, l) : encode_point_level(xi, dp, dl, l);
-        e[j][which][2 * l] = round_feature(v.x, f16);
-        e[j][which][2 * l + 1] = round_feature(v.y, f16);
+        e[j][which][2 * l] = round_feature(v.x, f16, mlp_f16);
+        e[j][which][2 * l + 1] = round_feature(v.y, f16, mlp_f16);
     }
     __syncthreads();
     for (int o = threadIdx.x; o < nout; o += 256) {
@@ -456,12 +457,14 @@ extern "C" int avr_ray_pose_bias(int32_t B, int32_t R, int32_t S, const float* v
                                  const float* dir_scale, const int32_t* dir_res, int32_t tx_levels,
                                  const void* tx_params, const int64_t* tx_offset, const float* tx_scale,
                                  const int32_t* tx_res, int32_t param_dtype, int32_t enc_dtype,
-                                 const float* w_dir, const float* w_tx, int32_t n_out, float* bias,
-                                 void* stream) {
+                                 int32_t mlp_dtype, const float* w_dir, const float* w_tx, int32_t n_out,
+                                 float* bias, void* stream) {
     AVR_REQUIRE(B >= 1 && R >= 1 && S >= 1 && view && tx && dir_params && tx_params && w_dir && w_tx && bias &&
                     n_out >= 1,
                 "avr_ray_pose_bias: bad args");
     AVR_REQUIRE(enc_dtype == AVR_DTYPE_F16 || enc_dtype == AVR_DTYPE_F32, "avr_ray_pose_bias: enc dtype");
+    AVR_REQUIRE(mlp_dtype == AVR_DTYPE_BF16 || mlp_dtype == AVR_DTYPE_F16, "avr_ray_pose_bias: mlp dtype");
+    const int mlp_f16 = mlp_dtype == AVR_DTYPE_F16;
     LevelTable dl, tl;
     if (int e = make_table(dir_levels, dir_offset, dir_scale, dir_res, &dl)) return e;
     if (int e = make_table(tx_levels, tx_offset, tx_scale, tx_res, &tl)) return e;
@@ -472,11 +475,11 @@ extern "C" int avr_ray_pose_bias(int32_t B, int32_t R, int32_t S, const float* v
     if (param_dtype == AVR_DTYPE_F16)
         hipLaunchKernelGGL(ray_pose_bias_kernel<__half>, grid, dim3(256), 0, st, (int)B, (int)R, (int)S, view, tx,
                            (const __half*)dir_params, dl, (int)dir_levels, (const __half*)tx_params, tl,
-                           (int)tx_levels, f16, w_dir, w_tx, (int)n_out, bias);
+                           (int)tx_levels, f16, mlp_f16, w_dir, w_tx, (int)n_out, bias);
     else if (param_dtype == AVR_DTYPE_F32)
         hipLaunchKernelGGL(ray_pose_bias_kernel<float>, grid, dim3(256), 0, st, (int)B, (int)R, (int)S, view, tx,
                            (const float*)dir_params, dl, (int)dir_levels, (const float*)tx_params, tl,
-                           (int)tx_levels, f16, w_dir, w_tx, (int)n_out, bias);
+                           (int)tx_levels, f16, mlp_f16, w_dir, w_tx, (int)n_out, bias);
     else
         return fail(AVR_E_ARG, "avr_ray_pose_bias: unknown param dtype");
     return check_launch("avr_ray_pose_bias");

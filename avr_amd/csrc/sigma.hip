@@ -31,9 +31,12 @@
 // MFMAs; every wave reads one 16-byte fragment per NT MFMAs with
 // conflict-free ds_read_b128.
 //
-// Rounding is the unfused bf16 path's: fp32 accumulation, bf16 activations
-// (ReLU before or after the rounding is the same), the decoder output rounded
-// to bf16 before leaky_relu (computed in fp32, rounded to bf16) and abs.
+// Rounding is the unfused 16-bit path's: fp32 accumulation, activations in
+// the MLP dtype E (bf16, or fp16 = tcnn's precision, model.py:21-31; ReLU
+// before or after the rounding is the same), the decoder output rounded to E
+// before leaky_relu (computed in fp32, rounded to E) and abs.  Fragments are
+// carried as raw dwords; E only decides the conversions and the MFMA
+// (v_mfma_f32_32x32x16_bf16 / _f16).
 #include "common.h"
 
 using namespace avr;
@@ -41,12 +44,26 @@ using namespace avr;
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef u32x4v frag8;  // 8 packed 16-bit values (one MFMA operand per lane)
+
+// the 16-bit MLP element types: bf16 (__bf16) or fp16 (_Float16)
+template <typename E>
+__device__ __forceinline__ f32x16 mfma16(frag8 a, frag8 b, f32x16 c) {
+    if constexpr (std::is_same<E, _Float16>::value)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b),
+                                                      c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                       c, 0, 0, 0);
+}
 
 constexpr int kChunk = 32768;  // bytes of packed fragments per LDS stage
 constexpr int kFrag = 1024;    // one fragment: 64 lanes x 8 bf16
@@ -66,32 +83,42 @@ struct Args {
     int extra_col[AVR_SIGMA_MAX_EXTRA];
     int extra_width[AVR_SIGMA_MAX_EXTRA];
     const char* wpack;
-    __hip_bfloat16* base;
+    uint16_t* base;  // E bits
     int ldb;
-    __hip_bfloat16* attn;
+    uint16_t* attn;  // E bits
     float slope;
     const float* bias;  // variant 2: per-group bias of the signal network's first layer [rows][512]
     int bias_div;
     int nt_store;       // variant 2: streaming (non-temporal) h1 stores
 };
 
-// two fp32 -> a dword of two bf16 (v_cvt_pk_bf16_f32, round to nearest even)
-__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
-    const bf16x2 p = __builtin_convertvector((f32x2v){a, b}, bf16x2);
-    return __builtin_bit_cast(uint32_t, p);
+// two fp32 -> a dword of two E (round to nearest even)
+template <typename E>
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+    if constexpr (std::is_same<E, _Float16>::value)
+        return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){a, b}, f16x2));
+    else
+        return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2v){a, b}, bf16x2));
 }
+// fp32 -> E -> fp32 (the 16-bit rounding of one value) and its bits
+template <typename E>
+__device__ __forceinline__ float round16(float v) { return (float)(E)v; }
+template <typename E>
+__device__ __forceinline__ uint16_t bits16(float v) { return __builtin_bit_cast(uint16_t, (E)v); }
 
-// ReLU of two packed bf16 (v_pk_max_i16 with 0: a set sign bit is a negative
-// int16).  One VALU op per two values; a NaN with the sign bit set becomes 0.
+// ReLU of two packed 16-bit floats (v_pk_max_i16 with 0: a set sign bit is a
+// negative int16; bf16 and fp16 alike).  One VALU op per two values; a NaN
+// with the sign bit set becomes 0.
 __device__ __forceinline__ float relu(float v) { return v < 0.0f ? 0.0f : v; }  // NaN passes
 
-__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t u) {
+__device__ __forceinline__ uint32_t relu16x2(uint32_t u) {
     const s16x2 r = __builtin_elementwise_max(__builtin_bit_cast(s16x2, u), (s16x2){0, 0});
     return __builtin_bit_cast(uint32_t, r);
 }
 
-// 8 consecutive features (fp16 or fp32) of row `row` starting at `col` -> bf16
-__device__ __forceinline__ bf16x8 load8(const Src& s, int64_t row, int width, int col) {
+// 8 consecutive features (fp16 or fp32) of row `row` starting at `col` -> E
+template <typename E>
+__device__ __forceinline__ frag8 load8(const Src& s, int64_t row, int width, int col) {
     float f[8];
     if (s.lm_rows > 0) {  // feature pairs col/2 .. col/2+3 of the row, one per level plane
 #pragma unroll
@@ -118,10 +145,10 @@ __device__ __forceinline__ bf16x8 load8(const Src& s, int64_t row, int width, in
         f[0] = a[0]; f[1] = a[1]; f[2] = a[2]; f[3] = a[3];
         f[4] = b[0]; f[5] = b[1]; f[6] = b[2]; f[7] = b[3];
     }
-    u32x4v r;
+    frag8 r;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) r[q] = pack_bf16(f[2 * q], f[2 * q + 1]);
-    return __builtin_bit_cast(bf16x8, r);
+    for (int q = 0; q < 4; ++q) r[q] = pack2<E>(f[2 * q], f[2 * q + 1]);
+    return r;
 }
 
 // Cooperative global -> LDS staging of 32 KB chunks into two LDS buffers.
@@ -179,9 +206,9 @@ struct Stager {
 
 // acc[nt][ot] = W X^T for one layer: KS k-steps of input fragments, OT output
 // tiles, CO tiles per LDS chunk.
-template <int NT, int KS, int OT, int CO, class ST>
+template <typename E, int NT, int KS, int OT, int CO, class ST>
 __device__ __forceinline__ void dense(ST& st, int lane,
-                                      const bf16x8 (&x)[NT][KS], f32x16 (&acc)[NT][OT]) {
+                                      const frag8 (&x)[NT][KS], f32x16 (&acc)[NT][OT]) {
     static_assert(OT % CO == 0 && CO * KS * kFrag <= kChunk, "chunk overflow");
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
@@ -195,55 +222,52 @@ __device__ __forceinline__ void dense(ST& st, int lane,
         // k-step outer: the CO*NT accumulators of a k-step are independent,
         // so no MFMA waits on the previous one's result; the next k-step's
         // CO weight fragments are read while this one's MFMAs run
-        bf16x8 a[2][CO];
+        frag8 a[2][CO];
 #pragma unroll
         for (int o = 0; o < CO; ++o)
-            a[0][o] = *reinterpret_cast<const bf16x8*>(lds + (o * KS) * kFrag + lane * 16);
+            a[0][o] = *reinterpret_cast<const frag8*>(lds + (o * KS) * kFrag + lane * 16);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             if (ks + 1 < KS) {
 #pragma unroll
                 for (int o = 0; o < CO; ++o)
                     a[(ks + 1) & 1][o] =
-                        *reinterpret_cast<const bf16x8*>(lds + (o * KS + ks + 1) * kFrag + lane * 16);
+                        *reinterpret_cast<const frag8*>(lds + (o * KS + ks + 1) * kFrag + lane * 16);
             }
 #pragma unroll
             for (int o = 0; o < CO; ++o)
 #pragma unroll
                 for (int nt = 0; nt < NT; ++nt)
-                    acc[nt][c * CO + o] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[ks & 1][o], x[nt][ks],
-                                                                                  acc[nt][c * CO + o], 0, 0, 0);
+                    acc[nt][c * CO + o] = mfma16<E>(a[ks & 1][o], x[nt][ks], acc[nt][c * CO + o]);
         }
         st.finish_chunk();
     }
 }
 
-// one accumulator tile -> 8 dwords of bf16: dword q holds registers 2q, 2q+1
+// one accumulator tile -> 8 dwords of E: dword q holds registers 2q, 2q+1
+template <typename E>
 __device__ __forceinline__ void pack_tile(const f32x16& acc, uint32_t (&d)[8]) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) d[q] = pack_bf16(acc[2 * q], acc[2 * q + 1]);
+    for (int q = 0; q < 8; ++q) d[q] = pack2<E>(acc[2 * q], acc[2 * q + 1]);
 }
 
 // packed tile -> next layer's B fragments (k-step 2*ot + s = registers 8s..8s+7)
-__device__ __forceinline__ void tile_frags(const uint32_t (&d)[8], bool rectify, bf16x8& x0, bf16x8& x1) {
-    u32x4v a, b;
+__device__ __forceinline__ void tile_frags(const uint32_t (&d)[8], bool rectify, frag8& x0, frag8& x1) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        a[q] = rectify ? relu_bf16x2(d[q]) : d[q];
-        b[q] = rectify ? relu_bf16x2(d[4 + q]) : d[4 + q];
+        x0[q] = rectify ? relu16x2(d[q]) : d[q];
+        x1[q] = rectify ? relu16x2(d[4 + q]) : d[4 + q];
     }
-    x0 = __builtin_bit_cast(bf16x8, a);
-    x1 = __builtin_bit_cast(bf16x8, b);
 }
 
-template <int NT, int OT>
-__device__ __forceinline__ void to_frags(const f32x16 (&acc)[NT][OT], bf16x8 (&x)[NT][2 * OT]) {
+template <typename E, int NT, int OT>
+__device__ __forceinline__ void to_frags(const f32x16 (&acc)[NT][OT], frag8 (&x)[NT][2 * OT]) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int ot = 0; ot < OT; ++ot) {
             uint32_t d[8];
-            pack_tile(acc[nt][ot], d);
+            pack_tile<E>(acc[nt][ot], d);
             tile_frags(d, true, x[nt][2 * ot], x[nt][2 * ot + 1]);
         }
 }
@@ -252,21 +276,21 @@ __device__ __forceinline__ void to_frags(const f32x16 (&acc)[NT][OT], bf16x8 (&x
 // [0, 32*OT) and return them as the next layer's (rectified) fragments: lane
 // (column n, half h) holds rows 8g + 4h + 0..3 of each tile in registers
 // 4g..4g+3 -> one 8-byte store per g.
-template <int NT, int OT>
+template <typename E, int NT, int OT>
 __device__ __forceinline__ void store_and_frags(const Args& a, const f32x16 (&acc)[NT][OT], int64_t n0,
-                                                int lane, bool rectify, bf16x8 (&x)[NT][2 * OT]) {
+                                                int lane, bool rectify, frag8 (&x)[NT][2 * OT]) {
     const int h = lane >> 5;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
         const int64_t n = n0 + 32 * nt + (lane & 31);
-        __hip_bfloat16* row = a.base + n * a.ldb;
+        uint16_t* row = a.base + n * a.ldb;
 #pragma unroll
         for (int ot = 0; ot < OT; ++ot) {
             uint32_t d[8];
-            pack_tile(acc[nt][ot], d);
+            pack_tile<E>(acc[nt][ot], d);
             if (rectify) {
 #pragma unroll
-                for (int q = 0; q < 8; ++q) d[q] = relu_bf16x2(d[q]);
+                for (int q = 0; q < 8; ++q) d[q] = relu16x2(d[q]);
             }
             if (n < a.N) {
 #pragma unroll
@@ -279,17 +303,17 @@ __device__ __forceinline__ void store_and_frags(const Args& a, const f32x16 (&ac
 }
 
 // decoder output (row 0 of the single output tile: register 0 of lanes 0..31)
-template <int NT>
+template <typename E, int NT>
 __device__ __forceinline__ void store_attn(const Args& a, const f32x16 (&acc)[NT][1], int64_t n0, int lane) {
     if (lane >= 32) return;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
         const int64_t n = n0 + 32 * nt + lane;
         if (n >= a.N) continue;
-        const float y = (float)(__bf16)acc[nt][0][0];       // the GEMM's bf16 output
-        const float l = y > 0.0f ? y : y * a.slope;          // leaky_relu in fp32 ...
-        const float r = fabsf((float)(__bf16)l);             // ... rounded to bf16, abs
-        a.attn[n] = __float2bfloat16(r);
+        const float y = round16<E>(acc[nt][0][0]);       // the GEMM's 16-bit output
+        const float l = y > 0.0f ? y : y * a.slope;      // leaky_relu in fp32 ...
+        const float r = fabsf(round16<E>(l));            // ... rounded to E, abs
+        a.attn[n] = bits16<E>(r);
     }
 }
 
@@ -301,20 +325,20 @@ __device__ __forceinline__ int64_t src_row(const Src& s, int64_t n) {
 // extra feature segments copied (as bf16) into base columns after the MLP
 // output: lane (sample r, half h) copies 8-feature chunks h, h+2, ... of its
 // sample's row of every segment (one division per segment and lane)
-template <int NT>
+template <typename E, int NT>
 __device__ __forceinline__ void copy_extras(const Args& a, int64_t n0, int lane) {
     const int h = lane >> 5;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
         const int64_t n = n0 + 32 * nt + (lane & 31);
         if (n >= a.N) continue;
-        __hip_bfloat16* row = a.base + n * a.ldb;
+        uint16_t* row = a.base + n * a.ldb;
         for (int e = 0; e < a.n_extra; ++e) {
             const Src s = a.extra[e];
             const int w = a.extra_width[e];
             const int64_t r = src_row(s, n);
             for (int c = 8 * h; c < w; c += 16)
-                *reinterpret_cast<bf16x8*>(row + a.extra_col[e] + c) = load8(s, r, w, c);
+                *reinterpret_cast<frag8*>(row + a.extra_col[e] + c) = load8<E>(s, r, w, c);
         }
     }
 }
@@ -322,8 +346,8 @@ __device__ __forceinline__ void copy_extras(const Args& a, int64_t n0, int lane)
 // first-layer input fragments: lane (sample r, half h) k-step ks holds
 // features 8c..8c+7 with c = 2ks + h; chunks [0, 5) come from in0 (40 per
 // sample), [5, 10) from in1 (40 per pose) when the net has two inputs.
-template <int NT, int KS0>
-__device__ __forceinline__ void load_input(const Args& a, int64_t n0, int lane, bf16x8 (&x)[NT][KS0]) {
+template <typename E, int NT, int KS0>
+__device__ __forceinline__ void load_input(const Args& a, int64_t n0, int lane, frag8 (&x)[NT][KS0]) {
     const int h = lane >> 5;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -335,12 +359,11 @@ __device__ __forceinline__ void load_input(const Args& a, int64_t n0, int lane, 
         for (int ks = 0; ks < KS0; ++ks) {
             const int c = 2 * ks + h;
             if (c < 5) {
-                x[nt][ks] = load8(a.in0, r0, 40, 8 * c);
+                x[nt][ks] = load8<E>(a.in0, r0, 40, 8 * c);
             } else if (KS0 > 3 && c < 10) {
-                x[nt][ks] = load8(a.in1, r1, 40, 8 * (c - 5));
+                x[nt][ks] = load8<E>(a.in1, r1, 40, 8 * (c - 5));
             } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) x[nt][ks][j] = (__bf16)0.0f;
+                x[nt][ks] = frag8{0u, 0u, 0u, 0u};  // +0 in either format
             }
         }
     }
@@ -348,7 +371,7 @@ __device__ __forceinline__ void load_input(const Args& a, int64_t n0, int lane, 
 
 // Variant 0 (AVRModel): 40 -> 128 -> 128 -> 128 -> 128 (linear, = sigma_feat)
 // -> relu -> 128 -> 128 -> 128 -> 1.  8 chunks.
-template <int NT, int WAVES, int OCC, int DBG = 0>
+template <typename E, int NT, int WAVES, int OCC, int DBG = 0>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
 void sigma_meshrir_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) char lds[2 * kChunk];
@@ -357,38 +380,38 @@ void sigma_meshrir_kernel(Args a) {
     Stager<WAVES, DBG> st;
     st.start(a.wpack, lds, 8);
 
-    bf16x8 x0[NT][3];
-    load_input<NT, 3>(a, n0, lane, x0);
-    bf16x8 x[NT][8];
+    frag8 x0[NT][3];
+    load_input<E, NT, 3>(a, n0, lane, x0);
+    frag8 x[NT][8];
     {
         f32x16 acc[NT][4];
-        dense<NT, 3, 4, 4>(st, lane, x0, acc);
-        to_frags<NT, 4>(acc, x);
+        dense<E, NT, 3, 4, 4>(st, lane, x0, acc);
+        to_frags<E, NT, 4>(acc, x);
     }
 #pragma unroll
     for (int l = 0; l < 2; ++l) {
         f32x16 acc[NT][4];
-        dense<NT, 8, 4, 4>(st, lane, x, acc);
-        to_frags<NT, 4>(acc, x);
+        dense<E, NT, 8, 4, 4>(st, lane, x, acc);
+        to_frags<E, NT, 4>(acc, x);
     }
     {
         f32x16 acc[NT][4];
-        dense<NT, 8, 4, 4>(st, lane, x, acc);
+        dense<E, NT, 8, 4, 4>(st, lane, x, acc);
         // sigma_feat (linear) -> base; relu(sigma_feat) -> decoder
-        store_and_frags<NT, 4>(a, acc, n0, lane, false, x);
+        store_and_frags<E, NT, 4>(a, acc, n0, lane, false, x);
     }
 #pragma unroll
     for (int l = 0; l < 3; ++l) {
         f32x16 acc[NT][4];
-        dense<NT, 8, 4, 4>(st, lane, x, acc);
-        to_frags<NT, 4>(acc, x);
+        dense<E, NT, 8, 4, 4>(st, lane, x, acc);
+        to_frags<E, NT, 4>(acc, x);
     }
     {
         f32x16 acc[NT][1];
-        dense<NT, 8, 1, 1>(st, lane, x, acc);
-        store_attn<NT>(a, acc, n0, lane);
+        dense<E, NT, 8, 1, 1>(st, lane, x, acc);
+        store_attn<E, NT>(a, acc, n0, lane);
     }
-    if constexpr (!(DBG & 4)) copy_extras<NT>(a, n0, lane);
+    if constexpr (!(DBG & 4)) copy_extras<E, NT>(a, n0, lane);
 }
 
 // signal layer 1 epilogue (variant 2): h1[n][128c + o] = bf16(relu(acc + bias[n / bias_div][128c + o])).
@@ -397,7 +420,7 @@ void sigma_meshrir_kernel(Args a) {
 // (32 samples x 64 columns, 4 KB) goes through a per-wave LDS area (16-byte
 // chunks XOR-swizzled by row: conflict-free) and leaves as 4 instructions
 // of 8 rows x 128 contiguous bytes (full cache lines).
-template <int NT, bool STORE = true>
+template <typename E, int NT, bool STORE = true>
 __device__ __forceinline__ void store_h1(const Args& a, const f32x16 (&acc)[NT][4], int64_t n0, int lane, int c,
                                          char* tr) {
     const int h = lane >> 5, r = lane & 31;
@@ -415,8 +438,8 @@ __device__ __forceinline__ void store_h1(const Args& a, const f32x16 (&acc)[NT][
                 for (int g = 0; g < 4; ++g) {
                     const f32x4 b = *reinterpret_cast<const f32x4*>(brow + 32 * ot + 8 * g + 4 * h);
                     const f32x16& v = acc[nt][ot];
-                    const uint32_t w0 = pack_bf16(relu(v[4 * g] + b[0]), relu(v[4 * g + 1] + b[1]));
-                    const uint32_t w1 = pack_bf16(relu(v[4 * g + 2] + b[2]), relu(v[4 * g + 3] + b[3]));
+                    const uint32_t w0 = pack2<E>(relu(v[4 * g] + b[0]), relu(v[4 * g + 1] + b[1]));
+                    const uint32_t w1 = pack2<E>(relu(v[4 * g + 2] + b[2]), relu(v[4 * g + 3] + b[3]));
                     const int ch = (4 * j + g) ^ (r & 7);  // 16-B chunk of the 128-B row
                     *reinterpret_cast<u32x2v*>(tr + r * 128 + ch * 16 + 8 * h) = u32x2v{w0, w1};
                 }
@@ -446,7 +469,7 @@ __device__ __forceinline__ void store_h1(const Args& a, const f32x16 (&acc)[NT][
 // per-ray / per-pose columns of the layer (dir_enc, tx_enc) folded into
 // `bias` on the host, written as [N][512] bf16 in place of the
 // concatenated input.  12 chunks.
-template <int NT, int WAVES, int OCC, int DBG = 0>
+template <typename E, int NT, int WAVES, int OCC, int DBG = 0>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
 void sigma_meshrir_h1_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) char lds[2 * kChunk + WAVES * 4096];
@@ -455,30 +478,30 @@ void sigma_meshrir_h1_kernel(Args a) {
     Stager<WAVES, DBG & 3> st;
     st.start(a.wpack, lds, 12);
 
-    bf16x8 x0[NT][3];
-    load_input<NT, 3>(a, n0, lane, x0);
-    bf16x8 x[NT][8];
+    frag8 x0[NT][3];
+    load_input<E, NT, 3>(a, n0, lane, x0);
+    frag8 x[NT][8];
     {
         f32x16 acc[NT][4];
-        dense<NT, 3, 4, 4>(st, lane, x0, acc);
-        to_frags<NT, 4>(acc, x);
+        dense<E, NT, 3, 4, 4>(st, lane, x0, acc);
+        to_frags<E, NT, 4>(acc, x);
     }
 #pragma unroll
     for (int l = 0; l < 2; ++l) {
         f32x16 acc[NT][4];
-        dense<NT, 8, 4, 4>(st, lane, x, acc);
-        to_frags<NT, 4>(acc, x);
+        dense<E, NT, 8, 4, 4>(st, lane, x, acc);
+        to_frags<E, NT, 4>(acc, x);
     }
-    bf16x8 xs[NT][8];  // bf16(sigma_feat): the signal network's per-sample input
+    frag8 xs[NT][8];  // bf16(sigma_feat): the signal network's per-sample input
     {
         f32x16 acc[NT][4];
-        dense<NT, 8, 4, 4>(st, lane, x, acc);
+        dense<E, NT, 8, 4, 4>(st, lane, x, acc);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
             for (int ot = 0; ot < 4; ++ot) {
                 uint32_t d[8];
-                pack_tile(acc[nt][ot], d);
+                pack_tile<E>(acc[nt][ot], d);
                 tile_frags(d, false, xs[nt][2 * ot], xs[nt][2 * ot + 1]);
                 tile_frags(d, true, x[nt][2 * ot], x[nt][2 * ot + 1]);
             }
@@ -486,25 +509,25 @@ void sigma_meshrir_h1_kernel(Args a) {
 #pragma unroll
     for (int l = 0; l < 3; ++l) {
         f32x16 acc[NT][4];
-        dense<NT, 8, 4, 4>(st, lane, x, acc);
-        to_frags<NT, 4>(acc, x);
+        dense<E, NT, 8, 4, 4>(st, lane, x, acc);
+        to_frags<E, NT, 4>(acc, x);
     }
     {
         f32x16 acc[NT][1];
-        dense<NT, 8, 1, 1>(st, lane, x, acc);
-        store_attn<NT>(a, acc, n0, lane);
+        dense<E, NT, 8, 1, 1>(st, lane, x, acc);
+        store_attn<E, NT>(a, acc, n0, lane);
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         f32x16 acc[NT][4];
-        dense<NT, 8, 4, 4>(st, lane, xs, acc);
-        store_h1<NT, !(DBG & 4)>(a, acc, n0, lane, c, lds + 2 * kChunk + wave * 4096);
+        dense<E, NT, 8, 4, 4>(st, lane, xs, acc);
+        store_h1<E, NT, !(DBG & 4)>(a, acc, n0, lane, c, lds + 2 * kChunk + wave * 4096);
     }
 }
 
 // Variant 1 (AVRModel_complex): [40 | 40] -> 128 -> 128 -> 128 -> 256 (relu,
 // = rf) -> 128 -> 1.  8 chunks (the 256-wide layers take two each).
-template <int NT, int WAVES, int OCC>
+template <typename E, int NT, int WAVES, int OCC>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
 void sigma_raf_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) char lds[2 * kChunk];
@@ -513,37 +536,37 @@ void sigma_raf_kernel(Args a) {
     Stager<WAVES> st;
     st.start(a.wpack, lds, 8);
 
-    bf16x8 x0[NT][5];
-    load_input<NT, 5>(a, n0, lane, x0);
-    bf16x8 x[NT][8];
+    frag8 x0[NT][5];
+    load_input<E, NT, 5>(a, n0, lane, x0);
+    frag8 x[NT][8];
     {
         f32x16 acc[NT][4];
-        dense<NT, 5, 4, 4>(st, lane, x0, acc);
-        to_frags<NT, 4>(acc, x);
+        dense<E, NT, 5, 4, 4>(st, lane, x0, acc);
+        to_frags<E, NT, 4>(acc, x);
     }
 #pragma unroll
     for (int l = 0; l < 2; ++l) {
         f32x16 acc[NT][4];
-        dense<NT, 8, 4, 4>(st, lane, x, acc);
-        to_frags<NT, 4>(acc, x);
+        dense<E, NT, 8, 4, 4>(st, lane, x, acc);
+        to_frags<E, NT, 4>(acc, x);
     }
-    bf16x8 rf[NT][16];
+    frag8 rf[NT][16];
     {
         f32x16 acc[NT][8];
-        dense<NT, 8, 8, 4>(st, lane, x, acc);
-        store_and_frags<NT, 8>(a, acc, n0, lane, true, rf);  // rf = relu(sigma_feature)
+        dense<E, NT, 8, 8, 4>(st, lane, x, acc);
+        store_and_frags<E, NT, 8>(a, acc, n0, lane, true, rf);  // rf = relu(sigma_feature)
     }
     {
         f32x16 acc[NT][4];
-        dense<NT, 16, 4, 2>(st, lane, rf, acc);
-        to_frags<NT, 4>(acc, x);
+        dense<E, NT, 16, 4, 2>(st, lane, rf, acc);
+        to_frags<E, NT, 4>(acc, x);
     }
     {
         f32x16 acc[NT][1];
-        dense<NT, 8, 1, 1>(st, lane, x, acc);
-        store_attn<NT>(a, acc, n0, lane);
+        dense<E, NT, 8, 1, 1>(st, lane, x, acc);
+        store_attn<E, NT>(a, acc, n0, lane);
     }
-    copy_extras<NT>(a, n0, lane);
+    copy_extras<E, NT>(a, n0, lane);
 }
 
 bool src_ok(const avr_feat_src& s) {
@@ -553,31 +576,36 @@ bool src_ok(const avr_feat_src& s) {
 
 Src to_src(const avr_feat_src& s) { return Src{s.data, (int)s.dtype, (int)s.rows_div, s.lm_rows}; }
 
-template <int NT, int WAVES, int OCC, int DBG = 0>
+template <typename E, int NT, int WAVES, int OCC, int DBG = 0>
 int launch_meshrir(const Args& a, hipStream_t st) {
     const int64_t per_block = 32 * NT * WAVES;
     const dim3 grid((unsigned)((a.N + per_block - 1) / per_block));
-    hipLaunchKernelGGL((sigma_meshrir_kernel<NT, WAVES, OCC, DBG>), grid, dim3(64 * WAVES), 0, st, a);
+    hipLaunchKernelGGL((sigma_meshrir_kernel<E, NT, WAVES, OCC, DBG>), grid, dim3(64 * WAVES), 0, st, a);
     return check_launch("avr_sigma_fwd");
 }
 
-template <int NT, int WAVES, int OCC, int DBG = 0>
+template <typename E, int NT, int WAVES, int OCC, int DBG = 0>
 int launch_meshrir_h1(const Args& a, hipStream_t st) {
     const int64_t per_block = 32 * NT * WAVES;
     const dim3 grid((unsigned)((a.N + per_block - 1) / per_block));
-    hipLaunchKernelGGL((sigma_meshrir_h1_kernel<NT, WAVES, OCC, DBG>), grid, dim3(64 * WAVES), 0, st, a);
+    hipLaunchKernelGGL((sigma_meshrir_h1_kernel<E, NT, WAVES, OCC, DBG>), grid, dim3(64 * WAVES), 0, st, a);
     return check_launch("avr_sigma_fwd");
 }
 
-template <int WAVES, int OCC>
+template <typename E, int WAVES, int OCC>
 int launch_raf(const Args& a, hipStream_t st) {
     const int64_t per_block = 32 * WAVES;
     const dim3 grid((unsigned)((a.N + per_block - 1) / per_block));
-    hipLaunchKernelGGL((sigma_raf_kernel<1, WAVES, OCC>), grid, dim3(64 * WAVES), 0, st, a);
+    hipLaunchKernelGGL((sigma_raf_kernel<E, 1, WAVES, OCC>), grid, dim3(64 * WAVES), 0, st, a);
     return check_launch("avr_sigma_fwd");
 }
 
 }  // namespace
+
+namespace {
+template <typename E>
+int dispatch(const avr_sigma_desc* d, Args& a, bool h1, bool two, hipStream_t st);
+}
 
 extern "C" int avr_sigma_pack_bytes(int32_t variant, int64_t* bytes) {
     AVR_REQUIRE(bytes && (variant == AVR_SIGMA_MESHRIR || variant == AVR_SIGMA_RAF ||
@@ -622,41 +650,55 @@ extern "C" int avr_sigma_fwd(const avr_sigma_desc* d, const void* wpack, void* b
     }
     AVR_REQUIRE(col <= ldb, "avr_sigma_fwd: ldb smaller than the concatenated features");
     a.wpack = static_cast<const char*>(wpack);
-    a.base = static_cast<__hip_bfloat16*>(base);
+    a.base = static_cast<uint16_t*>(base);
     a.ldb = ldb;
-    a.attn = static_cast<__hip_bfloat16*>(attn);
+    a.attn = static_cast<uint16_t*>(attn);
     a.slope = d->leaky_slope;
     a.bias = d->bias;
     a.bias_div = d->bias_div;
+    AVR_REQUIRE(d->dtype == AVR_DTYPE_BF16 || d->dtype == AVR_DTYPE_F16,
+                "avr_sigma_fwd: dtype must be AVR_DTYPE_BF16 or AVR_DTYPE_F16");
     hipStream_t st = as_stream(stream);
+    if (d->dtype == AVR_DTYPE_F16) return dispatch<_Float16>(d, a, h1, two, st);
+    return dispatch<__bf16>(d, a, h1, two, st);
+}
+
+namespace {
+template <typename E>
+int dispatch(const avr_sigma_desc* d, Args& a, bool h1, bool two, hipStream_t st) {
     if (h1) {
         // 0: 4 waves, streaming h1 stores (120 us at config 2); 1: 8 waves;
         // 2, 3: the same with plain stores (130 us)
         a.nt_store = d->tile_cfg < 2;
-        if (d->tile_cfg == 1 || d->tile_cfg == 3) return launch_meshrir_h1<1, 8, 1>(a, st);
+        if (d->tile_cfg == 1 || d->tile_cfg == 3) return launch_meshrir_h1<E, 1, 8, 1>(a, st);
         // timing experiments (results are garbage): no barrier / no weight
-        // staging / no h1 stores
-        if (d->tile_cfg == 16) return launch_meshrir_h1<1, 4, 2, 1>(a, st);
-        if (d->tile_cfg == 17) return launch_meshrir_h1<1, 4, 2, 2>(a, st);
-        if (d->tile_cfg == 18) return launch_meshrir_h1<1, 4, 2, 4>(a, st);
-        if (d->tile_cfg == 19) return launch_meshrir_h1<1, 4, 2, 7>(a, st);
-        return launch_meshrir_h1<1, 4, 2>(a, st);
+        // staging / no h1 stores (bf16 builds only)
+        if constexpr (std::is_same<E, __bf16>::value) {
+            if (d->tile_cfg == 16) return launch_meshrir_h1<E, 1, 4, 2, 1>(a, st);
+            if (d->tile_cfg == 17) return launch_meshrir_h1<E, 1, 4, 2, 2>(a, st);
+            if (d->tile_cfg == 18) return launch_meshrir_h1<E, 1, 4, 2, 4>(a, st);
+            if (d->tile_cfg == 19) return launch_meshrir_h1<E, 1, 4, 2, 7>(a, st);
+        }
+        return launch_meshrir_h1<E, 1, 4, 2>(a, st);
     }
     const int cfg = d->tile_cfg;
     // tile configs (tools/probe_sigma.py, MI355X at config 2): MeshRIR
     // 0 = 64 samples per wave, 4 waves, 2 waves/SIMD (72 us); 1 = 32 per
     // wave, 8 waves (80 us); 2 = 32 per wave, 4 waves at 2 waves/SIMD; 3 = 64 per wave, 4
     // waves, 1 wave/SIMD.  RAF: 0 = 4 waves (120 us), 1 = 8 waves (137 us).
-    if (two) return cfg == 1 ? launch_raf<8, 1>(a, st) : launch_raf<4, 2>(a, st);
-    if (cfg == 1) return launch_meshrir<1, 8, 1>(a, st);
-    if (cfg == 2) return launch_meshrir<1, 4, 2>(a, st);
-    if (cfg == 3) return launch_meshrir<2, 4, 1>(a, st);
-    if (cfg == 16) return launch_meshrir<1, 8, 1, 1>(a, st);
-    if (cfg == 17) return launch_meshrir<1, 8, 1, 2>(a, st);
-    if (cfg == 18) return launch_meshrir<1, 8, 1, 3>(a, st);
-    if (cfg == 19) return launch_meshrir<1, 8, 1, 4>(a, st);
-    if (cfg == 20) return launch_meshrir<1, 8, 1, 7>(a, st);
-    return launch_meshrir<2, 4, 2>(a, st);
+    if (two) return cfg == 1 ? launch_raf<E, 8, 1>(a, st) : launch_raf<E, 4, 2>(a, st);
+    if (cfg == 1) return launch_meshrir<E, 1, 8, 1>(a, st);
+    if (cfg == 2) return launch_meshrir<E, 1, 4, 2>(a, st);
+    if (cfg == 3) return launch_meshrir<E, 2, 4, 1>(a, st);
+    if constexpr (std::is_same<E, __bf16>::value) {
+        if (cfg == 16) return launch_meshrir<E, 1, 8, 1, 1>(a, st);
+        if (cfg == 17) return launch_meshrir<E, 1, 8, 1, 2>(a, st);
+        if (cfg == 18) return launch_meshrir<E, 1, 8, 1, 3>(a, st);
+        if (cfg == 19) return launch_meshrir<E, 1, 8, 1, 4>(a, st);
+        if (cfg == 20) return launch_meshrir<E, 1, 8, 1, 7>(a, st);
+    }
+    return launch_meshrir<E, 2, 4, 2>(a, st);
 }
+}  // namespace
 
 extern "C" int avr_sigma_desc_size(void) { return (int)sizeof(avr_sigma_desc); }

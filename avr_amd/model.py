@@ -273,21 +273,21 @@ def _per_pose(x, layout):
     return x.reshape(B, R * S, 3)[:, 0].contiguous()
 
 
-def _bias_columns(w1):
+def _bias_columns(w1, dtype=torch.bfloat16):
     """The signal network's first-layer columns that act per ray (dir
-    encoding, 128:168) and per pose (tx encoding, 168:208), bf16-rounded as
-    the unfused GEMM reads them, in fp32 and transposed; kept on the weight
-    until it changes (version counter), like wcache.cast_weight."""
-    key = (w1.data_ptr(), w1._version)
+    encoding, 128:168) and per pose (tx encoding, 168:208), rounded to the
+    MLP dtype as the unfused GEMM reads them, in fp32 and transposed; kept on
+    the weight until it changes (version counter), like wcache.cast_weight."""
+    key = (w1.data_ptr(), w1._version, dtype)
     hit = None if capturing() else cache_lookup(w1, "_avr_bias_cols", key)
     if hit is not None:
         return hit
-    wb = cast_weight(w1, torch.bfloat16, True).float()
+    wb = cast_weight(w1, dtype, True).float()
     cols = (wb[:, 128:168].t().contiguous(), wb[:, 168:208].t().contiguous())
     return cols if capturing() else cache_store(w1, "_avr_bias_cols", key, cols)
 
 
-def _ray_pose_bias(dir_enc, tx_enc, view, tx, wd, wt, layout):
+def _ray_pose_bias(dir_enc, tx_enc, view, tx, wd, wt, layout, mlp_dtype=torch.bfloat16):
     """The first-layer bias of every ray in one launch (`avr_ray_pose_bias`):
     the per-ray direction and per-pose tx encodings, rounded as the unfused
     path rounds them, times their weight columns.  None when the grids do
@@ -309,6 +309,7 @@ def _ray_pose_bias(dir_enc, tx_enc, view, tx, wd, wt, layout):
               dir_enc.n_levels, dtab.data_ptr(), dir_enc._off.ctypes.data, dir_enc._scale.ctypes.data,
               dir_enc._res.ctypes.data, tx_enc.n_levels, ttab.data_ptr(), tx_enc._off.ctypes.data,
               tx_enc._scale.ctypes.data, tx_enc._res.ctypes.data, _code(dtab.dtype), _code(dir_enc.dtype),
+              _lib.DTYPE_F16 if mlp_dtype == torch.float16 else _lib.DTYPE_BF16,
               wd.data_ptr(), wt.data_ptr(), wd.size(1), bias.data_ptr(), st)
     return bias
 
@@ -382,7 +383,7 @@ class AVRModel(nn.Module):
         pos_enc = self._pos_encoding.forward_level_major(_unit(pts.reshape(-1, 3)))
         dir_e = self._dir_encoding(_unit(_per_ray(view.reshape(-1, 3), L)))
         tx_e = self._tx_encoding(_unit(_per_pose(tx.reshape(-1, 3), L)))
-        packed = self._sigma_pack.get(_sigma.MESHRIR, _sigma_params(self))
+        packed = self._sigma_pack.get(_sigma.MESHRIR, _sigma_params(self), self._model_encoder_sigma.dtype)
         attn, base = _sigma.sigma_fwd(_sigma.MESHRIR, packed, bs * n, [(pos_enc, 1)],
                                       [(dir_e, S), (tx_e, R * S)], 128, 0.01)
         return attn.view(bs, n, 1), base
@@ -397,16 +398,17 @@ class AVRModel(nn.Module):
         bs, n = pts.size(0), pts.size(1)
         pos_enc = self._pos_encoding.forward_level_major(_unit(pts.reshape(-1, 3)))
         w1 = self._model_signal.layers[0].weight
-        wd, wt = _bias_columns(w1)
-        bias = _ray_pose_bias(self._dir_encoding, self._tx_encoding, view, tx, wd, wt, L)
+        dt = self._model_encoder_sigma.dtype
+        wd, wt = _bias_columns(w1, dt)
+        bias = _ray_pose_bias(self._dir_encoding, self._tx_encoding, view, tx, wd, wt, L, dt)
         if bias is None:
             dir_e = self._dir_encoding(_unit(_per_ray(view.reshape(-1, 3), L)))
             tx_e = self._tx_encoding(_unit(_per_pose(tx.reshape(-1, 3), L)))
-            bias = dir_e.to(torch.bfloat16).float() @ wd
-            bias = (bias.view(B, R, -1) + (tx_e.to(torch.bfloat16).float() @ wt).view(B, 1, -1))
+            bias = dir_e.to(dt).float() @ wd
+            bias = (bias.view(B, R, -1) + (tx_e.to(dt).float() @ wt).view(B, 1, -1))
             bias = bias.reshape(B * R, -1).contiguous()
         params = _sigma_params(self) + [w1[:, :128]]
-        packed = self._sigma_pack.get(_sigma.MESHRIR_H1, params)
+        packed = self._sigma_pack.get(_sigma.MESHRIR_H1, params, dt)
         attn, h1 = _sigma.sigma_fwd(_sigma.MESHRIR_H1, packed, bs * n, [(pos_enc, 1)], [], 512, 0.01,
                                     bias=bias, bias_div=S)
         return attn.view(bs, n, 1), h1
@@ -529,7 +531,7 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
         t = _unit(_per_pose(tx.reshape(-1, 3), L))
         v = _unit(_per_ray(view.reshape(-1, 3), L))
         tv = _unit(_per_pose(tx_view.reshape(-1, 3), L))
-        packed = self._sigma_pack.get(_sigma.RAF, _sigma_params(self))
+        packed = self._sigma_pack.get(_sigma.RAF, _sigma_params(self), self._model_encoder_sigma.dtype)
         attn, base = _sigma.sigma_fwd(
             _sigma.RAF, packed, bs * n,
             [(self._pos_encoding.forward_level_major(p), 1), (self._tx_pos_encoding(t), R * S)],

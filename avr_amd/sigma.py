@@ -55,7 +55,7 @@ class SigmaDesc(ctypes.Structure):
                 ("n_samples", ctypes.c_int64), ("leaky_slope", ctypes.c_float),
                 ("input", FeatSrc * 2), ("n_extra", ctypes.c_int32),
                 ("extra", FeatSrc * MAX_EXTRA), ("extra_width", ctypes.c_int32 * MAX_EXTRA),
-                ("bias", ctypes.c_void_p), ("bias_div", ctypes.c_int32)]
+                ("bias", ctypes.c_void_p), ("bias_div", ctypes.c_int32), ("dtype", ctypes.c_int32)]
 
 
 def fragment_index(M, K, first):
@@ -94,10 +94,10 @@ def _gather_index(M, K, first, device):
     return v
 
 
-def pack_layers(variant, weights):
-    """Weights (fp32 [M, K] tensors, in SCHEDULE order) -> packed bf16
-    fragments, one 32 KB chunk per LDS stage (zero padded), as a flat
-    torch.bfloat16 tensor on the weights' device."""
+def pack_layers(variant, weights, dtype=torch.bfloat16):
+    """Weights (fp32 [M, K] tensors, in SCHEDULE order) -> packed fragments
+    in the MLP dtype (bf16 or fp16), one 32 KB chunk per LDS stage (zero
+    padded), as a flat tensor on the weights' device."""
     sched = SCHEDULE[variant]
     if len(weights) != len(sched):
         raise ValueError(f"variant {variant} takes {len(sched)} layers, got {len(weights)}")
@@ -109,7 +109,7 @@ def pack_layers(variant, weights):
         OT, KS = oi.shape[:2]
         wp = torch.zeros(OT * 32 + 1, KS * 16 + 1, dtype=torch.float32, device=w.device)
         wp[:M, :K] = w.detach().float()
-        frags = wp[oi, ki].to(torch.bfloat16)  # [OT, KS, 64, 8]
+        frags = wp[oi, ki].to(dtype)  # [OT, KS, 64, 8]
         for c in range(OT // co):
             part = frags[c * co:(c + 1) * co].reshape(-1)
             pad = CHUNK // 2 - part.numel()
@@ -128,11 +128,14 @@ def _dims(mlp):
     return [(lin.weight.shape[0], lin.weight.shape[1]) for lin in mlp.layers]
 
 
+MLP_DTYPES = (torch.bfloat16, torch.float16)
+
+
 def variant_of(model):
     """AVR_SIGMA_* if the model's sigma networks have exactly the shapes the
-    fused kernel implements (and bf16 MLPs), else None."""
+    fused kernel implements (and 16-bit MLPs: bf16, or fp16 = tcnn's), else None."""
     enc, dec = model._model_encoder_sigma, model._model_decoder_sigma
-    if enc.dtype != torch.bfloat16 or dec.dtype != torch.bfloat16:
+    if enc.dtype not in MLP_DTYPES or dec.dtype != enc.dtype:
         return None
     dims = _dims(enc) + _dims(dec)
     for v in (MESHRIR, RAF):
@@ -143,10 +146,11 @@ def variant_of(model):
 
 def h1_ok(model):
     """MESHRIR_H1 applies: an AVRModel whose signal network starts with a
-    bias-free 208 -> 512 layer on [sigma_feat 128 | dir 40 | tx 40] in bf16
-    and has at least one more hidden layer."""
+    bias-free 208 -> 512 layer on [sigma_feat 128 | dir 40 | tx 40] in the
+    sigma networks' 16-bit dtype and has at least one more hidden layer."""
     sig = model._model_signal
-    return (variant_of(model) == MESHRIR and sig.dtype == torch.bfloat16 and len(sig.layers) >= 3
+    return (variant_of(model) == MESHRIR and sig.dtype == model._model_encoder_sigma.dtype
+            and len(sig.layers) >= 3
             and tuple(sig.layers[0].weight.shape) == (512, 208))
 
 
@@ -154,14 +158,14 @@ class SigmaWeights:
     """Packed fragments of a model's sigma networks, repacked when any weight
     changes (parameter version counters)."""
 
-    def get(self, variant, params):
+    def get(self, variant, params, dtype=torch.bfloat16):
         if capturing():  # a captured graph repacks at every replay
-            return pack_layers(variant, params)
-        key = (variant,) + tuple((p.data_ptr(), p._version) for p in params)
+            return pack_layers(variant, params, dtype)
+        key = (variant, dtype) + tuple((p.data_ptr(), p._version) for p in params)
         hit = cache_lookup(self, "_entry", key)
         if hit is not None:
             return hit
-        return cache_store(self, "_entry", key, pack_layers(variant, params))
+        return cache_store(self, "_entry", key, pack_layers(variant, params, dtype))
 
 
 def _src(t, rows_div):
@@ -194,15 +198,20 @@ def sigma_fwd(variant, packed, n_samples, inputs, extras, out_width, slope, tile
               bias_div=1):
     """One launch: inputs = [(tensor [rows, 40] or level-major [20, rows, 2],
     rows_div)] (1 for MESHRIR, 2 for RAF); extras = [(tensor, rows_div)]
-    appended after the MLP output.  Returns (attn [N] bf16, base [N, out_width + sum widths] bf16)."""
+    appended after the MLP output.  The MLP dtype is the packed weights'
+    (bf16 or fp16).  Returns (attn [N], base [N, out_width + sum widths]) in it."""
     dev = packed.device
+    dtype = packed.dtype
+    if dtype not in MLP_DTYPES:
+        raise TypeError(f"packed sigma weights must be bf16 or fp16, got {dtype}")
     widths = [_width(t) for t, _ in extras]
     ldb = out_width + sum(widths)
     if ldb % 8:
         raise ValueError("concatenated feature width must be a multiple of 8")
-    base = torch.empty(n_samples, ldb, dtype=torch.bfloat16, device=dev)
-    attn = torch.empty(n_samples, dtype=torch.bfloat16, device=dev)
+    base = torch.empty(n_samples, ldb, dtype=dtype, device=dev)
+    attn = torch.empty(n_samples, dtype=dtype, device=dev)
     d = SigmaDesc()
+    d.dtype = _lib.DTYPE_F16 if dtype == torch.float16 else _lib.DTYPE_BF16
     d.variant = variant
     d.tile_cfg = tile_cfg
     d.n_samples = n_samples
@@ -228,11 +237,12 @@ def sigma_fwd(variant, packed, n_samples, inputs, extras, out_width, slope, tile
     return attn, base
 
 
-def reference_fwd(variant, weights, inputs, extras, n_samples, slope, bias=None, bias_div=1):
-    """Plain PyTorch statement of the same computation with the unfused bf16
-    path's roundings (fp32 GEMMs on bf16-rounded operands, bf16 outputs); the
-    test oracle for `sigma_fwd`.  Runs on any device."""
-    bf = torch.bfloat16
+def reference_fwd(variant, weights, inputs, extras, n_samples, slope, bias=None, bias_div=1,
+                  dtype=torch.bfloat16):
+    """Plain PyTorch statement of the same computation with the unfused
+    16-bit path's roundings (fp32 GEMMs on `dtype`-rounded operands, `dtype`
+    outputs); the test oracle for `sigma_fwd`.  Runs on any device."""
+    bf = dtype
 
     def lin(x, w, relu):
         y = (x.float() @ w.to(bf).float().t())

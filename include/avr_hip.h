@@ -228,10 +228,11 @@ int avr_hashgrid_fwd_lm(int64_t N, int32_t n_levels, const float* x, const void*
 /* AVRModel inference: the signal network's first-layer bias of every ray,
  * from the per-ray view direction and the per-pose tx position (model.py:221
  * concatenates both encodings to every sample):
- *   e_dir = bf16(enc(dir_grid((view[b][r*S] + 1) / 2))), e_tx likewise from
+ *   e_dir = mlp(enc(dir_grid((view[b][r*S] + 1) / 2))), e_tx likewise from
  *   tx[b][0];  bias[b*R + r][o] = sum_k e_dir[k] w_dir[k][o] + sum_k e_tx[k] w_tx[k][o]
  * view, tx [B][R*S][3] fp32 (network inputs in [-1, 1]); both grids' tables
  * in param_dtype; enc_dtype (F16/F32) the encodings' output rounding;
+ * mlp_dtype (BF16/F16) the MLP input rounding mlp(.);
  * w_dir [2*dir_levels][n_out], w_tx [2*tx_levels][n_out] fp32; bias
  * [B*R][n_out] fp32.  Level arrays are HOST pointers as above. */
 int avr_ray_pose_bias(int32_t B, int32_t R, int32_t S, const float* view, const float* tx,
@@ -239,8 +240,8 @@ int avr_ray_pose_bias(int32_t B, int32_t R, int32_t S, const float* view, const 
                       const float* dir_scale, const int32_t* dir_res, int32_t tx_levels,
                       const void* tx_params, const int64_t* tx_offset, const float* tx_scale,
                       const int32_t* tx_res, int32_t param_dtype, int32_t enc_dtype,
-                      const float* w_dir, const float* w_tx, int32_t n_out, float* bias,
-                      void* stream);
+                      int32_t mlp_dtype, const float* w_dir, const float* w_tx, int32_t n_out,
+                      float* bias, void* stream);
 
 /* grad_out[N][L*2] -> grad_params (fp32, accumulated with atomics; zero it
  * first). */
@@ -301,6 +302,8 @@ typedef struct {
     int32_t extra_width[AVR_SIGMA_MAX_EXTRA];
     const float* bias; /* AVR_SIGMA_MESHRIR_H1: [groups][512] fp32 */
     int32_t bias_div;  /* sample n uses bias row n / bias_div */
+    int32_t dtype;     /* MLP dtype: AVR_DTYPE_BF16 or AVR_DTYPE_F16 (tcnn's); packed
+                          weights, activations, base and attn are in it */
 } avr_sigma_desc;
 
 int avr_sigma_pack_bytes(int32_t variant, int64_t* bytes);

@@ -173,6 +173,12 @@ def test_variant_detection():
     assert sigma.variant_of(m32) is None
     r = AVRModel_complex(dict(RAF_MODEL, signal_output_dim=254), mlp_dtype=torch.bfloat16)
     assert sigma.variant_of(r) == sigma.RAF
+    # fp16 (tcnn's MLP precision) takes the fused kernel too
+    m16 = AVRModel(dict(MESHRIR_MODEL, signal_output_dim=254), mlp_dtype=torch.float16)
+    assert sigma.variant_of(m16) == sigma.MESHRIR and sigma.h1_ok(m16)
+    r16 = AVRModel_complex(dict(RAF_MODEL, signal_output_dim=254), mlp_dtype=torch.float16)
+    assert sigma.variant_of(r16) == sigma.RAF
+    assert sigma.pack_layers(sigma.RAF, _weights(sigma.RAF, 0), torch.float16).dtype == torch.float16
 
 
 def test_desc_struct_matches_library():

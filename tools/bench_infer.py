@@ -29,13 +29,13 @@ def main():
     ap.add_argument("--workload", default="c2_meshrir_1024x256x512")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mlp-dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--mlp-dtype", default="bf16", choices=["bf16", "fp16", "fp32"])
     ap.add_argument("--variants", default="unfused,fused_head_only,fused")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     w = WORKLOADS[args.workload]
     cfg = dict(MESHRIR_MODEL, signal_output_dim=w.T)
-    mlp_dtype = torch.bfloat16 if args.mlp_dtype == "bf16" else torch.float32
+    mlp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.mlp_dtype]
     model = AVRModel(cfg, mlp_dtype=mlp_dtype).to(dev)
     g = torch.Generator(device=dev).manual_seed(0)
     ro = torch.rand(w.batch, 3, device=dev, generator=g) * 4 - 2
