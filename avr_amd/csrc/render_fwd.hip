@@ -846,13 +846,11 @@ struct ReduceShape {
 template <int VEC>
 ReduceShape reduce_shape(int S, int T) {
     ReduceShape sh;
+    // one sample per column group: G = 1 beat G = 2 (and G = 2 beat G = 4)
+    // on configs 2 (fp32 and fp16) and 3 in every interleaved round of the
+    // round-2 sweeps (profiles/r02_sweepG_*.jsonl: config 2 fp32 111.8 vs
+    // 115.7 us per launch); fewer w/delay selects per loaded element
     sh.G = 1;
-    // super-rows of up to 512 chunks for fp32 (G = 2 at config 2: 5% faster
-    // than G = 1 in the same process, profiles/r01_sweep_g*.jsonl) and 256
-    // for 16-bit storage (more w/delay selects per byte: G = 4 measured 20%
-    // slower than G = 2 on config-2 shapes in fp16)
-    const int max_chunks = (VEC == 8) ? 256 : 512;
-    while (sh.G < 4 && 2 * sh.G * T <= max_chunks * VEC && 2 * sh.G <= S) sh.G *= 2;
     if (const char* g = getenv("AVR_REDUCE_G")) {  // tuning override (1, 2 or 4)
         const int v = atoi(g);
         if ((v == 1 || v == 2 || v == 4) && v <= S) sh.G = v;
