@@ -101,6 +101,8 @@ class TablePtrs(ctypes.Structure):
 _SIGS = {
     "avr_last_error": (ctypes.c_char_p, []),
     "avr_abi_version": (ctypes.c_int, []),
+    "avr_pinned_alloc": (ctypes.c_int, [_c_i64, _vp, _vp]),
+    "avr_pinned_free": (ctypes.c_int, [_vp]),
     "avr_tables": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "avr_depth_samples": (ctypes.c_int, [_vp, _vp, _vp]),
     "avr_ir_twiddle": (ctypes.c_int, [_c_i32, _vp, _vp]),
@@ -110,6 +112,7 @@ _SIGS = {
     "avr_weights_fwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32] + [_vp] * 7),
     "avr_ray_reduce_fwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32, _vp, _vp, _c_i32, _vp, _vp]),
     "avr_sample_rays_dev": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32] + [_vp] * 9),
+    "avr_sample_rays_staged": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32, _c_i32] + [_vp] * 7),
     "avr_reduce_splits": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp]),
     "avr_dft_phase_fwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32, _vp, _vp, _vp, _vp, _c_i32, _vp, _vp]),
     "avr_spectrum_finalize": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _vp, _vp, _vp]),

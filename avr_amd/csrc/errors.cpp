@@ -30,3 +30,25 @@ int check_launch(const char* what) {
 extern "C" const char* avr_last_error(void) { return avr::g_last_error.c_str(); }
 
 extern "C" int avr_abi_version(void) { return AVR_ABI_VERSION; }
+
+extern "C" int avr_pinned_alloc(int64_t bytes, void** host_ptr, void** dev_ptr) {
+    AVR_REQUIRE(bytes > 0 && host_ptr && dev_ptr, "avr_pinned_alloc: bad args");
+    *host_ptr = nullptr;
+    *dev_ptr = nullptr;
+    hipError_t e = hipHostMalloc(host_ptr, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return avr::fail((int)e, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    e = hipHostGetDevicePointer(dev_ptr, *host_ptr, 0);
+    if (e != hipSuccess) {
+        (void)hipHostFree(*host_ptr);
+        *host_ptr = nullptr;
+        return avr::fail((int)e, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e));
+    }
+    return 0;
+}
+
+extern "C" int avr_pinned_free(void* host_ptr) {
+    if (!host_ptr) return 0;
+    const hipError_t e = hipHostFree(host_ptr);
+    if (e != hipSuccess) return avr::fail((int)e, std::string("hipHostFree: ") + hipGetErrorString(e));
+    return 0;
+}

@@ -154,7 +154,14 @@ __global__ __launch_bounds__(kSampleThreads) void sample_rays_kernel(
     avr_render_params p, int B, AziJitter jit, const float* __restrict__ jit_dev, int r_begin,
     const float* __restrict__ rays_o, const float* __restrict__ pos_tx, const float* __restrict__ dir_tx,
     float* __restrict__ dirs, float* __restrict__ net_pts, float* __restrict__ net_view,
-    float* __restrict__ net_tx, float* __restrict__ net_dir_tx) {
+    float* __restrict__ net_tx, float* __restrict__ net_dir_tx, float* __restrict__ pose_out) {
+    if (pose_out && blockIdx.x == 0) {  // staged pose -> device copy for the later kernels
+        for (int i = threadIdx.x; i < 3 * B; i += kSampleThreads) {
+            pose_out[i] = rays_o[i];
+            pose_out[3 * B + i] = pos_tx[i];
+            if (dir_tx) pose_out[6 * B + i] = dir_tx[i];
+        }
+    }
     // directions of the (at most 256/S + 2) rays this block touches, once each
     __shared__ float sdir[kSampleThreads + 1][3];
     const int R = n_rays(p), S = p.n_samples;
@@ -166,6 +173,19 @@ __global__ __launch_bounds__(kSampleThreads) void sample_rays_kernel(
         const int r = r_begin + (int)((br0 + k) % R);
         const float u = r < p.n_azi * p.n_ele ? (jit_dev ? jit_dev[r / p.n_ele] : jit.u[r / p.n_ele]) : 0.0f;
         ray_direction(p, u, r, sdir[k]);
+    }
+    // the poses of the (at most 256/(R*S) + 2) listeners this block touches,
+    // read once per block (a staged pose lives in host memory: one bus read
+    // per block, not per sample)
+    __shared__ float spose[kSampleThreads + 1][9];
+    const int64_t b0 = br0 / R, b1 = br1 / R;
+    for (int k = threadIdx.x; k <= (int)(b1 - b0); k += kSampleThreads) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            spose[k][c] = rays_o[(b0 + k) * 3 + c];
+            spose[k][3 + c] = pos_tx[(b0 + k) * 3 + c];
+            spose[k][6 + c] = dir_tx ? dir_tx[(b0 + k) * 3 + c] : 0.0f;
+        }
     }
     __syncthreads();
     // stage the block's 256 x 3 outputs per tensor in LDS, then write them
@@ -179,6 +199,7 @@ __global__ __launch_bounds__(kSampleThreads) void sample_rays_kernel(
         const int rl = (int)(br % R);
         const int b = (int)(br / R);
         const float* dir = sdir[br - br0];
+        const float* pose = spose[b - b0];
         const float d = linspace_at(0.0f, 1.0f, S, s) * p.depth_scale + p.depth_offset;
         if (b == 0 && s == 0) {
             dirs[rl * 3 + 0] = dir[0];
@@ -187,11 +208,11 @@ __global__ __launch_bounds__(kSampleThreads) void sample_rays_kernel(
         }
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const float world = rays_o[b * 3 + c] + dir[c] * d;
+            const float world = pose[c] + dir[c] * d;
             obuf[0][threadIdx.x * 3 + c] = to_unit(world, p.lo, p.span);
             obuf[1][threadIdx.x * 3 + c] = -dir[c];
-            obuf[2][threadIdx.x * 3 + c] = to_unit(pos_tx[b * 3 + c], p.lo, p.span);
-            obuf[3][threadIdx.x * 3 + c] = dir_tx ? dir_tx[b * 3 + c] : 0.0f;
+            obuf[2][threadIdx.x * 3 + c] = to_unit(pose[3 + c], p.lo, p.span);
+            obuf[3][threadIdx.x * 3 + c] = pose[6 + c];
         }
     }
     __syncthreads();
@@ -771,7 +792,8 @@ extern "C" int avr_sample_rays(const avr_render_params* p, int32_t B, const floa
     hipLaunchKernelGGL(sample_rays_kernel, dim3((unsigned)((n + kSampleThreads - 1) / kSampleThreads)),
                        dim3(kSampleThreads), 0,
                        as_stream(stream), *p, (int)B, jit, (const float*)nullptr, (int)ray_begin, rays_o,
-                       pos_tx, dir_tx, dirs, net_pts, net_view, net_tx, dir_tx ? net_dir_tx : nullptr);
+                       pos_tx, dir_tx, dirs, net_pts, net_view, net_tx, dir_tx ? net_dir_tx : nullptr,
+                       (float*)nullptr);
     return check_launch("avr_sample_rays");
 }
 
@@ -792,8 +814,30 @@ extern "C" int avr_sample_rays_dev(const avr_render_params* p, int32_t B, const 
     hipLaunchKernelGGL(sample_rays_kernel, dim3((unsigned)((n + kSampleThreads - 1) / kSampleThreads)),
                        dim3(kSampleThreads), 0,
                        as_stream(stream), *p, (int)B, jit, u_azi_dev, (int)ray_begin, rays_o, pos_tx, dir_tx,
-                       dirs, net_pts, net_view, net_tx, dir_tx ? net_dir_tx : nullptr);
+                       dirs, net_pts, net_view, net_tx, dir_tx ? net_dir_tx : nullptr, (float*)nullptr);
     return check_launch("avr_sample_rays_dev");
+}
+
+extern "C" int avr_sample_rays_staged(const avr_render_params* p, int32_t B, const float* staged,
+                                      int32_t has_dir_tx, int32_t ray_begin, float* pose_out, float* dirs,
+                                      float* net_pts, float* net_view, float* net_tx, float* net_dir_tx,
+                                      void* stream) {
+    if (int e = validate(p)) return e;
+    AVR_REQUIRE(B >= 1 && staged && pose_out && dirs && net_pts && net_view && net_tx,
+                "avr_sample_rays_staged: bad args");
+    AVR_REQUIRE(!has_dir_tx || net_dir_tx, "avr_sample_rays_staged: dir_tx without net_dir_tx");
+    AVR_REQUIRE(ray_begin >= 0 && ray_begin + p->n_rays <= grid_rays(*p),
+                "avr_sample_rays_staged: ray range outside the sphere");
+    AziJitter jit{};
+    const float* ro = staged;
+    const float* tx = ro + 3 * B;
+    const float* dtx = has_dir_tx ? tx + 3 * B : nullptr;
+    const float* u = staged + 9 * B;
+    const int64_t n = (int64_t)B * n_rays(*p) * p->n_samples;
+    hipLaunchKernelGGL(sample_rays_kernel, dim3((unsigned)((n + kSampleThreads - 1) / kSampleThreads)),
+                       dim3(kSampleThreads), 0, as_stream(stream), *p, (int)B, jit, u, (int)ray_begin,
+                       ro, tx, dtx, dirs, net_pts, net_view, net_tx, dtx ? net_dir_tx : nullptr, pose_out);
+    return check_launch("avr_sample_rays_staged");
 }
 
 extern "C" int avr_weights_fwd(const avr_render_params* p, int32_t B, const void* attn,

@@ -460,7 +460,10 @@ class AVRRender(nn.Module):
         self.propagate_nonfinite = bool(kwargs.get("propagate_nonfinite", False))
         self._pcache = {}
         self._pcache_lock = threading.Lock()
-        self._jitter_dev = None  # device jitter buffer while a HIP graph is captured (avr_amd.graph)
+        # jitter the sampling kernel reads at run time while a HIP graph is
+        # captured (avr_amd.graph): a device tensor or a device address
+        self._jitter_dev = None
+        self._staged = None  # (device address, pose_out) of a staged pose block (avr_amd.graph)
         # bench/tuning instrumentation: an object whose events(...) returns the
         # hipEvent_t pair recorded around the ray reduction (bench.KernelTimer)
         self.kernel_timer = None
@@ -482,6 +485,8 @@ class AVRRender(nn.Module):
         jitter draw and the full direction set are still computed so every
         shard sees the same sphere.
         """
+        if self._staged is not None:
+            return self._sample_staged(position_tx.size(0), direction_tx is not None)
         dev = self._device(rays_o)
         B = position_tx.size(0)
         u_dev = self._jitter_dev if u_azi is None else None
@@ -512,7 +517,10 @@ class AVRRender(nn.Module):
             if u_dev is not None:
                 # graph capture: the jitter is read from device memory at replay
                 dirs = torch.empty(R, 3, **f32)
-                _lib.call("avr_sample_rays_dev", pref, B, _ptr(u_dev), r0, _ptr(rays_o),
+                # (a device tensor, or the device address of a pinned host
+                # buffer the captured kernel reads at replay: avr_amd.graph)
+                u_ptr = u_dev if isinstance(u_dev, int) else _ptr(u_dev)
+                _lib.call("avr_sample_rays_dev", pref, B, u_ptr, r0, _ptr(rays_o),
                           _ptr(position_tx), _ptr(direction_tx), _ptr(dirs), _ptr(pts), _ptr(view),
                           _ptr(tx), _ptr(dtx), st)
             elif p0.n_azi <= _lib.MAX_AZI:
@@ -536,6 +544,30 @@ class AVRRender(nn.Module):
                           _ptr(tx), _ptr(dtx), st)
         geom = dict(rays_o=rays_o, position_tx=position_tx, dirs=dirs, device=dev, B=B,
                     n_rays=R)
+        return pts, view, tx, dtx, geom
+
+    def _sample_staged(self, B, has_dtx):
+        """sample() with the pose and the jitter read at run time from the
+        staged block `self._staged = (device address, pose_out)` (HIP-graph
+        capture with host-side poses, avr_amd.graph): the kernel publishes
+        the pose into pose_out [9B] on the device for the render core."""
+        staged_ptr, pose_out = self._staged
+        dev = pose_out.device
+        R_all = int(self.n_azi) * int(self.n_ele) + 2
+        r0, r1 = self.ray_range if self.ray_range is not None else (0, R_all)
+        p0 = self._params(2, r1 - r0)
+        R, S = r1 - r0, p0.n_samples
+        f32 = dict(dtype=torch.float32, device=dev)
+        pts = torch.empty(B, R * S, 3, **f32)
+        view = torch.empty(B, R * S, 3, **f32)
+        tx = torch.empty(B, R * S, 3, **f32)
+        dtx = torch.empty(B, R * S, 3, **f32) if has_dtx else None
+        dirs = torch.empty(R, 3, **f32)
+        with _on(dev):
+            _lib.call("avr_sample_rays_staged", ctypes_ref(p0), B, staged_ptr, int(has_dtx), r0,
+                      _ptr(pose_out), _ptr(dirs), _ptr(pts), _ptr(view), _ptr(tx), _ptr(dtx), _stream(dev))
+        geom = dict(rays_o=pose_out[:3 * B].view(B, 3), position_tx=pose_out[3 * B:6 * B].view(B, 3),
+                    dirs=dirs, device=dev, B=B, n_rays=R)
         return pts, view, tx, dtx, geom
 
     def _params(self, T, R):

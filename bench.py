@@ -364,14 +364,37 @@ def bench_pose(args, w, world, rank, dev):
     run(args.warmup, n_streams)
     torch.cuda.synchronize()
 
-    # latency: one pose at a time on one stream (IR render ms/pose)
+    # latency: one pose at a time on one stream (IR render ms/pose), issued
+    # eagerly and replayed from a HIP graph (avr_amd.graph.GraphedRender:
+    # same kernels and results bit for bit, no per-launch host work)
     n_lat = max(5, min(args.steps, 20))
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(n_lat):
-        step(0)
+
+    def latency(fn):
         torch.cuda.synchronize()
-    latency_ms = (time.perf_counter() - t0) * 1e3 / n_lat
+        t0 = time.perf_counter()
+        for _ in range(n_lat):
+            fn()
+            torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3 / n_lat
+
+    latency_eager_ms = latency(lambda: step(0))
+    from avr_amd.graph import GraphedRender
+
+    graphed = GraphedRender(renderers[0])
+    # poses handed over from the host, as a data loader yields them
+    # (avr_runner.py:168): staged in the replay's pinned buffer, no copy
+    ro_h, tx_h = rays_o.cpu(), tx.cpu()
+    dtx_h = [None if d is None else d.cpu() for d in dtx]
+
+    def step_graph():
+        i = pose[0] % P
+        pose[0] += 1
+        with torch.no_grad():
+            return graphed.render_ir(ro_h[i], tx_h[i], dtx_h[i])
+
+    for _ in range(graphed.ring + 2):  # captures
+        step_graph()
+    latency_ms = latency(step_graph)
 
     # roofline phase: K launches on ONE stream with HIP events around the
     # dominant kernel on its stream, so no other kernel overlaps it and the
@@ -388,6 +411,8 @@ def bench_pose(args, w, world, rank, dev):
     res = _base_result(args, w, world, value, elapsed, "f32" if dt == torch.float32 else "f16-storage/f32-math")
     res.update({
         "ir_render_ms_per_pose": latency_ms / B,
+        "ir_render_path": "HIP-graph replay (avr_amd.graph.GraphedRender), host poses, synchronized per pose",
+        "ir_render_ms_per_pose_eager": latency_eager_ms / B,
         "host_issue_ms_per_step": t_issue * 1e3 / args.steps,
         "streams": n_streams,
         "config": {"workload": w.name, "mode": "pose", "rays": R, "samples": S, "T": T, "freq_bins": w.F,

@@ -72,6 +72,14 @@ typedef struct avr_render_params {
 const char* avr_last_error(void);
 int avr_abi_version(void);
 
+/* Host memory the GPU reads directly (pinned, mapped, fine-grained coherent:
+ * every device read goes over the bus, no stale cache lines).  Used for
+ * per-call scalars a captured HIP graph reads at replay (the azimuth jitter
+ * of avr_sample_rays_dev), so a replay needs no host-to-device copy.
+ * *dev_ptr is the address kernels use. */
+int avr_pinned_alloc(int64_t bytes, void** host_ptr, void** dev_ptr);
+int avr_pinned_free(void* host_ptr);
+
 /* ---- pose-independent tables (cached per device by the host) ----------
  * d_vals[S], frac[S] (= pts2rx_idx), shift[S] (int), pl_table[pl_len],
  * phase[S][F][2] (cos, sin of the fractional-delay phase),
@@ -118,6 +126,16 @@ int avr_sample_rays_dev(const avr_render_params* p, int32_t B, const float* u_az
                         int32_t ray_begin, const float* rays_o, const float* pos_tx,
                         const float* dir_tx, float* dirs, float* net_pts, float* net_view,
                         float* net_tx, float* net_dir_tx, void* stream);
+/* The same with the jitter AND the pose read from one staged block when the
+ * kernel runs: staged = [rays_o (B*3) | pos_tx (B*3) | dir_tx (B*3, read if
+ * has_dir_tx) | u_azi (n_azi)], typically device-mapped pinned host memory
+ * (avr_pinned_alloc) that a HIP-graph replay refreshes from the host with no
+ * copy.  The pose is also published to device memory for the later kernels:
+ * pose_out[0..3B) = rays_o, [3B..6B) = pos_tx, [6B..9B) = dir_tx. */
+int avr_sample_rays_staged(const avr_render_params* p, int32_t B, const float* staged,
+                           int32_t has_dir_tx, int32_t ray_begin, float* pose_out, float* dirs,
+                           float* net_pts, float* net_view, float* net_tx, float* net_dir_tx,
+                           void* stream);
 
 /* ---- a8 + a11: source delays and compositing weights -------------------
  * attn [B][R*S] (dtype), writes w[B][R][S] fp32 and delay[B][R][S] int32.

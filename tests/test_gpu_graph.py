@@ -21,8 +21,12 @@ class Stub(torch.nn.Module):
         return self.a, self.s
 
 
+@pytest.mark.parametrize("host_pose", [False, True])
 @pytest.mark.parametrize("name", ["c2_meshrir_1024x256x512", "c3_raf_furnished_b4"])
-def test_graph_replay_equals_eager(name):
+def test_graph_replay_equals_eager(name, host_pose):
+    """Device poses (copied into the graph's tensors) and host poses (staged
+    in the pinned buffer, published by the sampling kernel) both replay the
+    eager render bit for bit."""
     w = WORKLOADS[name]
     B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
     g = torch.Generator(device=DEV).manual_seed(1)
@@ -30,7 +34,7 @@ def test_graph_replay_equals_eager(name):
     sig = torch.randn(B, R * S, T, device=DEV, generator=g) * 0.1
     r = AVRRender(Stub(attn, sig), **w.render)
     gr = GraphedRender(r)
-    for k in range(3):  # capture, then replays with new poses and jitter
+    for k in range(5):  # captures (ring of 3), then replays with new poses and jitter
         ro = torch.rand(B, 3, device=DEV, generator=g) * 4 - 2
         tx = torch.rand(B, 3, device=DEV, generator=g) * 4 - 2
         dtx = (torch.nn.functional.normalize(torch.randn(B, 3, device=DEV, generator=g), dim=-1)
@@ -39,11 +43,40 @@ def test_graph_replay_equals_eager(name):
             torch.manual_seed(10 + k)
             out_e, ir_e = r.render_ir(ro, tx, dtx)
             torch.manual_seed(10 + k)
-            out_g, ir_g = gr.render_ir(ro, tx, dtx)
+            if host_pose:
+                out_g, ir_g = gr.render_ir(ro.cpu(), tx.cpu(), None if dtx is None else dtx.cpu())
+            else:
+                out_g, ir_g = gr.render_ir(ro, tx, dtx)
             torch.cuda.synchronize()
         assert torch.equal(out_g, out_e), k
         assert torch.equal(ir_g, ir_e), k
     assert len(gr._graphs) == 1
+
+
+def test_graph_ring_pipelined_replays():
+    """Replays issued back to back without a host sync: each ring instance
+    is reused only after its previous replay ran, so every render keeps its
+    own host pose and jitter draw (compared with eager renders of the same
+    seeds and poses)."""
+    w = WORKLOADS["c1_meshrir_plumbing"]
+    B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
+    g = torch.Generator(device=DEV).manual_seed(2)
+    attn = torch.rand(B, R * S, 1, device=DEV, generator=g) * 2
+    sig = torch.randn(B, R * S, T, device=DEV, generator=g) * 0.1
+    r = AVRRender(Stub(attn, sig), **w.render)
+    gr = GraphedRender(r, ring=3)
+    n = 8
+    ros = [torch.full((B, 3), 0.1 * k - 0.3) for k in range(n)]  # host poses, one per render
+    tx = torch.full((B, 3), 0.3)
+    with torch.no_grad():
+        torch.manual_seed(42)
+        got = [gr.render_ir(ros[k], tx)[1].clone() for k in range(n)]
+        torch.manual_seed(42)
+        ref = [r.render_ir(ros[k].to(DEV), tx.to(DEV))[1].clone() for k in range(n)]
+    torch.cuda.synchronize()
+    for k in range(n):
+        assert torch.equal(got[k], ref[k]), k
+    assert not all(torch.equal(got[0], x) for x in got[1:])  # the jitter did change
 
 
 @pytest.mark.parametrize("mlp_dtype", [torch.bfloat16, torch.float32])
