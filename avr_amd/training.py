@@ -180,22 +180,50 @@ class TrainStep:
         return total.detach(), [x.detach() for x in losses[:8]]
 
     # ------------------------------------------------------ checkpoints
-    def save_checkpoint(self, path):
-        """The reference's `.tar` layout (avr_runner.py:148-153)."""
+    def save_checkpoint(self, path, reference_layout=False):
+        """The reference's `.tar` layout (avr_runner.py:148-153).  With
+        `reference_layout` the networks are written as tcnn's flat `params`
+        (avr_amd.tcnn_compat), the form the reference's modules load."""
+        from .tcnn_compat import to_reference
+
         model = self.renderer.module if hasattr(self.renderer, "module") else self.renderer
         torch.save({
             'current_iteration': self.current_iteration,
-            'audionerf_network_state_dict': model.state_dict(),
+            'audionerf_network_state_dict': to_reference(model) if reference_layout else model.state_dict(),
             'optimizer_state_dict': self.optimizer.state_dict(),
             'scheduler_state_dict': self.scheduler.state_dict(),
         }, path)
         return path
 
     def load_checkpoint(self, path):
-        """avr_runner.py:105-130: restore weights, optimiser, scheduler, iteration."""
+        """avr_runner.py:105-130: restore weights, optimiser, scheduler, iteration.
+
+        A checkpoint written by the reference (tcnn networks: one flat
+        `params` per network) is recognised and converted
+        (avr_amd.tcnn_compat.from_reference).  Its Adam state is laid out
+        over the reference's flat parameters, so it is restored only when
+        every state tensor matches this model's parameter shapes; otherwise
+        the optimiser starts fresh (a warning says so)."""
+        import warnings
+
+        from .tcnn_compat import from_reference, is_reference_layout
+
         ckpt = torch.load(path, map_location="cpu", weights_only=True)
         model = self.renderer.module if hasattr(self.renderer, "module") else self.renderer
-        model.load_state_dict(ckpt['audionerf_network_state_dict'])
+        sd = ckpt['audionerf_network_state_dict']
+        if is_reference_layout(model, sd):
+            from_reference(model, sd)
+            shapes = [p.shape for g in self.optimizer.param_groups for p in g['params']]
+            st = ckpt['optimizer_state_dict'].get('state', {})
+            if any(int(i) >= len(shapes) or v.get('exp_avg', torch.empty(shapes[int(i)])).shape != shapes[int(i)]
+                   for i, v in st.items()):
+                warnings.warn("reference checkpoint: Adam state is over tcnn's flat parameters; "
+                              "optimizer state not restored", RuntimeWarning)
+                self.scheduler.load_state_dict(ckpt['scheduler_state_dict'])
+                self.current_iteration = int(ckpt['current_iteration'])
+                return ckpt
+        else:
+            model.load_state_dict(sd)
         self.optimizer.load_state_dict(ckpt['optimizer_state_dict'])
         self.scheduler.load_state_dict(ckpt['scheduler_state_dict'])
         self.current_iteration = int(ckpt['current_iteration'])

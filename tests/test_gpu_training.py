@@ -113,6 +113,47 @@ def test_checkpoint_round_trip(tmp_path):
 
 
 @pytest.mark.gpu
+def test_checkpoint_reference_layout(tmp_path):
+    """A checkpoint whose networks are tcnn flat `params` (the reference's
+    modules, avr_amd.tcnn_compat) restores the same weights: written by
+    save_checkpoint(reference_layout=True) it resumes exactly; with the
+    reference's flat-parameter Adam state the weights load and the
+    optimiser restarts with a warning."""
+    r, ori, rx, tx, dtx = _setup()
+    step = TrainStep(r, RAF_TRAIN, dict(fs=16000, speed=346.8))
+    for _ in range(2):
+        torch.manual_seed(1)
+        step(ori, rx, tx, dtx)
+    path = step.save_checkpoint(str(tmp_path / "ref.tar"), reference_layout=True)
+    sd = torch.load(path, weights_only=True)["audionerf_network_state_dict"]
+    assert any(k.endswith("_model_signal.params") for k in sd) and not any(".layers." in k for k in sd)
+    torch.manual_seed(1)
+    ref_total, _ = step(ori, rx, tx, dtx)
+
+    r2, _, _, _, _ = _setup(seed=123)
+    step2 = TrainStep(r2, RAF_TRAIN, dict(fs=16000, speed=346.8))
+    step2.load_checkpoint(path)
+    torch.manual_seed(1)
+    total2, _ = step2(ori, rx, tx, dtx)
+    assert abs(float(total2) - float(ref_total)) <= 1e-6 * abs(float(ref_total))
+
+    # the reference's own optimiser state: one moment tensor per flat params
+    ck = torch.load(path, weights_only=True)
+    flat = [v for k, v in ck["audionerf_network_state_dict"].items() if k.endswith(".params")]
+    ck["optimizer_state_dict"]["state"] = {
+        i: {"step": torch.tensor(2.0), "exp_avg": torch.zeros_like(v), "exp_avg_sq": torch.zeros_like(v)}
+        for i, v in enumerate(flat)}
+    ck["optimizer_state_dict"]["param_groups"][0]["params"] = list(range(len(flat)))
+    torch.save(ck, str(tmp_path / "ref_opt.tar"))
+    r3, _, _, _, _ = _setup(seed=321)
+    step3 = TrainStep(r3, RAF_TRAIN, dict(fs=16000, speed=346.8))
+    with pytest.warns(RuntimeWarning, match="optimizer state not restored"):
+        step3.load_checkpoint(str(tmp_path / "ref_opt.tar"))
+    for (k, a), b in zip(r2.state_dict().items(), r3.state_dict().values()):
+        assert torch.equal(a, b), k
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("wd", [0.0, 1e-2])
 def test_native_adam_matches_torch_adam(wd):
     """clip_sanitize_adam_ (avr_adam_step) against clip_and_sanitize_ +
