@@ -32,6 +32,10 @@ CASES = [
     ("raf_c3_like", RAF, 36, 18, 32, 1600, 512, 1),
     ("simu_long_T", SIMU, 8, 4, 48, 4094, 128, 1),
     ("meshrir_odd", dict(MESHRIR, xyz_min=0, xyz_max=10), 5, 3, 40, 510, 96, 3),
+    # K = 512: the reference networks' width (model.py:176-180)
+    ("meshrir_k512", MESHRIR, 16, 8, 64, 1022, 512, 2),
+    ("simu_long_k512", SIMU, 8, 4, 48, 4094, 512, 1),
+    ("ragged_k512", dict(MESHRIR, xyz_min=0, xyz_max=10), 5, 3, 40, 510, 512, 3),
 ]
 
 
@@ -204,3 +208,28 @@ def test_fused_head_model_reference_precision(mlp_dtype):
         end_to_end = r(ro, tx, dtx)  # the module's forward takes the fused path
     assert _rel(fused, plain) < 2e-5, _rel(fused, plain)
     assert torch.equal(end_to_end, fused)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_fused_head_config2_full_size(dtype):
+    """Config 2 at full size (1024 rays x 256 samples x T=1022, K=512): the
+    fused head against the plain render of h @ W^T; repeat renders equal."""
+    from avr_amd.workloads import WORKLOADS
+
+    w = WORKLOADS["c2_meshrir_1024x256x512"]
+    B, R, S, T, K = w.batch, w.n_rays, w.n_samples, w.T, 512
+    g = torch.Generator(device=DEV).manual_seed(9)
+    ro = torch.rand(B, 3, device=DEV, generator=g) * 4 - 2
+    tx = torch.rand(B, 3, device=DEV, generator=g) * 4 - 2
+    attn = torch.rand(B, R * S, 1, device=DEV, generator=g) * 2
+    h = torch.relu(torch.randn(B, R * S, K, device=DEV, generator=g)).to(dtype)
+    W = torch.randn(T, K, device=DEV, generator=g) / K ** 0.5
+    r = AVRRender(None, **w.render)
+    torch.manual_seed(5)
+    _, _, _, _, geom = r.sample(ro, tx)
+    with torch.no_grad():
+        fused = r.render_from_hidden(attn, h, W, dtype, geom)
+        again = r.render_from_hidden(attn, h, W, dtype, geom)
+        plain = r.render_from_network_output(attn, h.float() @ W.to(dtype).float().t(), geom)
+    assert torch.equal(fused, again)
+    assert _rel(fused, plain) < 2e-5, _rel(fused, plain)
