@@ -152,7 +152,7 @@ def test_checkpoint_reference_layout(tmp_path):
     from avr_amd.tcnn_compat import to_reference
     got = to_reference(r3)
     for k, v in ck["audionerf_network_state_dict"].items():
-        assert torch.equal(got[k].cpu(), v), k
+        assert torch.equal(got[k].cpu(), v.cpu()), k
 
 
 @pytest.mark.gpu
