@@ -103,6 +103,7 @@ _SIGS = {
     "avr_abi_version": (ctypes.c_int, []),
     "avr_pinned_alloc": (ctypes.c_int, [_c_i64, _vp, _vp]),
     "avr_pinned_free": (ctypes.c_int, [_vp]),
+    "avr_graph_launch": (ctypes.c_int, [_vp, _vp]),
     "avr_tables": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "avr_depth_samples": (ctypes.c_int, [_vp, _vp, _vp]),
     "avr_ir_twiddle": (ctypes.c_int, [_c_i32, _vp, _vp]),

@@ -52,3 +52,13 @@ extern "C" int avr_pinned_free(void* host_ptr) {
     if (e != hipSuccess) return avr::fail((int)e, std::string("hipHostFree: ") + hipGetErrorString(e));
     return 0;
 }
+
+// Launch of an instantiated graph (torch.cuda.CUDAGraph.raw_cuda_graph_exec)
+// without torch's replay prologue, which refreshes the device RNG's
+// seed/offset tensors: the render graphs draw nothing on the device.
+extern "C" int avr_graph_launch(void* graph_exec, void* stream) {
+    AVR_REQUIRE(graph_exec != nullptr, "avr_graph_launch: null graph");
+    const hipError_t e = hipGraphLaunch((hipGraphExec_t)graph_exec, (hipStream_t)stream);
+    if (e != hipSuccess) return avr::fail((int)e, std::string("hipGraphLaunch: ") + hipGetErrorString(e));
+    return 0;
+}

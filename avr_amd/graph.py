@@ -113,6 +113,12 @@ class GraphedRender:
             g.graph = torch.cuda.CUDAGraph()
             with torch.no_grad(), torch.cuda.graph(g.graph):
                 g.out, g.ir = r.render_ir(g.ro, g.tx, g.dtx)
+            # replayed by avr_graph_launch: the render draws no device random
+            # numbers, so torch's replay prologue (device-RNG seed/offset
+            # refresh) has nothing to do
+            g.exec = int(g.graph.raw_cuda_graph_exec())
+            g.pose_np = g.pose_h.numpy()
+            g.jit_n = n_azi + n_ele
         finally:
             r._jitter_dev = None
             r._staged = None
@@ -135,23 +141,24 @@ class GraphedRender:
                                        self.warmup if not insts else 0))
         g = insts[k]
         slot[1] = (k + 1) % self.ring
-        if g.done is not None:
+        if g.done is not None and not g.done.query():
             g.done.synchronize()  # its previous replay has read the buffer
         # the eager path's two CPU-generator draws (renderer.draw_jitter) in
         # one call (the generator fills them in order: tests/test_graph_cpu.py),
         # straight into the buffer the captured kernel reads
-        torch.rand(int(r.n_azi) + int(r.n_ele), out=g.jit_h)
+        torch.rand(g.jit_n, out=g.jit_h)
         B = g.B
         if g.host_pose:
-            g.pose_h[:3 * B].copy_(rays_o.reshape(-1))
-            g.pose_h[3 * B:6 * B].copy_(position_tx.reshape(-1))
+            p = g.pose_np  # numpy view of the pinned buffer: no dispatcher per copy
+            p[:3 * B] = rays_o.detach().reshape(-1).numpy()
+            p[3 * B:6 * B] = position_tx.detach().reshape(-1).numpy()
             if g.has_dtx:
-                g.pose_h[6 * B:].copy_(direction_tx.reshape(-1))
+                p[6 * B:] = direction_tx.detach().reshape(-1).numpy()
         elif g.dtx is not None:
             torch._foreach_copy_([g.ro, g.tx, g.dtx], [rays_o, position_tx, direction_tx])
         else:
             torch._foreach_copy_([g.ro, g.tx], [rays_o, position_tx])
-        g.graph.replay()
+        _lib.call("avr_graph_launch", g.exec, torch._C._cuda_getCurrentRawStream(dev.index))
         g.done = g.done or torch.cuda.Event()
         g.done.record()
         return g.out, g.ir

@@ -80,6 +80,12 @@ int avr_abi_version(void);
 int avr_pinned_alloc(int64_t bytes, void** host_ptr, void** dev_ptr);
 int avr_pinned_free(void* host_ptr);
 
+/* Launch an instantiated HIP graph (hipGraphExec_t) on a stream: the replay
+ * of a captured render (avr_amd.graph.GraphedRender) without the host work
+ * torch's CUDAGraph.replay adds for device-RNG state.  Valid only for graphs
+ * that draw no device random numbers (the render path draws on the CPU). */
+int avr_graph_launch(void* graph_exec, void* stream);
+
 /* ---- pose-independent tables (cached per device by the host) ----------
  * d_vals[S], frac[S] (= pts2rx_idx), shift[S] (int), pl_table[pl_len],
  * phase[S][F][2] (cos, sin of the fractional-delay phase),
