@@ -113,10 +113,12 @@ class GraphedRender:
             g.graph = torch.cuda.CUDAGraph()
             with torch.no_grad(), torch.cuda.graph(g.graph):
                 g.out, g.ir = r.render_ir(g.ro, g.tx, g.dtx)
-            # replayed by avr_graph_launch: the render draws no device random
-            # numbers, so torch's replay prologue (device-RNG seed/offset
-            # refresh) has nothing to do
-            g.exec = int(g.graph.raw_cuda_graph_exec())
+            # networks that declare `draws_no_device_rng` (ours; no dropout)
+            # are replayed by avr_graph_launch: the render itself draws on the
+            # CPU, so torch's replay prologue (device-RNG seed/offset refresh)
+            # has nothing to do.  Any other network keeps CUDAGraph.replay.
+            g.exec = (int(g.graph.raw_cuda_graph_exec())
+                      if getattr(r.network_fn, "draws_no_device_rng", False) else None)
             g.pose_np = g.pose_h.numpy()
             g.jit_n = n_azi + n_ele
         finally:
@@ -158,7 +160,10 @@ class GraphedRender:
             torch._foreach_copy_([g.ro, g.tx, g.dtx], [rays_o, position_tx, direction_tx])
         else:
             torch._foreach_copy_([g.ro, g.tx], [rays_o, position_tx])
-        _lib.call("avr_graph_launch", g.exec, torch._C._cuda_getCurrentRawStream(dev.index))
+        if g.exec is not None:
+            _lib.call("avr_graph_launch", g.exec, torch._C._cuda_getCurrentRawStream(dev.index))
+        else:
+            g.graph.replay()
         g.done = g.done or torch.cuda.Event()
         g.done.record()
         return g.out, g.ir

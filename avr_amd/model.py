@@ -348,6 +348,9 @@ class AVRModel(nn.Module):
     # ... and folds the signal network's last layer into the render
     # (forward_fused / finish_signal) for networks that declare this
     supports_fused_head = True
+    # no dropout or other device RNG: a captured render replays without
+    # torch's RNG prologue (avr_amd.graph)
+    draws_no_device_rng = True
 
     def _trunk(self, pts, view, tx, ch_idx, ray_layout):
         """Everything up to the signal network's input: (attn, features)."""
@@ -463,6 +466,7 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
 
     accepts_ray_layout = True
     supports_fused_head = True
+    draws_no_device_rng = True
 
     def forward(self, pts, view, tx, tx_view, ray_layout=None):
         attn, base = self._trunk(pts, view, tx, tx_view, ray_layout)

@@ -51,6 +51,8 @@ MODES = {  # mode -> default workload (avr_amd.workloads.WORKLOADS)
 
 
 class StubNet(torch.nn.Module):
+    draws_no_device_rng = True  # avr_amd.graph: replay without torch's RNG prologue
+
     def __init__(self, attn, signal):
         super().__init__()
         self.attn, self.signal = attn, signal

@@ -13,6 +13,8 @@ DEV = torch.device("cuda", 0)
 
 
 class Stub(torch.nn.Module):
+    draws_no_device_rng = True
+
     def __init__(self, a, s):
         super().__init__()
         self.a, self.s = a, s
@@ -21,18 +23,25 @@ class Stub(torch.nn.Module):
         return self.a, self.s
 
 
+class StubUndeclared(Stub):
+    """A network that does not declare itself free of device RNG."""
+    draws_no_device_rng = False
+
+
+@pytest.mark.parametrize("net", [Stub, StubUndeclared])
 @pytest.mark.parametrize("host_pose", [False, True])
 @pytest.mark.parametrize("name", ["c2_meshrir_1024x256x512", "c3_raf_furnished_b4"])
-def test_graph_replay_equals_eager(name, host_pose):
+def test_graph_replay_equals_eager(name, host_pose, net):
     """Device poses (copied into the graph's tensors) and host poses (staged
     in the pinned buffer, published by the sampling kernel) both replay the
-    eager render bit for bit."""
+    eager render bit for bit, launched by avr_graph_launch (declared
+    RNG-free network) or by torch's CUDAGraph.replay (any other)."""
     w = WORKLOADS[name]
     B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
     g = torch.Generator(device=DEV).manual_seed(1)
     attn = torch.rand(B, R * S, 1, device=DEV, generator=g) * 2
     sig = torch.randn(B, R * S, T, device=DEV, generator=g) * 0.1
-    r = AVRRender(Stub(attn, sig), **w.render)
+    r = AVRRender(net(attn, sig), **w.render)
     gr = GraphedRender(r)
     for k in range(5):  # captures (ring of 3), then replays with new poses and jitter
         ro = torch.rand(B, 3, device=DEV, generator=g) * 4 - 2
@@ -51,6 +60,8 @@ def test_graph_replay_equals_eager(name, host_pose):
         assert torch.equal(out_g, out_e), k
         assert torch.equal(ir_g, ir_e), k
     assert len(gr._graphs) == 1
+    inst = next(iter(gr._graphs.values()))[0][0]
+    assert (inst.exec is not None) == (net is Stub)
 
 
 def test_graph_ring_pipelined_replays():

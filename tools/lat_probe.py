@@ -17,6 +17,8 @@ from avr_amd.workloads import WORKLOADS  # noqa: E402
 
 
 class Stub(torch.nn.Module):
+    draws_no_device_rng = True
+
     def __init__(self, a, s):
         super().__init__()
         self.a, self.s = a, s
