@@ -51,6 +51,9 @@ def test_argument_errors_are_reported_without_gpu(lib):
     rc = lib.avr_tables(None, None, None, None, None, None, None, None)
     assert rc == 1001
     assert b"null" in lib.avr_last_error()
+    # a graph launch without an instantiated graph is refused before any HIP call
+    assert lib.avr_graph_launch(None, None) == 1001
+    assert b"avr_graph_launch" in lib.avr_last_error()
 
 
 def test_code_object_targets_gfx950(lib):
