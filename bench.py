@@ -120,6 +120,8 @@ def parse_args(argv=None):
     ap.add_argument("--workload", default=None, help="default: the mode's workload")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--no-network", action="store_true",
+                    help="pose mode: skip the config-2 inference through the reference network")
     ap.add_argument("--poses", type=int, default=16,
                     help="distinct synthetic poses cycled over the steps")
     ap.add_argument("--streams", type=int, default=2,
@@ -297,6 +299,48 @@ def cpu_baseline(w, budget_s=15.0):
         "sample": f"{len(times)} full poses of {w.name} (forward + irfft), best of {len(times)}; "
                   f"median {sorted(times)[len(times) // 2] * 1e3:.1f} ms/pose",
         "ms_per_pose": best * 1e3,
+    }
+
+
+def network_inference(w, dev, steps=20, warmup=3):
+    """Config-2 inference through the reference's own network, not the stub:
+    AVRModel with the avr_meshrir.yml `model:` block (random init), MLPs in
+    fp16 as tcnn runs them (model.py:21-31), one pose per step, no grad,
+    through the IR.  The default path: level-major hash grids, fused sigma
+    networks and first signal layer (csrc/sigma.hip), hipBLASLt for the two
+    512x512 signal layers, the fused signal head (csrc/head.hip) and the
+    render tail.  Reported beside `value`, which stays SURVEY §8(d)'s
+    stub-network metric."""
+    from avr_amd import AVRRender, spectrum_to_ir
+    from avr_amd.model import AVRModel
+    from avr_amd.workloads import MESHRIR_MODEL
+
+    torch.manual_seed(0)
+    model = AVRModel(dict(MESHRIR_MODEL, signal_output_dim=w.T), mlp_dtype=torch.float16).to(dev)
+    r = AVRRender(model, **w.render)
+    g = torch.Generator(device=dev).manual_seed(0)
+    ro = torch.rand(w.batch, 3, device=dev, generator=g) * 4 - 2
+    tx = torch.rand(w.batch, 3, device=dev, generator=g) * 4 - 2
+
+    def step():
+        with torch.no_grad():
+            return spectrum_to_ir(r(ro, tx))
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    return {
+        "network": "AVRModel (avr_meshrir.yml model block, random init), fp16 MLPs (tcnn precision)",
+        "path": "level-major hash grids + fused sigma networks + hipBLASLt 512x512 layers + fused signal head "
+                "+ render + irfft",
+        "ms_per_pose": ms,
+        "ray_samples_per_s": w.ray_samples / (ms * 1e-3),
+        "steps": steps,
     }
 
 
@@ -574,6 +618,9 @@ def main(argv=None):
     result = fn(args, w, world, rank, dev)
     if rank == 0 and world == 1 and args.mode == "pose" and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(w, args.cpu_budget)
+    if rank == 0 and world == 1 and args.mode == "pose" and w.name.startswith("c2_meshrir") \
+            and not args.no_network:
+        result["network_inference"] = network_inference(w, dev)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
