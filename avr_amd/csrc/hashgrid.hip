@@ -76,6 +76,16 @@ inline int64_t lm_min_points() {
     return v;
 }
 
+// grouped corner loads in the level-major forward (AVR_HASHGRID_GROUP=0
+// turns them off; experiments)
+inline bool group_loads() {
+    static const bool v = [] {
+        const char* e = getenv("AVR_HASHGRID_GROUP");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 struct Corner {
     float pos[3];
     uint32_t grid[3];
@@ -140,7 +150,40 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(int64_t N, int L,
 // output of hashgrid_fwd_kernel (avr_hashgrid_fwd for large N: training's
 // per-sample grids).  The 8-byte stores are strided, but they are 1/8 of the
 // gathered bytes; the gathers are what the L2-resident level saves.
-template <typename Tp, typename To, bool ROW_MAJOR = false>
+//
+// GROUP (fp16 tables): the two x-neighbour corners of a cell edge usually
+// sit in one aligned 16-byte group of 4 table entries: on hashed levels x
+// enters the hash with prime 1, so x -> x+1 flips only the trailing bits of
+// the entry (x mod 4 != 3: same group); on dense levels the entry is the
+// next one.  Each edge therefore issues one 16-byte load of the group
+// holding its first corner, and a second (exec-masked) load only in the
+// lanes whose second corner lies outside it: fewer address lookups per wave
+// than 8 separate loads, the same values, the same fmaf order (bit-identical
+// output).  Needs a 16-byte aligned table base (level sizes are multiples of
+// 8 entries); the host checks.
+template <typename Tp>
+struct EntryGroup;
+template <>
+struct EntryGroup<__half> {
+    static constexpr uint32_t kN = 4;
+    uint32_t d[4];
+    __device__ __forceinline__ void load(const __half* table, uint32_t e) {
+        const uint4 v = *reinterpret_cast<const uint4*>(table + 2 * (e & ~(kN - 1)));
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
+    }
+    __device__ __forceinline__ float2 get(uint32_t e) const {
+        const uint32_t j = e & (kN - 1);
+        const uint32_t v = j == 0 ? d[0] : j == 1 ? d[1] : j == 2 ? d[2] : d[3];
+        __half2 h;
+        __builtin_memcpy(&h, &v, 4);
+        return __half22float2(h);
+    }
+};
+
+template <typename Tp, typename To, bool ROW_MAJOR = false, bool GROUP = false>
 __global__ __launch_bounds__(256) void hashgrid_fwd_lm_kernel(int64_t N, const float* __restrict__ x,
                                                               const Tp* __restrict__ params,
                                                               LevelTable lt, To* __restrict__ out) {
@@ -153,23 +196,53 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_lm_kernel(int64_t N, const f
     const uint32_t res = lt.res[l];
     const Tp* table = params + 2 * lt.offset[l];
     float2 acc = make_float2(0.0f, 0.0f);
+    // corner weights and entries in the order k = 0..7 (x bit fastest)
+    float wgt[8];
+    uint32_t ent[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        float wgt = 1.0f;
+        float w = 1.0f;
         uint32_t g[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
             if (k & (1 << d)) {
-                wgt *= c.pos[d];
+                w *= c.pos[d];
                 g[d] = c.grid[d] + 1;
             } else {
-                wgt *= 1.0f - c.pos[d];
+                w *= 1.0f - c.pos[d];
                 g[d] = c.grid[d];
             }
         }
-        const float2 v = load_pair(table, grid_index(size, res, g[0], g[1], g[2]));
-        acc.x = fmaf(wgt, v.x, acc.x);
-        acc.y = fmaf(wgt, v.y, acc.y);
+        wgt[k] = w;
+        ent[k] = grid_index(size, res, g[0], g[1], g[2]);
+    }
+    if constexpr (GROUP) {
+        constexpr uint32_t kN = EntryGroup<Tp>::kN;
+        EntryGroup<Tp> grp[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) grp[j].load(table, ent[2 * j]);
+        float2 far[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            far[j] = make_float2(0.0f, 0.0f);
+            if ((ent[2 * j + 1] ^ ent[2 * j]) >= kN) far[j] = load_pair(table, ent[2 * j + 1]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float2 v0 = grp[j].get(ent[2 * j]);
+            const float2 v1 = ((ent[2 * j + 1] ^ ent[2 * j]) >= kN) ? far[j] : grp[j].get(ent[2 * j + 1]);
+            acc.x = fmaf(wgt[2 * j], v0.x, acc.x);
+            acc.y = fmaf(wgt[2 * j], v0.y, acc.y);
+            acc.x = fmaf(wgt[2 * j + 1], v1.x, acc.x);
+            acc.y = fmaf(wgt[2 * j + 1], v1.y, acc.y);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float2 v = load_pair(table, ent[k]);
+            acc.x = fmaf(wgt[k], v.x, acc.x);
+            acc.y = fmaf(wgt[k], v.y, acc.y);
+        }
     }
     store_pair(out, ROW_MAJOR ? i * (int64_t)gridDim.y + l : (int64_t)l * N + i, acc);
 }
@@ -249,6 +322,43 @@ int make_table(int L, const int64_t* off, const float* scale, const int32_t* res
     return 0;
 }
 
+template <typename Tp, typename To, bool ROW_MAJOR>
+void launch_lm(dim3 grid, hipStream_t st, int64_t N, const float* x, const void* params, LevelTable lt,
+               void* out, bool grp) {
+    if constexpr (std::is_same_v<Tp, __half>) {
+        if (grp) {
+            hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<Tp, To, ROW_MAJOR, true>), grid, dim3(256), 0, st, N,
+                               x, (const Tp*)params, lt, (To*)out);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<Tp, To, ROW_MAJOR, false>), grid, dim3(256), 0, st, N, x,
+                           (const Tp*)params, lt, (To*)out);
+}
+
+// Level-major forward launch; grouped corner loads for fp16 tables whose
+// base is 16-byte aligned (level offsets are multiples of 8 entries).  fp32
+// tables keep the 8-byte loads: a 16-byte group holds only 2 entries there
+// and measured slower (config-2 points: 102 -> 119 us level-major, 141 ->
+// 156 us row-major); fp16: 113-117 -> 103-106 us level-major, 138-140 ->
+// 116-118 us row-major (profiles/r02_hashgrid_group_ab.jsonl)
+template <bool ROW_MAJOR>
+int launch_fwd_lm(dim3 grid, hipStream_t st, int64_t N, const float* x, const void* params,
+                  int32_t param_dtype, const LevelTable& lt, void* out, int32_t out_dtype) {
+    const bool grp = group_loads() && ((uintptr_t)params & 15) == 0;
+    if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F32)
+        launch_lm<float, float, ROW_MAJOR>(grid, st, N, x, params, lt, out, grp);
+    else if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F16)
+        launch_lm<float, __half, ROW_MAJOR>(grid, st, N, x, params, lt, out, grp);
+    else if (param_dtype == AVR_DTYPE_F16 && out_dtype == AVR_DTYPE_F16)
+        launch_lm<__half, __half, ROW_MAJOR>(grid, st, N, x, params, lt, out, grp);
+    else if (param_dtype == AVR_DTYPE_F16 && out_dtype == AVR_DTYPE_F32)
+        launch_lm<__half, float, ROW_MAJOR>(grid, st, N, x, params, lt, out, grp);
+    else
+        return fail(AVR_E_ARG, "avr_hashgrid_fwd: unknown dtype");
+    return 0;
+}
+
 }  // namespace
 
 // level_offset / level_scale / level_res are HOST pointers (small metadata,
@@ -270,20 +380,7 @@ extern "C" int avr_hashgrid_fwd(int64_t N, int32_t n_levels, const float* x, con
     // time), same values and output layout (tools/probe_hashgrid.py)
     if (N >= lm_min_points()) {
         const dim3 glm((unsigned)((N + 255) / 256), (unsigned)L);
-        if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F32)
-            hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<float, float, true>), glm, dim3(256), 0, st, N, x,
-                               (const float*)params, lt, (float*)out);
-        else if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F16)
-            hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<float, __half, true>), glm, dim3(256), 0, st, N, x,
-                               (const float*)params, lt, (__half*)out);
-        else if (param_dtype == AVR_DTYPE_F16 && out_dtype == AVR_DTYPE_F16)
-            hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<__half, __half, true>), glm, dim3(256), 0, st, N, x,
-                               (const __half*)params, lt, (__half*)out);
-        else if (param_dtype == AVR_DTYPE_F16 && out_dtype == AVR_DTYPE_F32)
-            hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<__half, float, true>), glm, dim3(256), 0, st, N, x,
-                               (const __half*)params, lt, (float*)out);
-        else
-            return fail(AVR_E_ARG, "avr_hashgrid_fwd: unknown dtype");
+        if (int e = launch_fwd_lm<true>(glm, st, N, x, params, param_dtype, lt, out, out_dtype)) return e;
         return check_launch("avr_hashgrid_fwd");
     }
     if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F32)
@@ -336,20 +433,7 @@ extern "C" int avr_hashgrid_fwd_lm(int64_t N, int32_t n_levels, const float* x, 
     if (int e = make_table(n_levels, level_offset, level_scale, level_res, &lt)) return e;
     const dim3 grid((unsigned)((N + 255) / 256), (unsigned)n_levels);
     hipStream_t st = as_stream(stream);
-    if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F32)
-        hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<float, float>), grid, dim3(256), 0, st, N, x,
-                           (const float*)params, lt, (float*)out);
-    else if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F16)
-        hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<float, __half>), grid, dim3(256), 0, st, N, x,
-                           (const float*)params, lt, (__half*)out);
-    else if (param_dtype == AVR_DTYPE_F16 && out_dtype == AVR_DTYPE_F16)
-        hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<__half, __half>), grid, dim3(256), 0, st, N, x,
-                           (const __half*)params, lt, (__half*)out);
-    else if (param_dtype == AVR_DTYPE_F16 && out_dtype == AVR_DTYPE_F32)
-        hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<__half, float>), grid, dim3(256), 0, st, N, x,
-                           (const __half*)params, lt, (float*)out);
-    else
-        return fail(AVR_E_ARG, "avr_hashgrid_fwd_lm: unknown dtype");
+    if (int e = launch_fwd_lm<false>(grid, st, N, x, params, param_dtype, lt, out, out_dtype)) return e;
     return check_launch("avr_hashgrid_fwd_lm");
 }
 
