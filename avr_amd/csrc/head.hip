@@ -280,6 +280,70 @@ __device__ __forceinline__ void bitonic_sort(uint32_t* keys, int n) {
     }
 }
 
+// The same bitonic network with the keys in registers: thread t holds
+// positions t*KPT .. t*KPT+KPT-1 (n = 256*KPT).  Exchange distances below
+// KPT stay inside a thread, those below 64*KPT cross lanes of one wave
+// (ds_bpermute shuffles, no barrier); only the distances that cross waves
+// go through LDS.  At n = 1024 that is 3 barrier-separated LDS passes
+// instead of 55.  Same compare-exchanges, so the same sorted keys.
+template <int KPT>
+__device__ __forceinline__ void bitonic_sort_regs(uint32_t* keys) {
+    constexpr int n = kThreads * KPT;
+    constexpr int kWaveSpan = 64 * KPT;  // distances below this stay in a wave
+    const int t = threadIdx.x;
+    uint32_t v[KPT];
+#pragma unroll
+    for (int e = 0; e < KPT; ++e) v[e] = keys[t * KPT + e];
+#pragma unroll
+    for (int k = 2; k <= n; k <<= 1) {
+        if ((k >> 1) >= kWaveSpan) {  // cross-wave distances through LDS
+#pragma unroll
+            for (int e = 0; e < KPT; ++e) keys[t * KPT + e] = v[e];
+            lds_barrier();
+            for (int j = k >> 1; j >= kWaveSpan; j >>= 1) {
+                for (int i = t; i < (n >> 1); i += kThreads) {
+                    const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
+                    const int hi = lo + j;
+                    const uint32_t a = keys[lo], c = keys[hi];
+                    if ((a > c) == ((lo & k) == 0)) {
+                        keys[lo] = c;
+                        keys[hi] = a;
+                    }
+                }
+                lds_barrier();
+            }
+#pragma unroll
+            for (int e = 0; e < KPT; ++e) v[e] = keys[t * KPT + e];
+            lds_barrier();  // every read done before the next LDS write
+        }
+#pragma unroll
+        for (int j = ((k >> 1) < kWaveSpan ? (k >> 1) : kWaveSpan >> 1); j >= KPT; j >>= 1) {
+#pragma unroll
+            for (int e = 0; e < KPT; ++e) {
+                const int i = t * KPT + e;
+                const uint32_t p = (uint32_t)__shfl_xor((int)v[e], j / KPT, 64);
+                const bool keep_min = ((i & k) == 0) == ((i & j) == 0);
+                v[e] = keep_min ? min(v[e], p) : max(v[e], p);
+            }
+        }
+#pragma unroll
+        for (int j = ((k >> 1) < KPT ? (k >> 1) : KPT >> 1); j >= 1; j >>= 1) {
+#pragma unroll
+            for (int e = 0; e < KPT; ++e) {
+                if (e & j) continue;
+                const int i = t * KPT + e;  // lower of the pair (e, e ^ j)
+                const uint32_t a = v[e], c = v[e ^ j];
+                const bool asc = (i & k) == 0;
+                v[e] = asc ? min(a, c) : max(a, c);
+                v[e ^ j] = asc ? max(a, c) : min(a, c);
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < KPT; ++e) keys[t * KPT + e] = v[e];
+    lds_barrier();
+}
+
 // Rays of column (b, s) with a non-empty window (d < lim), sorted by
 // (delay, ray) -- a total order, so the sort is deterministic: keys
 // (d << 12 | r) in LDS through a bitonic sort; afterwards cnt[t] = number of
@@ -303,7 +367,14 @@ __device__ __forceinline__ int sort_rays(const Rays<RPT>& rays, int lim, int T, 
     }
     lds_barrier();
     block_inclusive_scan(cnt, T, wtot);
-    bitonic_sort(keys, nk);
+    if (nk == 1024)
+        bitonic_sort_regs<4>(keys);
+    else if (nk == 2048)
+        bitonic_sort_regs<8>(keys);
+    else if (nk == 4096)
+        bitonic_sort_regs<16>(keys);
+    else
+        bitonic_sort(keys, nk);
     return T > 0 ? cnt[T - 1] : 0;
 }
 
