@@ -883,10 +883,13 @@ int head_shape(const avr_render_params& p, int B, int R, int K, int es, HeadShap
     if (T > kThreads * 16) return fail(AVR_E_CONFIG, "fused head: T > 4096 not supported");
     if (R > kThreads * 16) return fail(AVR_E_CONFIG, "fused head: more than 4096 rays per shard");
     const int nt = T <= 1024 ? 4 : (T <= 2048 ? 8 : 16);
-    // feature block: prefetched W rows in registers (kb*nt <= 64), and the
-    // backward's Q[kb][T] in <= 80 KiB of LDS (two workgroups per CU)
+    // feature block: prefetched W rows in registers (kb*nt <= 64), the
+    // backward's Q[kb][T] in <= 80 KiB of LDS (two workgroups per CU), and
+    // the cumulative sums C[kb][R] within the 150 KiB budget (many rays)
     int kb = 16;
-    while (kb > 4 && ((size_t)kb * q_stride(T) * 4 > 80 * 1024 || kb * nt > 64)) kb /= 2;
+    while (kb > 4 && ((size_t)kb * q_stride(T) * 4 > 80 * 1024 || kb * nt > 64 ||
+                      cumsum_lds_bytes(R, kb) > 150 * 1024))
+        kb /= 2;
     const size_t lds_sort = 4 * ((size_t)T + (size_t)R + (size_t)pow2_ceil(R) + 4);
     if ((size_t)kb * q_stride(T) * 4 > 150 * 1024 || cumsum_lds_bytes(R, kb) > 150 * 1024 ||
         lds_sort > 150 * 1024)

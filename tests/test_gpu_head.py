@@ -36,6 +36,11 @@ CASES = [
     ("meshrir_k512", MESHRIR, 16, 8, 64, 1022, 512, 2),
     ("simu_long_k512", SIMU, 8, 4, 48, 4094, 512, 1),
     ("ragged_k512", dict(MESHRIR, xyz_min=0, xyz_max=10), 5, 3, 40, 510, 512, 3),
+    # ray counts for every form of the delay sort: 1154 rays (config 4's
+    # RAF-E sphere) sort 2048 keys, 2562 rays 4096 keys, 8 keys per thread /
+    # 16 keys per thread in registers (650 and 1024 rays above: 4)
+    ("raf_e_rays", RAF, 48, 24, 16, 510, 64, 1),
+    ("many_rays", MESHRIR, 64, 40, 8, 254, 64, 1),
 ]
 
 
