@@ -118,6 +118,7 @@ _SIGS = {
     "avr_dft_phase_fwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32, _vp, _vp, _vp, _vp, _c_i32, _vp, _vp]),
     "avr_spectrum_finalize": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _vp, _vp, _vp]),
     "avr_irfft": (ctypes.c_int, [_c_i32, _c_i32, _vp, _vp, _vp, _vp]),
+    "avr_irfft_bwd": (ctypes.c_int, [_c_i32, _c_i32, _vp, _vp, _vp, _vp]),
     "avr_dft_phase_bwd": (ctypes.c_int, [_vp, _c_i32] + [_vp] * 7),
     "avr_ray_reduce_bwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32] + [_vp] * 6),
     "avr_weights_bwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32, _vp, _vp, _vp, _vp]),
@@ -132,6 +133,7 @@ _SIGS = {
     "avr_head_splits": (ctypes.c_int, [_vp, _c_i32, _c_i32, _c_i32, _vp]),
     "avr_head_sort": (ctypes.c_int, [_vp, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "avr_head_pack_w": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp, _c_i32, _vp, _vp]),
+    "avr_head_fwd_exact": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp, _vp]),
     "avr_head_fwd": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _vp, _c_i32, _vp,
                                     _vp]),
     "avr_head_bwd_workspace": (ctypes.c_int, [_vp, _c_i32, _c_i32, _c_i32, _vp]),

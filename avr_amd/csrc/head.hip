@@ -367,6 +367,9 @@ __device__ __forceinline__ int sort_rays(const Rays<RPT>& rays, int lim, int T, 
     }
     lds_barrier();
     block_inclusive_scan(cnt, T, wtot);
+    // the scan does not end with a barrier; the sorts below only hide that
+    // for nk >= 2 (a one-ray shard runs no sort pass)
+    lds_barrier();
     if (nk == 1024)
         bitonic_sort_regs<4>(keys);
     else if (nk == 2048)

@@ -1,0 +1,275 @@
+// Fused signal head, output-rounding-exact form.
+//
+// The reference's signal network returns x = h W^T from a 16-bit network
+// (tcnn's fp16, model.py:21-31, 176-180): the render sees every element of x
+// ROUNDED to 16 bits (renderer_cpu.py:73,80,90 upcast it with .float()).  The
+// linear-algebra head of head.hip sums exact products and never forms x, so
+// it cannot reproduce that rounding.  This kernel forms x tile by tile on the
+// matrix cores, rounds each element to the MLP's 16-bit type exactly as the
+// unfused layer's output does (fp32 accumulation, one round to nearest even),
+// and reduces it over rays on the spot:
+//
+//   z[b,s,t] = sum_{p < cnt[b,s,t]} ws[b,s,p] * round16( sum_k h[b,perm_p,s,k] W[t,k] )
+//
+// with the column's live rays sorted by delay (avr_head_sort: perm, ws and
+// cnt[t] = number of rays with delay <= t), so the masked part of the
+// [rays x t] plane is a staircase: a 32-ray x 32-t tile whose first ray
+// starts after cnt at the tile's last t is skipped whole.  x never reaches
+// HBM; h is read once from HBM (the t-blocks of a column run on one XCD and
+// share its rows through that XCD's L2).
+//
+// Work: one workgroup per (column b*S+s, block of 32*WAVES t).  Wave w owns
+// the 32 t of tile w: its W rows are the MFMA B operand, held in registers
+// for the whole launch (K/16 fragments of 8 16-bit values).  The A operand,
+// 32 sorted rays x K features, is staged per ray tile in LDS (double
+// buffered, row stride K*2+16 bytes: ds_read_b128 of 32 rows conflict-free),
+// loaded whole-row by all waves one tile ahead.  v_mfma_f32_32x32x16_{f16,bf16}
+// over K, then the epilogue rounds, masks (p < cnt[t]), weights and sums the
+// tile's rows into a per-lane register in a fixed order (sorted position
+// order; the two lane halves added last), so results are deterministic.
+// Every (b, s, t) is written by exactly one lane: the output is ONE slab
+// [B][S][T] (n_split = 1 for avr_dft_phase_fwd), zero at t >= T-1-shift_s.
+#include "common.h"
+
+using namespace avr;
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t frag8 __attribute__((ext_vector_type(4)));  // 8 packed 16-bit values
+
+template <typename E>
+__device__ __forceinline__ f32x16 mfma16(frag8 a, frag8 b, f32x16 c) {
+    if constexpr (std::is_same<E, __half>::value)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b),
+                                                      c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                       c, 0, 0, 0);
+}
+
+// x rounded to the 16-bit type E (round to nearest even) and back: the value
+// the unfused layer's 16-bit output holds
+template <typename E>
+__device__ __forceinline__ float round16(float x) {
+    if constexpr (std::is_same<E, __half>::value)
+        return __half2float(__float2half(x));
+    else
+        return __bfloat162float(__float2bfloat16(x));
+}
+
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: global loads stay in flight
+    __builtin_amdgcn_s_barrier();
+}
+
+constexpr int kTileRays = 32;
+
+// LDS row stride of the A tile in bytes: K 16-bit values + 16 bytes, so 32
+// rows read at one column offset fall on distinct bank quads
+__host__ __device__ constexpr int a_row_bytes(int KS) { return KS * 32 + 16; }
+
+template <int KS, int WAVES>
+__host__ __device__ constexpr size_t exact_lds_bytes(int R) {
+    return 2 * (size_t)kTileRays * a_row_bytes(KS) + 8 * (size_t)((R + kTileRays - 1) / kTileRays * kTileRays);
+}
+
+template <typename E, int KS, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void head_exact_fwd_kernel(
+    avr_render_params pp, int B, int R, int K, const E* __restrict__ h, const E* __restrict__ W,
+    const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
+    float* __restrict__ z, int ntb, int per_xcd, int dbg) {
+    constexpr int NT = 64 * WAVES;
+    constexpr int TB = 32 * WAVES;  // t per workgroup
+    constexpr int ROWB = a_row_bytes(KS);
+    constexpr int CPT = (kTileRays * KS * 2 + NT - 1) / NT;  // 16-byte chunks per thread and tile
+    extern __shared__ __attribute__((aligned(16))) char lds_x[];
+    char* abuf = lds_x;                                                      // [2][32][ROWB]
+    int* pl = reinterpret_cast<int*>(lds_x + 2 * kTileRays * ROWB);          // perm of the column [R]
+    float* wl = reinterpret_cast<float*>(pl + R);                            // ws of the column [R]
+
+    const int T = pp.T, S = pp.n_samples;
+    // XCD-aware order: the t-blocks of one column are consecutive on one XCD
+    // (workgroup g runs on XCD g % 8), so they share the column's h rows in L2
+    const int64_t total = (int64_t)B * S * ntb;
+    const int64_t L = (int64_t)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (L >= total) return;
+    const int64_t col = L / ntb;
+    const int tb = (int)(L % ntb);
+    const int s = (int)(col % S), b = (int)(col / S);
+    const int lim = tail_limit(pp, s);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int half = lane >> 5, j = lane & 31;
+    const int t0 = tb * TB + wave * 32;
+    const int t = t0 + j;
+    float* zcol = z + col * T;
+    const int tlast = min(tb * TB + TB, lim) - 1;  // last live t of the block
+    if (tlast < tb * TB) {  // the block lies past the tail window
+        for (int i = threadIdx.x; i < TB; i += NT)
+            if (tb * TB + i < T) zcol[tb * TB + i] = 0.0f;
+        return;
+    }
+    const int* ccol = cnt + col * T;
+    const int nblk = ccol[tlast];  // rays live anywhere in the block (cnt is nondecreasing)
+    const int cnt_t = (t < lim) ? ccol[t] : 0;
+    const int cwave = (t0 < lim) ? ccol[min(t0 + 31, lim - 1)] : 0;  // rays live in this wave's tile
+
+    // B operand: W rows t0..t0+31, k = 16 ks + 8 half + 0..7 (registers for the launch)
+    frag8 wf[KS];
+    const int ks_n = K / 16;
+    {
+        const E* wrow = W + (int64_t)min(t, T - 1) * K + 8 * half;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            wf[ks] = ks < ks_n ? *reinterpret_cast<const frag8*>(wrow + 16 * ks) : frag8{0u, 0u, 0u, 0u};
+    }
+    // the column's sorted rays and weights for the block's tiles; positions
+    // past nblk repeat a live ray (its rows are masked) with weight 0
+    const int ntile = (nblk + kTileRays - 1) / kTileRays;
+    for (int p = threadIdx.x; p < ntile * kTileRays; p += NT) {
+        const bool in = p < nblk;
+        pl[p] = perm[col * R + (in ? p : nblk - 1)];
+        wl[p] = in ? ws[col * R + p] : 0.0f;
+    }
+    __syncthreads();
+    const int cpr = K / 8;  // 16-byte chunks per row
+    const int64_t hstride = (int64_t)S * K;
+    const E* hcol = h + ((int64_t)b * R * S + s) * K;
+
+    // A-tile staging: whole h rows, 16 bytes per lane, two tiles in flight
+    // (registers) ahead of the one the MFMAs read from LDS
+    auto issue = [&](frag8 (&ld)[CPT], int tile) {
+        const int p0 = tile * kTileRays;
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            const int ch = threadIdx.x + NT * c;
+            const int row = ch / cpr, cc = ch - row * cpr;
+            if (row < kTileRays && !(dbg & 2))
+                ld[c] = __builtin_nontemporal_load(
+                    reinterpret_cast<const frag8*>(hcol + (int64_t)pl[p0 + row] * hstride + 8 * cc));
+        }
+    };
+    auto commit = [&](const frag8 (&ld)[CPT], int buf) {
+        char* a = abuf + buf * kTileRays * ROWB;
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            const int ch = threadIdx.x + NT * c;
+            const int row = ch / cpr, cc = ch - row * cpr;
+            if (row < kTileRays) *reinterpret_cast<frag8*>(a + row * ROWB + 16 * cc) = ld[c];
+        }
+    };
+
+    float zl = 0.0f;
+    auto compute = [&](int it) {
+        const int p0 = it * kTileRays;
+        if (p0 >= cwave) return;  // wave-uniform: no live (ray, t) pair of this wave in the tile
+        const char* a = abuf + (it & 1) * kTileRays * ROWB + j * ROWB + 16 * half;
+        f32x16 acc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+        if (!(dbg & 1)) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                acc = mfma16<E>(*reinterpret_cast<const frag8*>(a + 32 * ks), wf[ks], acc);
+        }
+        // register r holds row (r & 3) + 8 (r >> 2) + 4 half of the tile, column t
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 wv = *reinterpret_cast<const float4*>(wl + p0 + 8 * g + 4 * half);
+            const float w4[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int p = p0 + e + 8 * g + 4 * half;
+                const float wsel = (p < cnt_t) ? w4[e] : 0.0f;
+                zl = fmaf(wsel, round16<E>(acc[4 * g + e]), zl);
+            }
+        }
+    };
+
+    frag8 ldA[CPT], ldB[CPT];
+    // one iteration: `nxt` holds tile it+1 (in flight), `nn` receives tile it+2
+    auto body = [&](int it, frag8 (&nxt)[CPT], frag8 (&nn)[CPT]) {
+        if (it + 2 < ntile) issue(nn, it + 2);
+        compute(it);
+        if (it + 1 < ntile) commit(nxt, (it + 1) & 1);  // waits for tile it+1's loads only
+        lds_barrier();  // LDS traffic done; the loads of tile it+2 stay in flight
+    };
+    if (ntile > 0) {
+        issue(ldA, 0);
+        if (K < 16 * KS) {  // the k-steps past K read zeros (the commits never write there)
+            for (int i = threadIdx.x; i < 2 * kTileRays * ROWB / 16; i += NT)
+                reinterpret_cast<frag8*>(abuf)[i] = frag8{0u, 0u, 0u, 0u};
+            __syncthreads();
+        }
+        if (ntile > 1) issue(ldB, 1);
+        commit(ldA, 0);
+        lds_barrier();
+    }
+    for (int it = 0; it < ntile; it += 2) {
+        body(it, ldB, ldA);
+        if (it + 1 < ntile) body(it + 1, ldA, ldB);
+    }
+    const float other = __shfl_xor(zl, 32, 64);
+    if (half == 0 && t < T) zcol[t] = (t < lim) ? zl + other : 0.0f;
+}
+
+int exact_shape(const avr_render_params& p, int K, int* KS, int* waves) {
+    if (K % 16 != 0 || K < 16 || K > 512) return fail(AVR_E_CONFIG, "exact head: K must be a multiple of 16, <= 512");
+    const int ks = K / 16;
+    *KS = ks <= 8 ? 8 : (ks <= 16 ? 16 : 32);
+    int w = 8;
+    if (const char* e = getenv("AVR_HEAD_EXACT_WAVES")) w = atoi(e) == 4 ? 4 : 8;  // experiments
+    *waves = w;
+    return 0;
+}
+
+template <typename Kern>
+void allow_lds(Kern k, size_t lds) {
+    if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+}
+
+}  // namespace
+
+extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t K, const void* h,
+                                  const void* W, int32_t dtype, const int32_t* perm, const float* ws,
+                                  const int32_t* cnt, float* z, void* stream) {
+    AVR_REQUIRE(p && B >= 1 && h && W && perm && ws && cnt && z, "avr_head_fwd_exact: bad args");
+    AVR_REQUIRE(dtype == AVR_DTYPE_F16 || dtype == AVR_DTYPE_BF16, "avr_head_fwd_exact: h/W must be fp16 or bf16");
+    AVR_REQUIRE(reinterpret_cast<uintptr_t>(h) % 16 == 0 && reinterpret_cast<uintptr_t>(W) % 16 == 0,
+                "avr_head_fwd_exact: h and W must be 16-byte aligned");
+    const int R = n_rays(*p), S = p->n_samples, T = p->T;
+    AVR_REQUIRE(R >= 1 && R <= 4096 && T >= 2 && S >= 1, "avr_head_fwd_exact: shape out of range");
+    int KS, waves;
+    if (int e = exact_shape(*p, K, &KS, &waves)) return e;
+    const int TB = 32 * waves;
+    const int ntb = (T + TB - 1) / TB;
+    const int64_t total = (int64_t)B * S * ntb;
+    const int per_xcd = (int)((total + 7) / 8);
+    const dim3 grid((unsigned)(8 * per_xcd));
+    const char* dbg_env = getenv("AVR_HEAD_EXACT_DBG");  // profiling only: 1 no MFMA, 2 no h loads
+    const int dbg = dbg_env ? atoi(dbg_env) : 0;
+    hipStream_t st = as_stream(stream);
+    auto go = [&](auto kern, auto ks_tag, auto w_tag, auto hp) {
+        constexpr int KSV = decltype(ks_tag)::value, WV = decltype(w_tag)::value;
+        const size_t lds = exact_lds_bytes<KSV, WV>(R);
+        allow_lds(kern, lds);
+        hipLaunchKernelGGL(kern, grid, dim3(64 * WV), lds, st, *p, (int)B, R, (int)K, hp, (decltype(hp))W,
+                           perm, ws, cnt, z, ntb, per_xcd, dbg);
+    };
+#define AVR_HX(TY, KSV, WV)                                                                          \
+    if (KS == KSV && waves == WV)                                                                    \
+        go(head_exact_fwd_kernel<TY, KSV, WV>, std::integral_constant<int, KSV>{},                   \
+           std::integral_constant<int, WV>{}, (const TY*)h);
+#define AVR_HX_ALL(TY) AVR_HX(TY, 8, 8) AVR_HX(TY, 16, 8) AVR_HX(TY, 32, 8) AVR_HX(TY, 8, 4) AVR_HX(TY, 16, 4) AVR_HX(TY, 32, 4)
+    if (dtype == AVR_DTYPE_F16) {
+        AVR_HX_ALL(__half)
+    } else {
+        AVR_HX_ALL(__hip_bfloat16)
+    }
+#undef AVR_HX_ALL
+#undef AVR_HX
+    return check_launch("avr_head_fwd_exact");
+}

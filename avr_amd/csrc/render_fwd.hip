@@ -702,6 +702,51 @@ __global__ __launch_bounds__(256) void irfft_kernel(int F, int B1, const float2*
     }
 }
 
+// Adjoint irfft (torch's c2r backward): for bin k with weight c_k (1 at DC
+// and Nyquist, 2 inside),
+//   grad[k] = c_k / n * ( sum_t g[t] cos(2 pi k t/n), -sum_t g[t] sin(2 pi k t/n) )
+// and a zero imaginary part at DC / Nyquist.  Block = 32 bins x 8 t-slices;
+// each thread walks t = slice + 8j with the twiddle index advanced
+// incrementally, the 8 slices combined in LDS in a fixed order.
+__global__ __launch_bounds__(256) void irfft_bwd_kernel(int F, const float* __restrict__ gir,
+                                                        const float2* __restrict__ twg,
+                                                        float2* __restrict__ grad) {
+    extern __shared__ float lds_irb[];
+    __shared__ float2 red[8][33];
+    const int n = 2 * (F - 1);
+    const int b = blockIdx.y;
+    float2* tw = reinterpret_cast<float2*>(lds_irb);  // [n]
+    float* g = lds_irb + 2 * n;                       // [n]
+    stage_table<256>(tw, twg, n);
+    for (int i = threadIdx.x; i < n; i += 256) g[i] = gir[(int64_t)b * n + i];
+    __syncthreads();
+    const int kl = threadIdx.x & 31, sl = threadIdx.x >> 5;
+    const int k = blockIdx.x * 32 + kl;
+    const int km = k < F ? k : 0;
+    int idx = (int)(((int64_t)km * sl) % n);
+    const int step = (int)(((int64_t)km * 8) % n);
+    float ac = 0.f, as = 0.f;
+    for (int t = sl; t < n; t += 8) {
+        const float2 c = tw[idx];
+        ac = fmaf(g[t], c.x, ac);
+        as = fmaf(g[t], c.y, as);
+        idx += step;
+        if (idx >= n) idx -= n;
+    }
+    red[sl][kl] = make_float2(ac, as);
+    __syncthreads();
+    if (sl == 0 && k < F) {
+        float2 r = red[0][kl];
+        for (int q = 1; q < 8; ++q) {
+            r.x += red[q][kl].x;
+            r.y += red[q][kl].y;
+        }
+        const bool edge = (k == 0) || (k == F - 1);
+        const float c = (edge ? 1.0f : 2.0f) / (float)n;
+        grad[(int64_t)b * F + k] = make_float2(c * r.x, edge ? 0.0f : -c * r.y);
+    }
+}
+
 int pick_blocks(int64_t n, int threads, int cap = 4096) {
     int64_t g = (n + threads - 1) / threads;
     if (g < 1) g = 1;
@@ -1078,6 +1123,20 @@ int launch_irfft(int B, int F, const float* spec, const float* spec2, const floa
 extern "C" int avr_irfft(int32_t B, int32_t F, const float* spec, const float* tw, float* ir,
                          void* stream) {
     return avr::launch_irfft(B, F, spec, nullptr, tw, ir, nullptr, stream);
+}
+
+extern "C" int avr_irfft_bwd(int32_t B, int32_t F, const float* grad_ir, const float* tw,
+                             float* grad_spec, void* stream) {
+    AVR_REQUIRE(B >= 1 && F >= 2 && grad_ir && tw && grad_spec, "avr_irfft_bwd: bad args");
+    const int n = 2 * (F - 1);
+    const size_t lds = (size_t)n * (sizeof(float2) + sizeof(float));
+    AVR_REQUIRE(lds <= 160 * 1024, "avr_irfft_bwd: n too large for LDS");
+    if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)irfft_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+    hipLaunchKernelGGL(irfft_bwd_kernel, dim3((F + 31) / 32, B), dim3(256), lds, as_stream(stream), (int)F,
+                       grad_ir, reinterpret_cast<const float2*>(tw), reinterpret_cast<float2*>(grad_spec));
+    return check_launch("avr_irfft_bwd");
 }
 
 // ---------------------------------------------------- one-call render core

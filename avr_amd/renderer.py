@@ -329,7 +329,7 @@ class FusedHeadCore(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, attn, h, w_master, dtype, p, tables, rays_o, position_tx, dirs, cache=False):
+    def forward(ctx, attn, h, w_master, dtype, p, tables, rays_o, position_tx, dirs, cache=False, exact=False):
         dev = h.device
         B, K = h.size(0), h.size(-1)
         S, T = p.n_samples, p.T
@@ -343,13 +343,21 @@ class FusedHeadCore(torch.autograd.Function):
         ws = torch.empty(B, S, R, dtype=torch.float32, device=dev)
         cnt = torch.empty(B, S, T, dtype=torch.int32, device=dev)
         _lib.call("avr_head_sort", pref, B, _ptr(w), _ptr(delay), _ptr(perm), _ptr(ws), _ptr(cnt), st)
-        ns = ctypes.c_int32(0)
-        _lib.call("avr_head_splits", pref, B, K, code, ctypes.byref(ns))
-        n_split = ns.value
-        part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
-        Wp = _packed_head_weight(w_master, W, cache, pref, (p.T, R, B, K, code), st)
-        _lib.call("avr_head_fwd", pref, B, K, _ptr(h), _ptr(Wp), code, _ptr(perm), _ptr(ws), _ptr(cnt),
-                  n_split, _ptr(part), st)
+        if exact:
+            # every signal element formed and rounded to the 16-bit type, as
+            # the unfused layer (the reference network) outputs it
+            n_split = 1
+            part = torch.empty(1, B, S, T, dtype=torch.float32, device=dev)
+            _lib.call("avr_head_fwd_exact", pref, B, K, _ptr(h), _ptr(W), code, _ptr(perm), _ptr(ws), _ptr(cnt),
+                      _ptr(part), st)
+        else:
+            ns = ctypes.c_int32(0)
+            _lib.call("avr_head_splits", pref, B, K, code, ctypes.byref(ns))
+            n_split = ns.value
+            part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
+            Wp = _packed_head_weight(w_master, W, cache, pref, (p.T, R, B, K, code), st)
+            _lib.call("avr_head_fwd", pref, B, K, _ptr(h), _ptr(Wp), code, _ptr(perm), _ptr(ws), _ptr(cnt),
+                      n_split, _ptr(part), st)
         out = _spectrum(p, tables, part, n_split, B, dev, st)
         ctx.p, ctx.tables = p, tables
         ctx.save_for_backward(attn, h, W, w, delay, perm, ws, cnt)
@@ -377,17 +385,19 @@ class FusedHeadCore(torch.autograd.Function):
                   _ptr(work), nbytes.value, st)
         grad_attn = _grad_attn(p, tables, attn, grad_w, st) if ctx.needs_input_grad[0] else None
         return (grad_attn, grad_h if ctx.needs_input_grad[1] else None,
-                grad_W if ctx.needs_input_grad[2] else None, None, None, None, None, None, None, None)
+                grad_W if ctx.needs_input_grad[2] else None, None, None, None, None, None, None, None, None)
 
 
 def _poison_nonfinite(out, tensors, ir_out=None):
     """out + NaN where any element of `tensors` is non-finite, else out + 0
     (the reference's NaN propagation through its masks; no host sync)."""
-    bad = torch.zeros((), dtype=torch.bool, device=out.device)
+    bad = None
     for t in tensors:
-        bad = bad | ~torch.isfinite(t).all()
-    poison = torch.where(bad, torch.tensor(float("nan"), device=out.device),
-                         torch.tensor(0.0, device=out.device))
+        b = ~torch.isfinite(t).all()
+        bad = b if bad is None else bad | b
+    # scalar operands: no host-to-device copy, so a HIP-graph capture of a
+    # render with this option stays valid
+    poison = torch.where(bad, float("nan"), 0.0)
     if ir_out is not None:
         ir_out.add_(poison)
     return out + poison
@@ -458,6 +468,14 @@ class AVRRender(nn.Module):
         # the output exactly like the reference (one extra read of the
         # network output, no host synchronisation).
         self.propagate_nonfinite = bool(kwargs.get("propagate_nonfinite", False))
+        # 16-bit networks through the fused head: form every signal element
+        # on the matrix cores and round it to the network's 16-bit type before
+        # the masked ray sum, as the reference's fp16 network output is
+        # rounded (renderer_cpu.py:73,80,90; csrc/head_exact.hip).
+        # exact_head=False keeps the linear-algebra head of csrc/head.hip,
+        # which sums the exact products (about 3e-4 relative off the
+        # reference's rounded render at fp16).
+        self.exact_head = bool(kwargs.get("exact_head", True))
         self._pcache = {}
         self._pcache_lock = threading.Lock()
         # jitter the sampling kernel reads at run time while a HIP graph is
@@ -653,8 +671,16 @@ class AVRRender(nn.Module):
         with _on(dev):
             tables = get_tables(p, dev)
             check_config(p, tables)
-            return FusedHeadCore.apply(attn, h, weight, dtype, p, tables, geom["rays_o"],
-                                       geom["position_tx"], geom["dirs"], not torch.is_grad_enabled())
+            exact = (self.exact_head and dtype in (torch.float16, torch.bfloat16) and K % 16 == 0
+                     and K <= 512)
+            out = FusedHeadCore.apply(attn, h, weight, dtype, p, tables, geom["rays_o"],
+                                      geom["position_tx"], geom["dirs"], not torch.is_grad_enabled(), exact)
+            if self.propagate_nonfinite:
+                # the head kernels skip rays with an empty window, so a
+                # non-finite h / attn of a masked ray never reaches `out`
+                # (the reference's signal = h W^T carries it through its masks)
+                out = _poison_nonfinite(out, (attn, h, weight))
+            return out
 
     def forward(self, rays_o, position_tx, direction_tx=None, ch_idx=None):
         """Render [B, F, 2] (real, imag) spectra; see renderer.py:31-124."""
@@ -662,10 +688,14 @@ class AVRRender(nn.Module):
 
     def render_ir(self, rays_o, position_tx, direction_tx=None, ch_idx=None):
         """(spectrum [B, F, 2], IR [B, 2(F-1)]): forward plus
-        `torch.real(torch.fft.irfft(...))` (utils/criterion.py:71), the IR
-        computed in the same native call (forward only, like spectrum_to_ir)."""
+        `torch.real(torch.fft.irfft(...))` (utils/criterion.py:71).  Without
+        autograd the IR is computed in the same native call; with autograd
+        recording it is spectrum_to_ir(out), which differentiates."""
         ir = []
-        out = self._render(rays_o, position_tx, direction_tx, ch_idx, ir)
+        # the IR inside the render's native call is a forward-only side
+        # output; with autograd recording, take it differentiably instead
+        grad = torch.is_grad_enabled()
+        out = self._render(rays_o, position_tx, direction_tx, ch_idx, None if grad else ir)
         return out, (ir[0] if ir else spectrum_to_ir(out))
 
     def _render(self, rays_o, position_tx, direction_tx, ch_idx, ir_slot):
@@ -699,23 +729,46 @@ class AVRRender(nn.Module):
 # --------------------------------------------------------------------------
 # a13: IR synthesis (utils/criterion.py:71 applied to the rendered spectrum)
 # --------------------------------------------------------------------------
+class _IRFFT(torch.autograd.Function):
+    """HIP irfft (avr_irfft) with its adjoint (avr_irfft_bwd) as backward."""
+
+    @staticmethod
+    def forward(ctx, out):
+        dev = out.device
+        B, F = out.size(0), out.size(1)
+        n = 2 * (F - 1)
+        tw = _ir_twiddle(n, dev)
+        ir = torch.empty(B, n, dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            _lib.call("avr_irfft", B, F, _ptr(out), _ptr(tw), _ptr(ir), _stream(dev))
+        return ir
+
+    @staticmethod
+    def backward(ctx, g):
+        dev = g.device
+        g = g.float().contiguous()
+        B, n = g.size(0), g.size(1)
+        F = n // 2 + 1
+        grad = torch.empty(B, F, 2, dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            _lib.call("avr_irfft_bwd", B, F, _ptr(g), _ptr(_ir_twiddle(n, dev)), _ptr(grad), _stream(dev))
+        return grad
+
+
 def spectrum_to_ir(out):
     """[B, F, 2] spectrum -> [B, 2(F-1)] IR with the HIP irfft kernel.
 
     Same result as `torch.real(torch.fft.irfft(out[...,0] + 1j*out[...,1]))`
-    (avr_runner.py:178 + utils/criterion.py:71).  Forward only.
+    (avr_runner.py:178 + utils/criterion.py:71), and differentiable like it:
+    the backward is the adjoint irfft kernel (torch's c2r backward: interior
+    bins doubled, no imaginary gradient at DC / Nyquist), so a loss taken on
+    the IR (utils/criterion.py:71-98) reaches the render.
     """
     if not out.is_cuda:
         raise RuntimeError("spectrum_to_ir needs a HIP tensor (no CPU fallback)")
-    dev = out.device
-    out = out.detach().float().contiguous()
-    B, F = out.size(0), out.size(1)
-    n = 2 * (F - 1)
-    tw = _ir_twiddle(n, dev)
-    ir = torch.empty(B, n, dtype=torch.float32, device=dev)
-    with torch.cuda.device(dev):
-        _lib.call("avr_irfft", B, F, _ptr(out), _ptr(tw), _ptr(ir), _stream(dev))
-    return ir
+    if out.dtype != torch.float32:
+        out = out.float()
+    return _IRFFT.apply(out.contiguous())
 
 
 _IRTW: dict = {}

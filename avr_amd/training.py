@@ -183,14 +183,19 @@ class TrainStep:
     def save_checkpoint(self, path, reference_layout=False):
         """The reference's `.tar` layout (avr_runner.py:148-153).  With
         `reference_layout` the networks are written as tcnn's flat `params`
-        (avr_amd.tcnn_compat), the form the reference's modules load."""
-        from .tcnn_compat import to_reference
+        (avr_amd.tcnn_compat) and the Adam state is converted to the same
+        parameters (one flat exp_avg / exp_avg_sq per tcnn module, in the
+        reference's module order), the form the reference's runner loads:
+        `load_state_dict` of the weights, then `optimizer.load_state_dict`
+        (avr_runner.py:116-124)."""
+        from .tcnn_compat import optimizer_state_to_reference, to_reference
 
         model = self.renderer.module if hasattr(self.renderer, "module") else self.renderer
+        opt = self.optimizer.state_dict()
         torch.save({
             'current_iteration': self.current_iteration,
             'audionerf_network_state_dict': to_reference(model) if reference_layout else model.state_dict(),
-            'optimizer_state_dict': self.optimizer.state_dict(),
+            'optimizer_state_dict': optimizer_state_to_reference(model, opt) if reference_layout else opt,
             'scheduler_state_dict': self.scheduler.state_dict(),
         }, path)
         return path
@@ -200,31 +205,30 @@ class TrainStep:
 
         A checkpoint written by the reference (tcnn networks: one flat
         `params` per network) is recognised and converted
-        (avr_amd.tcnn_compat.from_reference).  Its Adam state is laid out
-        over the reference's flat parameters, so it is restored only when
-        every state tensor matches this model's parameter shapes; otherwise
-        the optimiser starts fresh (a warning says so)."""
+        (avr_amd.tcnn_compat.from_reference), its Adam state too
+        (optimizer_state_from_reference).  When that state does not fit this
+        model's parameters (another parameter count or size), the optimiser
+        starts fresh and a warning says so."""
         import warnings
 
-        from .tcnn_compat import from_reference, is_reference_layout
+        from .tcnn_compat import from_reference, is_reference_layout, optimizer_state_from_reference
 
         ckpt = torch.load(path, map_location="cpu", weights_only=True)
         model = self.renderer.module if hasattr(self.renderer, "module") else self.renderer
         sd = ckpt['audionerf_network_state_dict']
+        opt_sd = ckpt['optimizer_state_dict']
         if is_reference_layout(model, sd):
             from_reference(model, sd)
-            shapes = [p.shape for g in self.optimizer.param_groups for p in g['params']]
-            st = ckpt['optimizer_state_dict'].get('state', {})
-            if any(int(i) >= len(shapes) or v.get('exp_avg', torch.empty(shapes[int(i)])).shape != shapes[int(i)]
-                   for i, v in st.items()):
-                warnings.warn("reference checkpoint: Adam state is over tcnn's flat parameters; "
-                              "optimizer state not restored", RuntimeWarning)
-                self.scheduler.load_state_dict(ckpt['scheduler_state_dict'])
-                self.current_iteration = int(ckpt['current_iteration'])
-                return ckpt
+            try:
+                opt_sd = optimizer_state_from_reference(model, opt_sd,
+                                                        self.optimizer.state_dict()["param_groups"])
+            except ValueError as e:
+                warnings.warn(f"reference checkpoint: {e}; optimizer state not restored", RuntimeWarning)
+                opt_sd = None
         else:
             model.load_state_dict(sd)
-        self.optimizer.load_state_dict(ckpt['optimizer_state_dict'])
+        if opt_sd is not None:
+            self.optimizer.load_state_dict(opt_sd)
         self.scheduler.load_state_dict(ckpt['scheduler_state_dict'])
         self.current_iteration = int(ckpt['current_iteration'])
         return ckpt

@@ -130,6 +130,10 @@ def parse_args(argv=None):
                          "on MI355X 2, 3 and 4 streams measure the same within 1%%)")
     ap.add_argument("--mlp-dtype", default="bf16", choices=["bf16", "fp16", "fp32"],
                     help="ddp-train mode: MLP compute dtype")
+    ap.add_argument("--oversubscribe", action="store_true",
+                    help="rehearsal of the N-rank path on ONE GPU: every rank on cuda:0, "
+                         "process group over gloo (RCCL needs one GPU per rank); the numbers "
+                         "are not a scaling measurement")
     args = ap.parse_args(argv)
     if args.workload is None:
         args.workload = MODES[args.mode]
@@ -168,6 +172,8 @@ def resolve_world(args, env=None, device_count=None):
         raise SystemExit("bench.py: --gpus must be >= 1")
     if n == 1:
         return "run", 1
+    if args.oversubscribe:
+        return "launch", n
     # counting devices does not initialise the GPU on this image
     have = torch.cuda.device_count() if device_count is None else device_count
     if have < n:
@@ -264,40 +270,73 @@ def roofline(w, timer, dt):
     }
 
 
-def cpu_baseline(w, budget_s=15.0):
+def cpu_baseline(w, budget_s=15.0, mode="pose"):
     """Time the CPU oracle (op-for-op torch-CPU restatement of renderer_cpu.py)
-    on this host's cores for a bounded sample of the same workload."""
+    on this host's cores for a bounded sample of the mode's workload:
+
+    * pose: full poses of the workload, forward + irfft;
+    * ray-shard: ONE rank's share of the pose (config 5 on the
+      CPU as a 1/8 ray shard): a sphere with about R/8 rays, all samples,
+      the full T, forward + irfft (the whole pose does not fit host RAM);
+    * ddp-train: the render core's forward + backward (reference autograd)
+      at the per-rank shape (the CPU has no hash-grid/MLP network to time).
+    `value` is ray-samples per second in every mode."""
     from oracle import avr_oracle as orc
 
     threads = torch.get_num_threads()
     g = torch.Generator().manual_seed(1)
-    B, RS, T = w.batch, w.n_rays * w.n_samples, w.T
+    sample = w
+    if mode == "ray-shard":
+        n_ele = w.render["n_ele"]
+        n_azi = max(1, round((w.n_rays / 8 - 2) / n_ele))
+        sample = w.replace(n_azi=n_azi)
+    B, RS, T = sample.batch, sample.n_rays * sample.n_samples, sample.T
     attn = torch.rand(B, RS, 1, generator=g) * 2
     sig = torch.randn(B, RS, T, generator=g) * 0.1
-    if w.signal_dtype == "float16":
+    if sample.signal_dtype == "float16":
         sig = sig.half()
     rays_o = torch.rand(B, 3, generator=g) * 4 - 2
     tx = torch.rand(B, 3, generator=g) * 4 - 2
-    dtx = torch.nn.functional.normalize(torch.randn(B, 3, generator=g), dim=-1) if w.with_dir_tx else None
-    cfg = orc.RenderConfig.from_kwargs(**w.render)
+    dtx = torch.nn.functional.normalize(torch.randn(B, 3, generator=g), dim=-1) if sample.with_dir_tx else None
+    cfg = orc.RenderConfig.from_kwargs(**sample.render)
+    train = mode == "ddp-train"
+    if train:
+        attn.requires_grad_(True)
+        sig.requires_grad_(True)
+        probe = torch.randn(B, sample.F, 2, generator=g)
     net = orc.StubNetwork(attn, sig)
     times = []
     t_start = time.time()
+    warm = True  # the first pass (allocator, thread pool, FFT plans) is not timed
     while True:
         t0 = time.time()
-        out = orc.render_spectrum(cfg, net, rays_o, tx, dtx)
-        orc.spectrum_to_ir(out)
-        times.append(time.time() - t0)
-        if time.time() - t_start > budget_s or len(times) >= 20:
+        if train:
+            out = orc.render_spectrum(cfg, net, rays_o, tx, dtx)
+            (out * probe).sum().backward()
+            attn.grad = sig.grad = None
+        else:
+            with torch.no_grad():
+                out = orc.render_spectrum(cfg, net, rays_o, tx, dtx)
+                orc.spectrum_to_ir(out)
+        if not warm:
+            times.append(time.time() - t0)
+        warm = False
+        del out
+        if times and (time.time() - t_start > budget_s or len(times) >= 20):
             break
     best = min(times)
+    what = {"pose": "full poses of {n} (forward + irfft)",
+            "ray-shard": "1/8 ray shards of {n}: {r} rays ({a}x{e}+2) x {s} samples x T={t} (forward + irfft)",
+            "ddp-train": "render-core forward + backward (reference autograd) of {n}, {b} poses"}[mode]
+    what = what.format(n=w.name, r=sample.n_rays, a=sample.render["n_azi"], e=sample.render["n_ele"],
+                       s=sample.n_samples, t=T, b=B)
     return {
-        "value": w.ray_samples / best,
+        "value": sample.ray_samples / best,
         "unit": "ray-samples/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{len(times)} full poses of {w.name} (forward + irfft), best of {len(times)}; "
-                  f"median {sorted(times)[len(times) // 2] * 1e3:.1f} ms/pose",
+        "sample": f"{len(times)} x {what}; best of {len(times)}, "
+                  f"median {sorted(times)[len(times) // 2] * 1e3:.1f} ms",
         "ms_per_pose": best * 1e3,
     }
 
@@ -462,8 +501,28 @@ def bench_pose(args, w, world, rank, dev):
     torch.cuda.synchronize()
     timer.enabled = False
 
-    # throughput (the reported value): K independent single-pose renders
-    elapsed, t_issue = timed(lambda: run(args.steps, n_streams), world, dev)
+    # throughput (the reported value): K independent single-pose renders,
+    # each replayed from its stream's HIP graph (the same kernels and
+    # results as the eager render, tests/test_gpu_graph.py) with the pose
+    # handed over from the host: per pose the host only draws the jitter,
+    # stages the pose and launches the graph, so it never gates the GPU --
+    # not even in the first steps of a short timed region, where eager
+    # issue (~75 us of Python per pose) used to leave the GPU idle
+    graphs = [graphed] + [GraphedRender(rr) for rr in renderers[1:]]
+
+    def run_graph(n, ns):
+        for i in range(n):
+            k = i % ns
+            with torch.cuda.stream(streams[k]):
+                j = pose[0] % P
+                pose[0] += 1
+                with torch.no_grad():
+                    graphs[k].render_ir(ro_h[j], tx_h[j], dtx_h[j])
+
+    run_graph(max(args.warmup, (graphed.ring + 2) * n_streams), n_streams)  # captures + warm replays
+    torch.cuda.synchronize()
+    elapsed_eager, _ = timed(lambda: run(args.steps, n_streams), world, dev)
+    elapsed, t_issue = timed(lambda: run_graph(args.steps, n_streams), world, dev)
     value = whole_job_rate(w.ray_samples, world, args.steps, elapsed)
     res = _base_result(args, w, world, value, elapsed, "f32" if dt == torch.float32 else "f16-storage/f32-math")
     res.update({
@@ -471,12 +530,14 @@ def bench_pose(args, w, world, rank, dev):
         "ir_render_path": "HIP-graph replay (avr_amd.graph.GraphedRender), host poses, synchronized per pose",
         "ir_render_ms_per_pose_eager": latency_eager_ms / B,
         "host_issue_ms_per_step": t_issue * 1e3 / args.steps,
+        "throughput_path": "HIP-graph replay per pose (avr_amd.graph.GraphedRender), host poses",
+        "ms_per_step_eager": elapsed_eager * 1e3 / args.steps,
         "streams": n_streams,
         "config": {"workload": w.name, "mode": "pose", "rays": R, "samples": S, "T": T, "freq_bins": w.F,
                    "poses_per_step": B, "distinct_poses": P,
                    "parallelism": f"poses x{world} (no data-path collective)",
                    "pipelining": f"{n_streams} HIP streams, consecutive poses round-robin, "
-                                 "one signal buffer per stream"},
+                                 "one signal buffer and one graph ring per stream"},
         "roofline": roofline(w, timer, dt),
     })
     return res
@@ -603,12 +664,15 @@ def main(argv=None):
     world = n
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", local if world > 1 and not args.oversubscribe else 0)
     torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if args.oversubscribe:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
         world = dist.get_world_size()
 
     from avr_amd.workloads import WORKLOADS
@@ -616,8 +680,10 @@ def main(argv=None):
     w = WORKLOADS[args.workload]
     fn = {"pose": bench_pose, "ray-shard": bench_ray_shard, "ddp-train": bench_ddp_train}[args.mode]
     result = fn(args, w, world, rank, dev)
-    if rank == 0 and world == 1 and args.mode == "pose" and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(w, args.cpu_budget)
+    if args.oversubscribe:
+        result["oversubscribed"] = f"{world} ranks on cuda:0 over gloo (launcher rehearsal, not a scaling number)"
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(w, args.cpu_budget, args.mode)
     if rank == 0 and world == 1 and args.mode == "pose" and w.name.startswith("c2_meshrir") \
             and not args.no_network:
         result["network_inference"] = network_inference(w, dev)

@@ -184,6 +184,12 @@ int avr_spectrum_finalize(int32_t B, int32_t P, int32_t F, const float* spart, f
  * spec[B][F][2] -> ir[B][n], n = 2*(F-1), tw = avr_ir_twiddle(n). */
 int avr_irfft(int32_t B, int32_t F, const float* spec, const float* tw, float* ir,
               void* stream);
+/* Adjoint of avr_irfft (torch's irfft backward: 1/n, the interior bins
+ * doubled, zero imaginary gradient at DC and Nyquist):
+ * grad_ir[B][n] -> grad_spec[B][F][2].  Differentiates the IR the loss is
+ * taken on (utils/criterion.py:71-72). */
+int avr_irfft_bwd(int32_t B, int32_t F, const float* grad_ir, const float* tw, float* grad_spec,
+                  void* stream);
 
 /* ---- a7-a13 in one host call -------------------------------------------
  * The pose-independent tables of avr_tables / avr_ir_twiddle. */
@@ -387,6 +393,16 @@ int avr_head_pack_w(const avr_render_params* p, int32_t B, int32_t K, const void
 int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* W,
                  int32_t dtype, const int32_t* perm, const float* ws, const int32_t* cnt,
                  int32_t n_split, float* zpart, void* stream);
+/* Output-rounding-exact forward for 16-bit networks (fp16 / bf16 h and W,
+ * W the plain [T][K] weight, K a multiple of 16, <= 512): every element of
+ * x = h W^T is formed on the matrix cores and rounded to the 16-bit type, as
+ * the unfused layer's (the reference network's) output is, before the masked
+ * weighted ray sum.  z [B][S][T] is ONE slab (n_split = 1 for
+ * avr_dft_phase_fwd), zero for t >= T-1-shift_s.  perm / ws / cnt from
+ * avr_head_sort; <= 4096 rays per shard. */
+int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* W,
+                       int32_t dtype, const int32_t* perm, const float* ws, const int32_t* cnt, float* z,
+                       void* stream);
 /* Backward: gz [B][S][T] (avr_dft_phase_bwd) -> grad_h [B][R][S][K] (dtype),
  * grad_w [B][R][S] fp32 (to avr_weights_bwd) and grad_W [T][K] fp32.
  * `workspace` holds avr_head_bwd_workspace() bytes of fp32 partials. */

@@ -98,3 +98,24 @@ def test_timed_reports_max_over_ranks_gloo():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert out[0] == out[1] >= 0.3
+
+
+def test_resolve_world_oversubscribe():
+    """--oversubscribe launches the ranks even with fewer GPUs than ranks
+    (they all use cuda:0 over gloo: the launcher rehearsal of the GPU test)."""
+    args = bench.parse_args(["--gpus", "2", "--oversubscribe"])
+    assert bench.resolve_world(args, env={}, device_count=1) == ("launch", 2)
+    assert bench.resolve_world(args, env={"WORLD_SIZE": "2"}) == ("run", 2)
+
+
+def test_cpu_baseline_modes_on_a_small_workload():
+    """Every mode's CPU leg runs the oracle on its own sample and reports
+    ray-samples/s (the ray-shard leg on a sphere of about R/8 rays)."""
+    from avr_amd.workloads import WORKLOADS
+
+    w = WORKLOADS["c1_meshrir_plumbing"]
+    for mode in ("pose", "ray-shard", "ddp-train"):
+        d = bench.cpu_baseline(w, 0.05, mode)
+        assert d["value"] > 0 and d["unit"] == "ray-samples/s" and d["kind"] == "port"
+    shard = bench.cpu_baseline(WORKLOADS["c1_meshrir_plumbing"].replace(n_azi=48, n_ele=5), 0.05, "ray-shard")
+    assert "32 rays (6x5+2)" in shard["sample"]

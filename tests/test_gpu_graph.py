@@ -127,3 +127,34 @@ def test_graph_replay_sees_optimizer_step_avrmodel(mlp_dtype):
     assert (e1 - e0).abs().max() > 1e-4 * e0.abs().max()  # the step changed the render
     torch.testing.assert_close(g1, e1, rtol=1e-5, atol=1e-6)
     assert len(gr._graphs) == 1
+
+
+def test_graph_replay_propagate_nonfinite():
+    """A render with propagate_nonfinite=True captures and replays (the
+    poison term uses scalar operands, no host-to-device copy): clean inputs
+    replay the eager spectrum bit for bit, a NaN in a masked chunk poisons
+    the replayed spectrum as it does the eager one."""
+    w = WORKLOADS["c1_meshrir_plumbing"]
+    B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
+    g = torch.Generator(device=DEV).manual_seed(2)
+    attn = torch.rand(B, R * S, 1, device=DEV, generator=g) * 2
+    sig = torch.randn(B, R * S, T, device=DEV, generator=g) * 0.1
+    r = AVRRender(Stub(attn, sig), propagate_nonfinite=True, **w.render)
+    gr = GraphedRender(r)
+    ro = torch.rand(B, 3, device=DEV, generator=g) * 4 - 2
+    tx = torch.rand(B, 3, device=DEV, generator=g) * 4 - 2
+    with torch.no_grad():
+        for k in range(4):
+            torch.manual_seed(20 + k)
+            out_e, ir_e = r.render_ir(ro, tx)
+            torch.manual_seed(20 + k)
+            out_g, ir_g = gr.render_ir(ro, tx)
+            torch.cuda.synchronize()
+            assert torch.isfinite(out_e).all()
+            assert torch.equal(out_g, out_e), k
+            assert torch.equal(ir_g, ir_e), k
+        sig[0, 0, 0] = float("nan")  # replays read the stub's tensor by pointer
+        torch.manual_seed(30)
+        out_g, ir_g = gr.render_ir(ro, tx)
+        torch.cuda.synchronize()
+        assert torch.isnan(out_g).all() and torch.isnan(ir_g).all()

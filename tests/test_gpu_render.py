@@ -392,3 +392,48 @@ def test_nonfinite_semantics():
     strict = _nan_render(inp, w, case.seed, masked, propagate_nonfinite=True)
     assert torch.isnan(strict).all()
     assert torch.equal(_nan_render(inp, w, case.seed, None, propagate_nonfinite=True), clean)
+
+
+@pytest.mark.parametrize("F", [2, 3, 128, 512, 801, 2048])
+def test_spectrum_to_ir_gradient_matches_torch_irfft(F):
+    """spectrum_to_ir's backward (avr_irfft_bwd) equals torch.fft.irfft's
+    autograd (utils/criterion.py:71-72: the loss is taken on the IR), DC and
+    Nyquist imaginary parts included (their gradient is zero)."""
+    from avr_amd import spectrum_to_ir
+
+    g = torch.Generator(device=DEV).manual_seed(F)
+    B = 3
+    spec = torch.randn(B, F, 2, device=DEV, generator=g)
+    probe = torch.randn(B, 2 * (F - 1), device=DEV, generator=g)
+    a = spec.clone().requires_grad_(True)
+    ir = spectrum_to_ir(a)
+    (ir * probe).sum().backward()
+    b = spec.double().clone().requires_grad_(True)
+    ir_ref = torch.real(torch.fft.irfft(b[..., 0] + 1j * b[..., 1], dim=-1))
+    (ir_ref * probe.double()).sum().backward()
+    assert ir.shape == ir_ref.shape
+    assert rel_l2(ir.detach().double().cpu(), ir_ref.detach().cpu()) < 1e-5
+    assert rel_l2(a.grad.double().cpu(), b.grad.cpu()) < 1e-5, rel_l2(a.grad.double().cpu(), b.grad.cpu())
+    assert torch.all(a.grad[:, 0, 1] == 0) and torch.all(a.grad[:, -1, 1] == 0)
+
+
+def test_render_ir_differentiable():
+    """render_ir with autograd recording returns an IR that carries the
+    gradient to the network outputs (the same as differentiating the
+    spectrum through torch's irfft)."""
+    case = Case("c1_s1")
+    w, inp = case.workload, case.inputs()
+    attn = torch.from_numpy(inp["attn"]).to(DEV).requires_grad_(True)
+    sig = torch.from_numpy(inp["signal"]).to(DEV).requires_grad_(True)
+    r = AVRRender(Net(attn, sig), **w.render)
+    torch.manual_seed(case.seed)
+    out, ir = r.render_ir(torch.from_numpy(inp["rays_o"]).to(DEV), torch.from_numpy(inp["position_tx"]).to(DEV))
+    probe = torch.linspace(-1, 1, ir.numel(), device=DEV).view_as(ir)
+    (ir * probe).sum().backward()
+    gs, ga = sig.grad.clone(), attn.grad.clone()
+    sig.grad = attn.grad = None
+    torch.manual_seed(case.seed)
+    out2 = r(torch.from_numpy(inp["rays_o"]).to(DEV), torch.from_numpy(inp["position_tx"]).to(DEV))
+    ir2 = torch.fft.irfft(out2[..., 0] + 1j * out2[..., 1], dim=-1)
+    (ir2 * probe).sum().backward()
+    assert rel_l2(gs.cpu(), sig.grad.cpu()) < 1e-4 and rel_l2(ga.cpu(), attn.grad.cpu()) < 1e-4

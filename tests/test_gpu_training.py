@@ -117,8 +117,9 @@ def test_checkpoint_reference_layout(tmp_path):
     """A checkpoint whose networks are tcnn flat `params` (the reference's
     modules, avr_amd.tcnn_compat) restores the same weights: written by
     save_checkpoint(reference_layout=True) it resumes exactly; with the
-    reference's flat-parameter Adam state the weights load and the
-    optimiser restarts with a warning."""
+    reference's flat-parameter Adam state the weights and the state load
+    (converted per layer); a state over another parameter count restarts
+    the optimiser with a warning."""
     r, ori, rx, tx, dtx = _setup()
     step = TrainStep(r, RAF_TRAIN, dict(fs=16000, speed=346.8))
     for _ in range(2):
@@ -137,22 +138,35 @@ def test_checkpoint_reference_layout(tmp_path):
     total2, _ = step2(ori, rx, tx, dtx)
     assert abs(float(total2) - float(ref_total)) <= 1e-6 * abs(float(ref_total))
 
-    # the reference's own optimiser state: one moment tensor per flat params
+    # the reference's own optimiser state: one moment tensor per flat params,
+    # in the reference's module order (the order of the `.params` keys)
     ck = torch.load(path, weights_only=True)
     flat = [v for k, v in ck["audionerf_network_state_dict"].items() if k.endswith(".params")]
     ck["optimizer_state_dict"]["state"] = {
-        i: {"step": torch.tensor(2.0), "exp_avg": torch.zeros_like(v), "exp_avg_sq": torch.zeros_like(v)}
+        i: {"step": torch.tensor(2.0), "exp_avg": torch.full_like(v, 1e-3), "exp_avg_sq": torch.zeros_like(v)}
         for i, v in enumerate(flat)}
     ck["optimizer_state_dict"]["param_groups"][0]["params"] = list(range(len(flat)))
     torch.save(ck, str(tmp_path / "ref_opt.tar"))
     r3, _, _, _, _ = _setup(seed=321)
     step3 = TrainStep(r3, RAF_TRAIN, dict(fs=16000, speed=346.8))
-    with pytest.warns(RuntimeWarning, match="optimizer state not restored"):
-        step3.load_checkpoint(str(tmp_path / "ref_opt.tar"))
+    step3.load_checkpoint(str(tmp_path / "ref_opt.tar"))  # converted, no warning
     from avr_amd.tcnn_compat import to_reference
     got = to_reference(r3)
     for k, v in ck["audionerf_network_state_dict"].items():
         assert torch.equal(got[k].cpu(), v.cpu()), k
+    for p in r3.parameters():
+        st = step3.optimizer.state[p]
+        assert float(st["step"]) == 2.0 and st["exp_avg"].shape == p.shape
+        assert torch.all(st["exp_avg"] == 1e-3)
+    # a state over another parameter count: weights load, the optimiser restarts
+    ck["optimizer_state_dict"]["param_groups"][0]["params"] = list(range(len(flat) - 1))
+    ck["optimizer_state_dict"]["state"].pop(len(flat) - 1)
+    torch.save(ck, str(tmp_path / "ref_opt_bad.tar"))
+    r4, _, _, _, _ = _setup(seed=322)
+    step4 = TrainStep(r4, RAF_TRAIN, dict(fs=16000, speed=346.8))
+    with pytest.warns(RuntimeWarning, match="optimizer state not restored"):
+        step4.load_checkpoint(str(tmp_path / "ref_opt_bad.tar"))
+    assert not step4.optimizer.state
 
 
 @pytest.mark.gpu
