@@ -12,7 +12,8 @@
 // covers 64/L points x all levels: the 8-byte feature pairs are written
 // fully coalesced, the coordinates are shared through L1, and the gathers of
 // one point's levels go to L2/MALL-resident tables (<= 2 MiB fp32 per level).
-// Interpolation math is fp32 regardless of the parameter dtype.
+// Weights and coordinates are fp32; the corner sum runs in the table type
+// (fp16 tables: half FMAs, as tcnn's fp16 GridEncoding; CornerAcc).
 #include "common.h"
 
 using namespace avr;
@@ -53,6 +54,50 @@ template <>
 __device__ __forceinline__ float2 load_pair<__half>(const __half* params, int64_t entry) {
     return __half22float2(*reinterpret_cast<const __half2*>(params + 2 * entry));
 }
+
+// Corner accumulation in the table type, as tcnn's kernel_grid does
+// (`result = fma((T)weight, grid_val(local_pos), result)`, corners in index
+// order with the x bit fastest): fp32 tables accumulate with fp32 fmaf; fp16
+// tables round the trilinear weight to half and accumulate with a packed half
+// FMA (v_pk_fma_f16: one rounding per feature per corner), so an fp16
+// encoding holds exactly the half values tcnn's fp16 GridEncoding returns.
+template <typename Tp>
+struct CornerAcc;
+template <>
+struct CornerAcc<float> {
+    using raw = float2;
+    float2 a = make_float2(0.0f, 0.0f);
+    __device__ __forceinline__ static raw load(const float* table, uint32_t e) {
+        return *reinterpret_cast<const float2*>(table + 2 * (size_t)e);
+    }
+    __device__ __forceinline__ void add(float w, raw v) {
+        a.x = fmaf(w, v.x, a.x);
+        a.y = fmaf(w, v.y, a.y);
+    }
+    __device__ __forceinline__ float2 get() const { return a; }
+};
+template <>
+struct CornerAcc<__half> {
+    using raw = __half2;
+    __half2 a = __float2half2_rn(0.0f);
+    __device__ __forceinline__ static raw load(const __half* table, uint32_t e) {
+        return *reinterpret_cast<const __half2*>(table + 2 * (size_t)e);
+    }
+    __device__ __forceinline__ void add(float w, raw v) {
+        // v_pk_fma_f16 explicitly: left to itself the compiler folds the
+        // weight's float->half conversion into v_fma_mixlo_f16, which rounds
+        // the fma to f32 and then to f16 (double rounding: ~1 element in 10^4
+        // one half-ulp off tcnn's single-rounded __hfma2)
+        const __half2 w2 = __float2half2_rn(w);
+        uint32_t r, wu, vu, au;
+        __builtin_memcpy(&wu, &w2, 4);
+        __builtin_memcpy(&vu, &v, 4);
+        __builtin_memcpy(&au, &a, 4);
+        asm("v_pk_fma_f16 %0, %1, %2, %3" : "=v"(r) : "v"(wu), "v"(vu), "v"(au));
+        __builtin_memcpy(&a, &r, 4);
+    }
+    __device__ __forceinline__ float2 get() const { return __half22float2(a); }  // exact
+};
 
 template <typename To>
 __device__ __forceinline__ void store_pair(To* out, int64_t i, float2 v);
@@ -117,7 +162,7 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(int64_t N, int L,
     const uint32_t size = (uint32_t)(lt.offset[l + 1] - lt.offset[l]);
     const uint32_t res = lt.res[l];
     const Tp* table = params + 2 * lt.offset[l];
-    float2 acc = make_float2(0.0f, 0.0f);
+    CornerAcc<Tp> acc;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         float wgt = 1.0f;
@@ -132,11 +177,9 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_kernel(int64_t N, int L,
                 g[d] = c.grid[d];
             }
         }
-        const float2 v = load_pair(table, grid_index(size, res, g[0], g[1], g[2]));
-        acc.x = fmaf(wgt, v.x, acc.x);
-        acc.y = fmaf(wgt, v.y, acc.y);
+        acc.add(wgt, CornerAcc<Tp>::load(table, grid_index(size, res, g[0], g[1], g[2])));
     }
-    store_pair(out, q, acc);
+    store_pair(out, q, acc.get());
 }
 
 // Level-major forward for inference: grid (points / 256, L), blockIdx.y =
@@ -174,12 +217,12 @@ struct EntryGroup<__half> {
         d[2] = v.z;
         d[3] = v.w;
     }
-    __device__ __forceinline__ float2 get(uint32_t e) const {
+    __device__ __forceinline__ __half2 get(uint32_t e) const {
         const uint32_t j = e & (kN - 1);
         const uint32_t v = j == 0 ? d[0] : j == 1 ? d[1] : j == 2 ? d[2] : d[3];
         __half2 h;
         __builtin_memcpy(&h, &v, 4);
-        return __half22float2(h);
+        return h;
     }
 };
 
@@ -195,7 +238,7 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_lm_kernel(int64_t N, const f
     const uint32_t size = (uint32_t)(lt.offset[l + 1] - lt.offset[l]);
     const uint32_t res = lt.res[l];
     const Tp* table = params + 2 * lt.offset[l];
-    float2 acc = make_float2(0.0f, 0.0f);
+    CornerAcc<Tp> acc;
     // corner weights and entries in the order k = 0..7 (x bit fastest)
     float wgt[8];
     uint32_t ent[8];
@@ -221,30 +264,25 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_lm_kernel(int64_t N, const f
         EntryGroup<Tp> grp[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) grp[j].load(table, ent[2 * j]);
-        float2 far[4];
+        using raw = typename CornerAcc<Tp>::raw;
+        raw far[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            far[j] = make_float2(0.0f, 0.0f);
-            if ((ent[2 * j + 1] ^ ent[2 * j]) >= kN) far[j] = load_pair(table, ent[2 * j + 1]);
+            far[j] = grp[j].get(ent[2 * j]);
+            if ((ent[2 * j + 1] ^ ent[2 * j]) >= kN) far[j] = CornerAcc<Tp>::load(table, ent[2 * j + 1]);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const float2 v0 = grp[j].get(ent[2 * j]);
-            const float2 v1 = ((ent[2 * j + 1] ^ ent[2 * j]) >= kN) ? far[j] : grp[j].get(ent[2 * j + 1]);
-            acc.x = fmaf(wgt[2 * j], v0.x, acc.x);
-            acc.y = fmaf(wgt[2 * j], v0.y, acc.y);
-            acc.x = fmaf(wgt[2 * j + 1], v1.x, acc.x);
-            acc.y = fmaf(wgt[2 * j + 1], v1.y, acc.y);
+            const raw v0 = grp[j].get(ent[2 * j]);
+            const raw v1 = ((ent[2 * j + 1] ^ ent[2 * j]) >= kN) ? far[j] : grp[j].get(ent[2 * j + 1]);
+            acc.add(wgt[2 * j], v0);
+            acc.add(wgt[2 * j + 1], v1);
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const float2 v = load_pair(table, ent[k]);
-            acc.x = fmaf(wgt[k], v.x, acc.x);
-            acc.y = fmaf(wgt[k], v.y, acc.y);
-        }
+        for (int k = 0; k < 8; ++k) acc.add(wgt[k], CornerAcc<Tp>::load(table, ent[k]));
     }
-    store_pair(out, ROW_MAJOR ? i * (int64_t)gridDim.y + l : (int64_t)l * N + i, acc);
+    store_pair(out, ROW_MAJOR ? i * (int64_t)gridDim.y + l : (int64_t)l * N + i, acc.get());
 }
 
 // Backward: scatter-add of w_corner * dL/dy into the tables.
@@ -464,7 +502,7 @@ __device__ __forceinline__ float2 encode_point_level(const float* xi, const Tp* 
     const uint32_t size = (uint32_t)(lt.offset[l + 1] - lt.offset[l]);
     const uint32_t res = lt.res[l];
     const Tp* table = params + 2 * lt.offset[l];
-    float2 acc = make_float2(0.0f, 0.0f);
+    CornerAcc<Tp> acc;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         float wgt = 1.0f;
@@ -479,11 +517,9 @@ __device__ __forceinline__ float2 encode_point_level(const float* xi, const Tp* 
                 g[d] = c.grid[d];
             }
         }
-        const float2 v = load_pair(table, grid_index(size, res, g[0], g[1], g[2]));
-        acc.x = fmaf(wgt, v.x, acc.x);
-        acc.y = fmaf(wgt, v.y, acc.y);
+        acc.add(wgt, CornerAcc<Tp>::load(table, grid_index(size, res, g[0], g[1], g[2])));
     }
-    return acc;
+    return acc.get();
 }
 
 __device__ __forceinline__ float round_feature(float v, bool f16, bool mlp_f16) {

@@ -76,11 +76,11 @@ __host__ __device__ constexpr size_t exact_lds_bytes(int R) {
     return 2 * (size_t)kTileRays * a_row_bytes(KS) + 8 * (size_t)((R + kTileRays - 1) / kTileRays * kTileRays);
 }
 
-template <typename E, int KS, int WAVES>
+template <typename E, int KS, int WAVES, int DBG = 0>
 __global__ __launch_bounds__(64 * WAVES) void head_exact_fwd_kernel(
     avr_render_params pp, int B, int R, int K, const E* __restrict__ h, const E* __restrict__ W,
     const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
-    float* __restrict__ z, int ntb, int per_xcd, int dbg) {
+    float* __restrict__ z, int ntb, int per_xcd) {
     constexpr int NT = 64 * WAVES;
     constexpr int TB = 32 * WAVES;  // t per workgroup
     constexpr int ROWB = a_row_bytes(KS);
@@ -88,7 +88,8 @@ __global__ __launch_bounds__(64 * WAVES) void head_exact_fwd_kernel(
     extern __shared__ __attribute__((aligned(16))) char lds_x[];
     char* abuf = lds_x;                                                      // [2][32][ROWB]
     int* pl = reinterpret_cast<int*>(lds_x + 2 * kTileRays * ROWB);          // perm of the column [R]
-    float* wl = reinterpret_cast<float*>(pl + R);                            // ws of the column [R]
+    // ws of the column after the padded perm, 16-byte aligned (read as float4)
+    float* wl = reinterpret_cast<float*>(pl + (R + kTileRays - 1) / kTileRays * kTileRays);
 
     const int T = pp.T, S = pp.n_samples;
     // XCD-aware order: the t-blocks of one column are consecutive on one XCD
@@ -116,14 +117,17 @@ __global__ __launch_bounds__(64 * WAVES) void head_exact_fwd_kernel(
     const int cnt_t = (t < lim) ? ccol[t] : 0;
     const int cwave = (t0 < lim) ? ccol[min(t0 + 31, lim - 1)] : 0;  // rays live in this wave's tile
 
-    // B operand: W rows t0..t0+31, k = 16 ks + 8 half + 0..7 (registers for the launch)
+    // B operand: W rows t0..t0+31, k = 16 ks + 8 half + 0..7 (registers for
+    // the launch); k-steps past K are zero (loads clamped, then selected)
     frag8 wf[KS];
     const int ks_n = K / 16;
     {
         const E* wrow = W + (int64_t)min(t, T - 1) * K + 8 * half;
 #pragma unroll
+        for (int ks = 0; ks < KS; ++ks) wf[ks] = *reinterpret_cast<const frag8*>(wrow + 16 * min(ks, ks_n - 1));
+#pragma unroll
         for (int ks = 0; ks < KS; ++ks)
-            wf[ks] = ks < ks_n ? *reinterpret_cast<const frag8*>(wrow + 16 * ks) : frag8{0u, 0u, 0u, 0u};
+            if (ks >= ks_n) wf[ks] = frag8{0u, 0u, 0u, 0u};
     }
     // the column's sorted rays and weights for the block's tiles; positions
     // past nblk repeat a live ray (its rows are masked) with weight 0
@@ -133,32 +137,41 @@ __global__ __launch_bounds__(64 * WAVES) void head_exact_fwd_kernel(
         pl[p] = perm[col * R + (in ? p : nblk - 1)];
         wl[p] = in ? ws[col * R + p] : 0.0f;
     }
+    // this thread's chunks of a tile: row and 16-byte column, fixed over the
+    // tiles (chunks past 32 rows wrap: duplicates of the same values)
+    const int cpr = K / 8;
+    int crow[CPT], hoff[CPT], aoff[CPT];
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+        const int ch = (threadIdx.x + NT * c) % (kTileRays * cpr);
+        crow[c] = ch / cpr;
+        const int cc = ch - crow[c] * cpr;
+        hoff[c] = 8 * cc;
+        aoff[c] = crow[c] * ROWB + 16 * cc;
+    }
     __syncthreads();
-    const int cpr = K / 8;  // 16-byte chunks per row
     const int64_t hstride = (int64_t)S * K;
     const E* hcol = h + ((int64_t)b * R * S + s) * K;
 
-    // A-tile staging: whole h rows, 16 bytes per lane, two tiles in flight
-    // (registers) ahead of the one the MFMAs read from LDS
+    // A-tile staging: whole h rows, 16 bytes per lane, loaded unconditionally
+    // (no exec-masked load whose result would be waited for in its branch),
+    // two tiles in flight ahead of the one the MFMAs read from LDS
     auto issue = [&](frag8 (&ld)[CPT], int tile) {
         const int p0 = tile * kTileRays;
+        int ray[CPT];
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) ray[c] = pl[p0 + crow[c]];
 #pragma unroll
         for (int c = 0; c < CPT; ++c) {
-            const int ch = threadIdx.x + NT * c;
-            const int row = ch / cpr, cc = ch - row * cpr;
-            if (row < kTileRays && !(dbg & 2))
-                ld[c] = __builtin_nontemporal_load(
-                    reinterpret_cast<const frag8*>(hcol + (int64_t)pl[p0 + row] * hstride + 8 * cc));
+            // DBG & 2: every tile reads the first row (L2-resident): no HBM stream
+            const int64_t off = (DBG & 2) ? (int64_t)hoff[c] : (int64_t)ray[c] * hstride + hoff[c];
+            ld[c] = *reinterpret_cast<const frag8*>(hcol + off);
         }
     };
     auto commit = [&](const frag8 (&ld)[CPT], int buf) {
         char* a = abuf + buf * kTileRays * ROWB;
 #pragma unroll
-        for (int c = 0; c < CPT; ++c) {
-            const int ch = threadIdx.x + NT * c;
-            const int row = ch / cpr, cc = ch - row * cpr;
-            if (row < kTileRays) *reinterpret_cast<frag8*>(a + row * ROWB + 16 * cc) = ld[c];
-        }
+        for (int c = 0; c < CPT; ++c) *reinterpret_cast<frag8*>(a + aoff[c]) = ld[c];
     };
 
     float zl = 0.0f;
@@ -167,11 +180,14 @@ __global__ __launch_bounds__(64 * WAVES) void head_exact_fwd_kernel(
         if (p0 >= cwave) return;  // wave-uniform: no live (ray, t) pair of this wave in the tile
         const char* a = abuf + (it & 1) * kTileRays * ROWB + j * ROWB + 16 * half;
         f32x16 acc;
+        if constexpr (DBG & 1) {  // no MFMA: the epilogue on the A fragment
+            const frag8 v = *reinterpret_cast<const frag8*>(a);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
-        if (!(dbg & 1)) {
+            for (int i = 0; i < 16; ++i) acc[i] = __uint_as_float(v[i & 3]);
+        } else {
+            acc = mfma16<E>(*reinterpret_cast<const frag8*>(a), wf[0], f32x16{});
 #pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
+            for (int ks = 1; ks < KS; ++ks)
                 acc = mfma16<E>(*reinterpret_cast<const frag8*>(a + 32 * ks), wf[ks], acc);
         }
         // register r holds row (r & 3) + 8 (r >> 2) + 4 half of the tile, column t
@@ -215,12 +231,187 @@ __global__ __launch_bounds__(64 * WAVES) void head_exact_fwd_kernel(
     if (half == 0 && t < T) zcol[t] = (t < lim) ? zl + other : 0.0f;
 }
 
+// One wave per SIMD (4 waves, 128 t per workgroup, up to 512 registers per
+// lane): the register file holds the wave's W fragments AND all K/16 A
+// fragments of the current ray tile, so a tile's MFMAs issue back to back
+// (no per-MFMA LDS wait), and the epilogue of the previous tile is placed in
+// the same basic block as the current tile's MFMAs, whose issue gaps it
+// fills.  After the barrier that publishes tile it+1 its fragments are read
+// at once.  Same arithmetic and summation order as head_exact_fwd_kernel.
+template <typename E, int KS, int DBG = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void head_exact_pipe_kernel(
+    avr_render_params pp, int B, int R, int K, const E* __restrict__ h, const E* __restrict__ W,
+    const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
+    float* __restrict__ z, int ntb, int per_xcd) {
+    constexpr int WAVES = 4;
+    constexpr int NT = 64 * WAVES;
+    constexpr int TB = 32 * WAVES;
+    constexpr int ROWB = a_row_bytes(KS);
+    constexpr int CPT = (kTileRays * KS * 2 + NT - 1) / NT;
+    extern __shared__ __attribute__((aligned(16))) char lds_x[];
+    char* abuf = lds_x;
+    int* pl = reinterpret_cast<int*>(lds_x + 2 * kTileRays * ROWB);
+    float* wl = reinterpret_cast<float*>(pl + (R + kTileRays - 1) / kTileRays * kTileRays);
+
+    const int T = pp.T, S = pp.n_samples;
+    const int64_t total = (int64_t)B * S * ntb;
+    const int64_t L = (int64_t)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (L >= total) return;
+    const int64_t col = L / ntb;
+    const int tb = (int)(L % ntb);
+    const int s = (int)(col % S), b = (int)(col / S);
+    const int lim = tail_limit(pp, s);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int half = lane >> 5, j = lane & 31;
+    const int t0 = tb * TB + wave * 32;
+    const int t = t0 + j;
+    float* zcol = z + col * T;
+    const int tlast = min(tb * TB + TB, lim) - 1;
+    if (tlast < tb * TB) {
+        for (int i = threadIdx.x; i < TB; i += NT)
+            if (tb * TB + i < T) zcol[tb * TB + i] = 0.0f;
+        return;
+    }
+    const int* ccol = cnt + col * T;
+    const int nblk = ccol[tlast];
+    const int cnt_t = (t < lim) ? ccol[t] : 0;
+    const int cwave = (t0 < lim) ? ccol[min(t0 + 31, lim - 1)] : 0;
+    const int ntile = (nblk + kTileRays - 1) / kTileRays;
+    const int wtiles = (cwave + kTileRays - 1) / kTileRays;  // tiles 0..wtiles-1 hold this wave's live pairs
+
+    frag8 wf[KS];
+    const int ks_n = K / 16;
+    {
+        const E* wrow = W + (int64_t)min(t, T - 1) * K + 8 * half;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) wf[ks] = *reinterpret_cast<const frag8*>(wrow + 16 * min(ks, ks_n - 1));
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+            if (ks >= ks_n) wf[ks] = frag8{0u, 0u, 0u, 0u};
+    }
+    for (int p = threadIdx.x; p < ntile * kTileRays; p += NT) {
+        const bool in = p < nblk;
+        pl[p] = perm[col * R + (in ? p : nblk - 1)];
+        wl[p] = in ? ws[col * R + p] : 0.0f;
+    }
+    const int cpr = K / 8;
+    int crow[CPT], hoff[CPT], aoff[CPT];
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+        const int ch = (threadIdx.x + NT * c) % (kTileRays * cpr);
+        crow[c] = ch / cpr;
+        const int cc = ch - crow[c] * cpr;
+        hoff[c] = 8 * cc;
+        aoff[c] = crow[c] * ROWB + 16 * cc;
+    }
+    __syncthreads();
+    const int64_t hstride = (int64_t)S * K;
+    const E* hcol = h + ((int64_t)b * R * S + s) * K;
+
+    auto issue = [&](frag8 (&ld)[CPT], int tile) {
+        const int p0 = tile * kTileRays;
+        int ray[CPT];
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) ray[c] = pl[p0 + crow[c]];
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+            const int64_t off = (DBG & 2) ? (int64_t)hoff[c] : (int64_t)ray[c] * hstride + hoff[c];
+            ld[c] = *reinterpret_cast<const frag8*>(hcol + off);
+        }
+    };
+    auto commit = [&](const frag8 (&ld)[CPT], int buf) {
+        char* a = abuf + buf * kTileRays * ROWB;
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) *reinterpret_cast<frag8*>(a + aoff[c]) = ld[c];
+    };
+    frag8 af[KS];
+    auto read_frags = [&](int buf) {
+        const char* a = abuf + buf * kTileRays * ROWB + j * ROWB + 16 * half;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) af[ks] = *reinterpret_cast<const frag8*>(a + 32 * ks);
+    };
+    float zl = 0.0f;
+    auto mfma_tile = [&]() {
+        f32x16 acc;
+        if constexpr (DBG & 1) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] = __uint_as_float(af[i & 7][i & 3]);
+        } else {
+            acc = mfma16<E>(af[0], wf[0], f32x16{});
+#pragma unroll
+            for (int ks = 1; ks < KS; ++ks) acc = mfma16<E>(af[ks], wf[ks], acc);
+        }
+        return acc;
+    };
+    auto epilogue = [&](const f32x16& acc, int it) {
+        const int p0 = it * kTileRays;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 wv = *reinterpret_cast<const float4*>(wl + p0 + 8 * g + 4 * half);
+            const float w4[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int p = p0 + e + 8 * g + 4 * half;
+                const float wsel = (p < cnt_t) ? w4[e] : 0.0f;
+                zl = fmaf(wsel, round16<E>(acc[4 * g + e]), zl);
+            }
+        }
+    };
+
+    frag8 ldA[CPT], ldB[CPT];
+    f32x16 accA, accB;
+    // iteration it: MFMAs of tile it into `cur` while the epilogue of tile
+    // it-1 (`prev`) fills their gaps; then tile it+1 is committed, published
+    // by the barrier, and its fragments are read
+    auto body = [&](int it, frag8 (&nxt)[CPT], frag8 (&nn)[CPT], f32x16& cur, f32x16& prev) {
+        if (it + 2 < ntile) issue(nn, it + 2);
+        if (it < wtiles) {
+            cur = mfma_tile();
+            if (it >= 1) epilogue(prev, it - 1);
+        } else if (it == wtiles && it >= 1) {
+            epilogue(prev, it - 1);
+        }
+        if (it + 1 < ntile) commit(nxt, (it + 1) & 1);
+        lds_barrier();
+        if (it + 1 < ntile) read_frags((it + 1) & 1);
+    };
+    if (ntile > 0) {
+        issue(ldA, 0);
+        if (K < 16 * KS) {
+            for (int i = threadIdx.x; i < 2 * kTileRays * ROWB / 16; i += NT)
+                reinterpret_cast<frag8*>(abuf)[i] = frag8{0u, 0u, 0u, 0u};
+            __syncthreads();
+        }
+        if (ntile > 1) issue(ldB, 1);
+        commit(ldA, 0);
+        lds_barrier();
+        read_frags(0);
+    }
+    int it = 0;
+    for (; it + 1 < ntile; it += 2) {
+        body(it, ldB, ldA, accA, accB);
+        body(it + 1, ldA, ldB, accB, accA);
+    }
+    if (it < ntile) {
+        body(it, ldB, ldA, accA, accB);
+        ++it;
+        // the last tile's epilogue (if this wave computed it)
+        if (it - 1 < wtiles) epilogue(accA, it - 1);
+    } else if (it >= 1 && it - 1 < wtiles) {
+        epilogue(accB, it - 1);
+    }
+    const float other = __shfl_xor(zl, 32, 64);
+    if (half == 0 && t < T) zcol[t] = (t < lim) ? zl + other : 0.0f;
+}
+
 int exact_shape(const avr_render_params& p, int K, int* KS, int* waves) {
     if (K % 16 != 0 || K < 16 || K > 512) return fail(AVR_E_CONFIG, "exact head: K must be a multiple of 16, <= 512");
     const int ks = K / 16;
     *KS = ks <= 8 ? 8 : (ks <= 16 ? 16 : 32);
+    // 0: head_exact_pipe_kernel (one wave per SIMD, 4 waves); 8 / 4: the
+    // two-waves-per-SIMD head_exact_fwd_kernel (experiments)
     int w = 8;
-    if (const char* e = getenv("AVR_HEAD_EXACT_WAVES")) w = atoi(e) == 4 ? 4 : 8;  // experiments
+    if (const char* e = getenv("AVR_HEAD_EXACT_WAVES")) w = atoi(e) == 4 ? 4 : (atoi(e) == 8 ? 8 : 0);
     *waves = w;
     return 0;
 }
@@ -244,12 +435,13 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
     AVR_REQUIRE(R >= 1 && R <= 4096 && T >= 2 && S >= 1, "avr_head_fwd_exact: shape out of range");
     int KS, waves;
     if (int e = exact_shape(*p, K, &KS, &waves)) return e;
-    const int TB = 32 * waves;
+    const int TB = 32 * (waves == 0 ? 4 : waves);
     const int ntb = (T + TB - 1) / TB;
     const int64_t total = (int64_t)B * S * ntb;
     const int per_xcd = (int)((total + 7) / 8);
     const dim3 grid((unsigned)(8 * per_xcd));
-    const char* dbg_env = getenv("AVR_HEAD_EXACT_DBG");  // profiling only: 1 no MFMA, 2 no h loads
+    // profiling only: 1 = no MFMA, 2 = no HBM stream (fp16, K = 512, 8 waves)
+    const char* dbg_env = getenv("AVR_HEAD_EXACT_DBG");
     const int dbg = dbg_env ? atoi(dbg_env) : 0;
     hipStream_t st = as_stream(stream);
     auto go = [&](auto kern, auto ks_tag, auto w_tag, auto hp) {
@@ -257,8 +449,34 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
         const size_t lds = exact_lds_bytes<KSV, WV>(R);
         allow_lds(kern, lds);
         hipLaunchKernelGGL(kern, grid, dim3(64 * WV), lds, st, *p, (int)B, R, (int)K, hp, (decltype(hp))W,
-                           perm, ws, cnt, z, ntb, per_xcd, dbg);
+                           perm, ws, cnt, z, ntb, per_xcd);
     };
+    using I32 = std::integral_constant<int, 32>;
+    using I8 = std::integral_constant<int, 8>;
+    using I4 = std::integral_constant<int, 4>;
+    if (waves == 0) {  // default form
+        if (dbg && dtype == AVR_DTYPE_F16 && KS == 32) {
+            if (dbg == 1) go(head_exact_pipe_kernel<__half, 32, 1>, I32{}, I4{}, (const __half*)h);
+            else if (dbg == 2) go(head_exact_pipe_kernel<__half, 32, 2>, I32{}, I4{}, (const __half*)h);
+            else go(head_exact_pipe_kernel<__half, 32, 3>, I32{}, I4{}, (const __half*)h);
+            return check_launch("avr_head_fwd_exact");
+        }
+#define AVR_HP(TY, KSV) \
+        if (KS == KSV) go(head_exact_pipe_kernel<TY, KSV>, std::integral_constant<int, KSV>{}, I4{}, (const TY*)h);
+        if (dtype == AVR_DTYPE_F16) {
+            AVR_HP(__half, 8) AVR_HP(__half, 16) AVR_HP(__half, 32)
+        } else {
+            AVR_HP(__hip_bfloat16, 8) AVR_HP(__hip_bfloat16, 16) AVR_HP(__hip_bfloat16, 32)
+        }
+#undef AVR_HP
+        return check_launch("avr_head_fwd_exact");
+    }
+    if (dbg && dtype == AVR_DTYPE_F16 && KS == 32 && waves == 8) {
+        if (dbg == 1) go(head_exact_fwd_kernel<__half, 32, 8, 1>, I32{}, I8{}, (const __half*)h);
+        else if (dbg == 2) go(head_exact_fwd_kernel<__half, 32, 8, 2>, I32{}, I8{}, (const __half*)h);
+        else go(head_exact_fwd_kernel<__half, 32, 8, 3>, I32{}, I8{}, (const __half*)h);
+        return check_launch("avr_head_fwd_exact");
+    }
 #define AVR_HX(TY, KSV, WV)                                                                          \
     if (KS == KSV && waves == WV)                                                                    \
         go(head_exact_fwd_kernel<TY, KSV, WV>, std::integral_constant<int, KSV>{},                   \

@@ -28,6 +28,9 @@ def _points(n, seed):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("n", [4096, 20000])  # 20000: the level-major dispatch (>= 16384 points)
 def test_forward_matches_restatement(dtype, n):
+    """fp32 encodings within 2e-6 of the restatement (same fma chain), fp16
+    encodings bit-identical to it (half weight, half fma chain, tcnn's
+    kernel_grid with T = half)."""
     enc = HashGridEncoding(3, CFG, dtype=dtype, seed=5).to(DEV)
     with torch.no_grad():
         enc.params.uniform_(-1, 1)
@@ -35,9 +38,14 @@ def test_forward_matches_restatement(dtype, n):
     out = enc(torch.from_numpy(x).to(DEV)).detach().float().cpu().numpy()
     # fp16 encodings read fp16 tables (tcnn's param precision), fp32 ones fp32
     table = enc.params.detach().to(enc.param_dtype).float().cpu().numpy()
-    ref = hgo.encode(x, table, enc._off, enc._scale, enc._res)
-    tol = 2e-6 if dtype == torch.float32 else 1e-3
-    np.testing.assert_allclose(out, ref, rtol=tol, atol=tol)
+    if dtype == torch.float16:
+        # tcnn's fp16 GridEncoding: half weights, half fma chain in corner
+        # order -- the same half values, bit for bit
+        ref = hgo.encode(x, table, enc._off, enc._scale, enc._res, table_dtype=np.float16)
+        np.testing.assert_array_equal(out, ref)
+    else:
+        ref = hgo.encode(x, table, enc._off, enc._scale, enc._res)
+        np.testing.assert_allclose(out, ref, rtol=2e-6, atol=2e-6)
 
 
 def test_backward_matches_restatement():
@@ -94,3 +102,46 @@ def test_level_major_forward_on_ray_points(dtype):
         a = enc(x)  # 4096 points: the per-point kernel
         b = enc.forward_level_major(x)
         assert torch.equal(a, b.permute(1, 0, 2).reshape(x.size(0), 40))
+
+
+def _ray_points(n_rays, n_samples, seed, step=1.3e-3):
+    """Ray-ordered points as the renderer lays them out: many consecutive
+    samples in one coarse cell (atomic contention on the coarse levels)."""
+    rng = np.random.default_rng(seed)
+    o = rng.uniform(0.2, 0.8, size=(n_rays, 1, 3))
+    d = rng.standard_normal(size=(n_rays, 1, 3))
+    d /= np.linalg.norm(d, axis=-1, keepdims=True)
+    t = np.arange(n_samples)[None, :, None] * step
+    return np.clip(o + d * t, 0, 1).reshape(-1, 3).astype(np.float32)
+
+
+@pytest.mark.parametrize("log2", [18, 20])
+@pytest.mark.parametrize("gdtype", [torch.float32, torch.float16])
+def test_backward_reference_size_tables(log2, gdtype):
+    """The backward where it runs: 20 levels at the reference's table sizes
+    (2^18 everywhere, 2^20 for MeshRIR's direction grid,
+    config_files/avr_meshrir.yml:56-61), ray-ordered points (equal
+    addresses within a wave and across waves: the run-sum and the fp32
+    atomics both exercised) plus random ones (hash collisions on the fine
+    levels), with fp32 and fp16 upstream gradients (an fp16 encoding's
+    grad_out is fp16), against the float64 scatter-add of the restatement.
+    fp32 atomics in any order: 1e-5 relative to the gradient's scale."""
+    cfg = dict(CFG, log2_hashmap_size=log2)
+    enc = HashGridEncoding(3, cfg, dtype=gdtype, seed=9).to(DEV)
+    x = np.concatenate([_ray_points(48, 256, 4), _points(8192, 5)])
+    xt = torch.from_numpy(x).to(DEV)
+    out = enc(xt)
+    assert out.dtype == gdtype
+    rng = np.random.default_rng(6)
+    g = rng.standard_normal(size=out.shape).astype(np.float32)
+    gt = torch.from_numpy(g).to(DEV).to(gdtype)
+    out.backward(gt)
+    g_used = gt.float().cpu().numpy()  # the values the kernel reads
+    ref = hgo.encode_backward(x, g_used, enc._off, enc._scale, enc._res, enc.n_params)
+    got = enc.params.grad.double().cpu().numpy()
+    scale = np.abs(ref).max()
+    assert scale > 0
+    err = np.abs(got - ref).max() / scale
+    assert err < 1e-5, err
+    # every touched entry is touched in both, and no other
+    np.testing.assert_array_equal(got != 0, ref != 0)
