@@ -404,14 +404,242 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (half == 0 && t < T) zcol[t] = (t < lim) ? zl + other : 0.0f;
 }
 
+// LDS-DMA form for K = 512 (the reference networks' width), 8 waves, two
+// per SIMD: each 1 KiB h row goes from global memory straight into its
+// (padded) LDS row with one global_load_lds_dwordx4 (no staging registers),
+// three tile buffers so two tiles are in flight behind the one the MFMAs
+// read; the freed registers let more A-fragment reads run ahead of the
+// MFMA chain.  Tile it+1's rows are complete when this wave's DMA count
+// drops to the tile it+2 rows it issued after them (s_waitcnt vmcnt), and
+// visible to every wave after the barrier.  Same arithmetic and order as
+// head_exact_fwd_kernel.
+// One 16-byte-per-lane LDS-DMA load: lane i's 16 bytes at g land at LDS byte
+// address lds + 16 i.  Issued as inline asm so the compiler does not treat
+// the in-flight DMA as an LDS write every later ds_read must wait for (with
+// the builtin it inserts vmcnt(0) inside the MFMA chain, which drains the
+// prefetched tiles); completion is waited for explicitly (wait_dma).
+__device__ __forceinline__ void dma_row16(const void* g, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(g)
+                 : "memory", "m0");
+}
+
+template <typename E, int TR, int NBUF, int DBG = 0>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void head_exact_dma_kernel(
+    avr_render_params pp, int B, int R, int K, const E* __restrict__ h, const E* __restrict__ W,
+    const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
+    float* __restrict__ z, int ntb, int per_xcd) {
+    constexpr int KS = 32, WAVES = 8, NT = 512, TB = 256;
+    constexpr int PD = NBUF - 1;            // tiles in flight behind the one being computed
+    constexpr int ROWB = a_row_bytes(KS);   // 1040
+    constexpr int RPW = TR / WAVES;         // rows each wave moves per tile
+    static_assert(TR % 32 == 0 && RPW * (NBUF - 2) <= 63 && NBUF <= 4, "tile rays / buffers");
+    extern __shared__ __attribute__((aligned(16))) char lds_x[];
+    char* abuf = lds_x;  // [NBUF][TR][ROWB]
+    int* pl = reinterpret_cast<int*>(lds_x + NBUF * TR * ROWB);
+    float* wl = reinterpret_cast<float*>(pl + (R + TR - 1) / TR * TR);
+
+    const int T = pp.T, S = pp.n_samples;
+    const int64_t total = (int64_t)B * S * ntb;
+    const int64_t L = (int64_t)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (L >= total) return;
+    const int64_t col = L / ntb;
+    const int tb = (int)(L % ntb);
+    const int s = (int)(col % S), b = (int)(col / S);
+    const int lim = tail_limit(pp, s);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int half = lane >> 5, j = lane & 31;
+    const int t0 = tb * TB + wave * 32;
+    const int t = t0 + j;
+    float* zcol = z + col * T;
+    const int tlast = min(tb * TB + TB, lim) - 1;
+    if (tlast < tb * TB) {
+        for (int i = threadIdx.x; i < TB; i += NT)
+            if (tb * TB + i < T) zcol[tb * TB + i] = 0.0f;
+        return;
+    }
+    const int* ccol = cnt + col * T;
+    const int nblk = ccol[tlast];
+    const int cnt_t = (t < lim) ? ccol[t] : 0;
+    const int cwave = (t0 < lim) ? ccol[min(t0 + 31, lim - 1)] : 0;
+    // rays live at EVERY t of this wave's tile (cnt is nondecreasing in t):
+    // a 32-ray sub-tile below it needs no mask in its epilogue
+    const int cfull = __builtin_amdgcn_readfirstlane((t0 + 31 < lim) ? ccol[t0] : 0);
+    const int ntile = (nblk + TR - 1) / TR;
+
+    frag8 wf[KS];
+    {
+        const E* wrow = W + (int64_t)min(t, T - 1) * K + 8 * half;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) wf[ks] = *reinterpret_cast<const frag8*>(wrow + 16 * ks);
+        // land them here: otherwise the compiler sinks these loads into the
+        // tile loop and waits on them there by vmcnt, which also counts the
+        // tile DMAs in flight (it does not see the asm-issued ones)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(wf[ks]));
+    }
+    for (int p = threadIdx.x; p < ntile * TR; p += NT) {
+        const bool in = p < nblk;
+        pl[p] = perm[col * R + (in ? p : nblk - 1)];
+        wl[p] = in ? ws[col * R + p] : 0.0f;
+    }
+    __syncthreads();
+    const int64_t hstride = (int64_t)S * K;
+    const E* hcol = h + ((int64_t)b * R * S + s) * K + 8 * lane;
+
+    // rows wave*RPW .. +RPW-1 of tile `tile` into buffer tile % NBUF; the
+    // wave's RPW ray indices come from LDS in one vector read
+    auto issue = [&](int tile) {
+        const int p0 = tile * TR + wave * RPW;
+        char* a = abuf + (tile % NBUF) * TR * ROWB + wave * RPW * ROWB;
+        int ray[RPW];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) ray[r] = pl[p0 + r];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const int rr = __builtin_amdgcn_readfirstlane(ray[r]);
+            const int64_t off = (DBG & 2) ? (int64_t)(r & 7) * hstride : (int64_t)rr * hstride;
+            dma_row16(hcol + off, (uint32_t)(uintptr_t)(a + r * ROWB));
+        }
+    };
+
+    float zl = 0.0f;
+    constexpr int kDepth = 8;  // A fragments read this many k-steps ahead of their MFMA
+    auto epilogue = [&](const f32x16& acc, int p0) {
+        if constexpr (DBG & 4) {  // no epilogue: keep the MFMA result alive only
+            zl += acc[0];
+            return;
+        }
+        if (p0 + 32 <= cfull) {  // every (ray, t) pair of the sub-tile is live
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 wv = *reinterpret_cast<const float4*>(wl + p0 + 8 * g + 4 * half);
+                zl = fmaf(wv.x, round16<E>(acc[4 * g + 0]), zl);
+                zl = fmaf(wv.y, round16<E>(acc[4 * g + 1]), zl);
+                zl = fmaf(wv.z, round16<E>(acc[4 * g + 2]), zl);
+                zl = fmaf(wv.w, round16<E>(acc[4 * g + 3]), zl);
+            }
+            return;
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const float4 wv = *reinterpret_cast<const float4*>(wl + p0 + 8 * g + 4 * half);
+            const float w4[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int p = p0 + e + 8 * g + 4 * half;
+                const float wsel = (p < cnt_t) ? w4[e] : 0.0f;
+                zl = fmaf(wsel, round16<E>(acc[4 * g + e]), zl);
+            }
+        }
+    };
+    // NQ consecutive 32-ray sub-tiles starting at row q0 of the tile in
+    // buffer `buf`: their MFMA chains back to back (the fragment reads of the
+    // next chain run under the previous one's MFMAs), then their epilogues
+    // in sub-tile order (the summation order of the other forms)
+    auto chains = [&](auto nq_tag, int buf, int q0, int p0) {
+        constexpr int NQ = decltype(nq_tag)::value;
+        const char* a = abuf + buf * TR * ROWB + (32 * q0 + j) * ROWB + 16 * half;
+        f32x16 acc[NQ];
+        if constexpr (DBG & 1) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const frag8 v = *reinterpret_cast<const frag8*>(a + q * 32 * ROWB);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[q][i] = __uint_as_float(v[i & 3]);
+            }
+        } else {
+            constexpr int N = NQ * KS;  // k-steps of all chains, in order
+            auto frag_at = [&](int n) {
+                return *reinterpret_cast<const frag8*>(a + (n / KS) * 32 * ROWB + 32 * (n % KS));
+            };
+            frag8 fr[kDepth];
+#pragma unroll
+            for (int i = 0; i < kDepth; ++i) fr[i] = frag_at(i);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) acc[q] = f32x16{};
+#pragma unroll
+            for (int n = 0; n < N; ++n) {
+                acc[n / KS] = mfma16<E>(fr[n % kDepth], wf[n % KS], acc[n / KS]);
+                if (n + kDepth < N) fr[n % kDepth] = frag_at(n + kDepth);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, kDepth, 0);  // the first kDepth DS reads
+#pragma unroll
+            for (int n = 0; n < N; ++n) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+                if (n + kDepth < N) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // then one DS read
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) epilogue(acc[q], p0 + 32 * q);
+    };
+    auto compute = [&](int it) {
+        const int p0 = it * TR, buf = it % NBUF;
+        if constexpr (TR == 64) {
+            if (p0 + 32 < cwave)
+                chains(std::integral_constant<int, 2>{}, buf, 0, p0);
+            else if (p0 < cwave)
+                chains(std::integral_constant<int, 1>{}, buf, 0, p0);
+        } else {
+            if (p0 < cwave) chains(std::integral_constant<int, 1>{}, buf, 0, p0);
+        }
+    };
+    // s_waitcnt vmcnt(n) (expcnt / lgkmcnt not waited on; gfx9 encoding)
+#define AVR_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 0xF) | (0x7 << 4) | (0xF << 8) | (((N) >> 4) << 14))
+    // this wave's DMAs still allowed in flight once the oldest tile landed:
+    // the RPW rows of each younger tile issued (n of them)
+    auto wait_vm = [](int n) {
+        switch (n) {  // the immediate must be a constant
+            case 0: AVR_VMCNT(0); break;
+            case 1: AVR_VMCNT(RPW); break;
+            case 2: AVR_VMCNT(2 * RPW); break;
+            default: AVR_VMCNT(0); break;
+        }
+    };
+#undef AVR_VMCNT
+    for (int i = 0; i < PD; ++i)
+        if (i < ntile) issue(i);
+    if (ntile > 0) {
+        wait_vm(min(PD, ntile) - 1);  // tile 0 landed (the younger ones may still fly)
+        __builtin_amdgcn_s_barrier();
+    }
+    if constexpr (DBG & 8) {  // no DMA, no barrier: every tile computed from the tile-0 buffer
+        for (int it = 0; it < ((DBG & 16) ? 0 : ntile); ++it) {  // DBG & 16: prologue and output only
+            const int p0 = it * TR;
+            if (p0 < cwave) chains(std::integral_constant<int, 1>{}, 0, 0, p0);
+        }
+        const float other = __shfl_xor(zl, 32, 64);
+        if (half == 0 && t < T) zcol[t] = (t < lim) ? zl + other : 0.0f;
+        return;
+    }
+    for (int it = 0; it < ntile; ++it) {
+        // into the buffer tile it-1 used: every wave left it at the last barrier
+        if (it + PD < ntile) issue(it + PD);
+        compute(it);
+        if (it + 1 < ntile) {
+            wait_vm(min(PD, ntile - 1 - it) - 1);  // tile it+1's rows from this wave have landed
+            __builtin_amdgcn_s_waitcnt(0xC07F);     // and every LDS read of tile it is done
+            __builtin_amdgcn_s_barrier();
+        }
+    }
+    const float other = __shfl_xor(zl, 32, 64);
+    if (half == 0 && t < T) zcol[t] = (t < lim) ? zl + other : 0.0f;
+}
+
 int exact_shape(const avr_render_params& p, int K, int* KS, int* waves) {
     if (K % 16 != 0 || K < 16 || K > 512) return fail(AVR_E_CONFIG, "exact head: K must be a multiple of 16, <= 512");
     const int ks = K / 16;
     *KS = ks <= 8 ? 8 : (ks <= 16 ? 16 : 32);
     // 0: head_exact_pipe_kernel (one wave per SIMD, 4 waves); 8 / 4: the
     // two-waves-per-SIMD head_exact_fwd_kernel (experiments)
-    int w = 8;
-    if (const char* e = getenv("AVR_HEAD_EXACT_WAVES")) w = atoi(e) == 4 ? 4 : (atoi(e) == 8 ? 8 : 0);
+    // default: the LDS-DMA form with 64-ray tiles for K = 512 (the reference
+    // networks' width), the register-staged form otherwise
+    int w = K == 512 ? 17 : 8;
+    if (const char* e = getenv("AVR_HEAD_EXACT_WAVES")) {
+        const int v = atoi(e);
+        w = (v == 4 || v == 8 || (v >= 16 && v <= 18)) ? v : 0;  // 16-18: the LDS-DMA forms (K = 512)
+    }
+    if (w >= 16 && K != 512) w = 8;
     *waves = w;
     return 0;
 }
@@ -435,7 +663,7 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
     AVR_REQUIRE(R >= 1 && R <= 4096 && T >= 2 && S >= 1, "avr_head_fwd_exact: shape out of range");
     int KS, waves;
     if (int e = exact_shape(*p, K, &KS, &waves)) return e;
-    const int TB = 32 * (waves == 0 ? 4 : waves);
+    const int TB = 32 * (waves == 0 ? 4 : (waves >= 16 ? 8 : waves));
     const int ntb = (T + TB - 1) / TB;
     const int64_t total = (int64_t)B * S * ntb;
     const int per_xcd = (int)((total + 7) / 8);
@@ -454,6 +682,38 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
     using I32 = std::integral_constant<int, 32>;
     using I8 = std::integral_constant<int, 8>;
     using I4 = std::integral_constant<int, 4>;
+    if (waves >= 16 && KS == 32 && K == 512) {  // LDS-DMA forms (16: 32-ray tiles x 3 buffers, 17: 64 x 2, 18: 32 x 4)
+        const int TRv = waves == 17 ? 64 : 32, NB = waves == 16 ? 3 : (waves == 17 ? 2 : 4);
+        const size_t lds = (size_t)NB * TRv * a_row_bytes(32) + 8 * (size_t)((R + TRv - 1) / TRv * TRv);
+        auto go_dma = [&](auto kern, auto hp) {
+            allow_lds(kern, lds);
+            hipLaunchKernelGGL(kern, grid, dim3(512), lds, st, *p, (int)B, R, (int)K, hp, (decltype(hp))W, perm, ws,
+                               cnt, z, ntb, per_xcd);
+        };
+#define AVR_HD(TRV, NBV)                                                                              \
+        if (dtype == AVR_DTYPE_F16) {                                                                 \
+            if (dbg == 1) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 1>, (const __half*)h);        \
+            else if (dbg == 2) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 2>, (const __half*)h);   \
+            else if (dbg == 3) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 3>, (const __half*)h);   \
+            else if (dbg == 4) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 4>, (const __half*)h);   \
+            else if (dbg == 6) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 6>, (const __half*)h);   \
+            else if (dbg == 8) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 8>, (const __half*)h);   \
+            else if (dbg == 12) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 12>, (const __half*)h); \
+            else if (dbg == 24) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 24>, (const __half*)h); \
+            else go_dma(head_exact_dma_kernel<__half, TRV, NBV, 0>, (const __half*)h);                 \
+        } else {                                                                                      \
+            go_dma(head_exact_dma_kernel<__hip_bfloat16, TRV, NBV, 0>, (const __hip_bfloat16*)h);     \
+        }
+        if (waves == 16) {
+            AVR_HD(32, 3)
+        } else if (waves == 17) {
+            AVR_HD(64, 2)
+        } else {
+            AVR_HD(32, 4)
+        }
+#undef AVR_HD
+        return check_launch("avr_head_fwd_exact");
+    }
     if (waves == 0) {  // default form
         if (dbg && dtype == AVR_DTYPE_F16 && KS == 32) {
             if (dbg == 1) go(head_exact_pipe_kernel<__half, 32, 1>, I32{}, I4{}, (const __half*)h);
