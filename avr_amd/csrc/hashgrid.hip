@@ -16,6 +16,8 @@
 // (fp16 tables: half FMAs, as tcnn's fp16 GridEncoding; CornerAcc).
 #include "common.h"
 
+#include <algorithm>
+
 using namespace avr;
 
 namespace {
@@ -298,55 +300,89 @@ __global__ __launch_bounds__(256) void hashgrid_fwd_lm_kernel(int64_t N, const f
 // wave-instruction (4 points x 16 dwords) touches ~4 segments per point
 // instead of 16 requests per point for a lane-per-point layout.
 //
-// Points of a wave that hit the same dword (consecutive samples of a ray in
-// one coarse cell) are first summed over runs of equal addresses across the
-// 4 points (head flags at lane stride 16) and only the last one adds.
-template <typename Tg>
-__global__ __launch_bounds__(256) void hashgrid_bwd_kernel(int64_t N, int L,
+// Each 16-lane group walks RUN consecutive points in order (the renderer's
+// points are ray-major, so these are consecutive samples of one ray) and a
+// lane keeps a pending (dword, sum): while the next point's corner hits the
+// same dword (a coarse cell several samples long) the value is added in
+// registers, and only a change of dword, or the end of the walk, issues the
+// atomic.  Coarse levels, where up to ~8 samples share a cell, then issue a
+// fraction of the requests; fine levels issue one per point as before.  All
+// coordinate and gradient loads of the walk are issued up front; the atomics
+// need no return, so the walk never waits on them.
+template <typename Tg, int RUN>
+__global__ __launch_bounds__(256) void hashgrid_bwd_kernel(int64_t N, int L, int l0,
                                                            const float* __restrict__ x,
                                                            const Tg* __restrict__ gout,
                                                            LevelTable lt,
                                                            float* __restrict__ gparams) {
-    const int l = blockIdx.y;
-    const int lane = threadIdx.x & 63;
+    const int l = l0 + (int)blockIdx.y;
     const int slot = threadIdx.x & 15;
     const int k = slot >> 1, f = slot & 1;
-    const int64_t i = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
-    const bool live = i < N;
-    const int64_t ic = live ? i : N - 1;
-    const float xi[3] = {x[ic * 3 + 0], x[ic * 3 + 1], x[ic * 3 + 2]};
-    const float g = live ? load_f(gout, ic * (2 * L) + 2 * l + f) : 0.0f;
-    const Corner c = locate(xi, lt.scale[l]);
+    const int64_t first = ((int64_t)blockIdx.x * 16 + (threadIdx.x >> 4)) * RUN;
     const uint32_t size = (uint32_t)(lt.offset[l + 1] - lt.offset[l]);
     const uint32_t res = lt.res[l];
-    float wgt = 1.0f;
-    uint32_t gg[3];
+    const float scale = lt.scale[l];
+    float* __restrict__ table = gparams + 2 * lt.offset[l];
+    float xi[RUN][3], g[RUN];
 #pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        if (k & (1 << d)) {
-            wgt *= c.pos[d];
-            gg[d] = c.grid[d] + 1;
+    for (int it = 0; it < RUN; ++it) {
+        const int64_t i = first + it;
+        const int64_t ic = i < N ? i : N - 1;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) xi[it][d] = x[ic * 3 + d];
+        g[it] = i < N ? load_f(gout, ic * (2 * L) + 2 * l + f) : 0.0f;
+    }
+    uint32_t pe = 0xffffffffu;
+    float pv = 0.0f;
+#pragma unroll
+    for (int it = 0; it < RUN; ++it) {
+        const Corner c = locate(xi[it], scale);
+        float wgt = 1.0f;
+        uint32_t gg[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            if (k & (1 << d)) {
+                wgt *= c.pos[d];
+                gg[d] = c.grid[d] + 1;
+            } else {
+                wgt *= 1.0f - c.pos[d];
+                gg[d] = c.grid[d];
+            }
+        }
+        const uint32_t e = 2u * grid_index(size, res, gg[0], gg[1], gg[2]) + (uint32_t)f;
+        const float v = wgt * g[it];
+        if (e == pe) {
+            pv += v;
         } else {
-            wgt *= 1.0f - c.pos[d];
-            gg[d] = c.grid[d];
+            if (pv != 0.0f) atomicAdd(table + pe, pv);
+            pe = e;
+            pv = v;
         }
     }
-    const uint32_t e = 2u * grid_index(size, res, gg[0], gg[1], gg[2]) + (uint32_t)f;
-    float v = wgt * g;
-    // runs of equal e over the wave's 4 points (same slot: lanes 16 apart)
-    const int p = lane >> 4;
-    const uint32_t prev = __shfl_up(e, 16, 64);
-    const bool head = p == 0 || prev != e;
-    const unsigned long long heads = __ballot(head);
-    int start = p;
-    while (!((heads >> (16 * start + slot)) & 1ull)) --start;  // <= 3 steps
-#pragma unroll
-    for (int off = 16; off < 64; off <<= 1) {
-        const float o = __shfl_up(v, off, 64);
-        if (lane - off >= 16 * start + slot) v += o;
+    if (pv != 0.0f) atomicAdd(table + pe, pv);
+}
+
+// points walked per 16-lane group (AVR_HASHGRID_BWD_RUN overrides: 1, 4, 8,
+// 16 or 32; experiments)
+inline int bwd_run() {
+    const char* e = getenv("AVR_HASHGRID_BWD_RUN");
+    const int v = e ? atoi(e) : 16;
+    return (v == 1 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 16;
+}
+
+template <typename Tg>
+void launch_bwd(hipStream_t st, int64_t N, int L, const float* x, const Tg* gout, const LevelTable& lt,
+                float* gparams) {
+    const int run = bwd_run();
+    const int64_t pts_per_block = 16 * (int64_t)run;  // 16 groups of 16 lanes
+    const dim3 grid((unsigned)((N + pts_per_block - 1) / pts_per_block), (unsigned)L);
+#define AVR_HG_BWD(I)                                                                                          \
+    if (run == I) {                                                                                            \
+        hipLaunchKernelGGL((hashgrid_bwd_kernel<Tg, I>), grid, dim3(256), 0, st, N, L, 0, x, gout, lt, gparams); \
+        return;                                                                                                \
     }
-    const bool tail = p == 3 || ((heads >> (lane + 16)) & 1ull);
-    if (tail && v != 0.0f) atomicAdd(gparams + 2 * lt.offset[l] + e, v);
+    AVR_HG_BWD(1) AVR_HG_BWD(4) AVR_HG_BWD(8) AVR_HG_BWD(16) AVR_HG_BWD(32)
+#undef AVR_HG_BWD
 }
 
 int make_table(int L, const int64_t* off, const float* scale, const int32_t* res, LevelTable* lt) {
@@ -394,6 +430,441 @@ int launch_fwd_lm(dim3 grid, hipStream_t st, int64_t N, const float* x, const vo
         launch_lm<__half, float, ROW_MAJOR>(grid, st, N, x, params, lt, out, grp);
     else
         return fail(AVR_E_ARG, "avr_hashgrid_fwd: unknown dtype");
+    return 0;
+}
+
+// ------------------------------------------- partitioned backward (no atomics)
+// The atomic backward above is bound by memory-side atomic requests (one per
+// 64-B segment a wave-instruction touches, ~4.5 per point and hashed level)
+// and, on the coarse levels, by many adders per address (every ray starts at
+// the listener, so its first samples share cells at every coarse level).
+// This form never adds into HBM concurrently:
+//   1. count:   every (level, chunk of kChunkPts points) block walks its
+//               points, merges equal entries along each 8-lane group's run,
+//               and counts the merged contributions per table partition
+//               (kPartEntries consecutive entries of one level) in LDS;
+//   2. scan:    one wave per partition turns its per-chunk counts into
+//               offsets and a total;
+//   3. scatter: the same walk writes each contribution (entry within the
+//               partition, value pair) into its partition's segment of a
+//               workspace (key and value arrays; partition-contiguous,
+//               chunk-ordered segments, slot order within a chunk free);
+//   4. reduce:  one block per partition sums its contributions into a 64 KB
+//               LDS image of the partition (LDS float atomics) and adds the
+//               image to the gradient with plain vector loads/stores (the
+//               block owns those entries: no other writer).
+// The workspace holds N * L * 8 contributions at most (12 B each).
+constexpr int kPartBits = 10;
+constexpr int kPartEntries = 1 << kPartBits;      // 1024 entries = 8 KB of fp32 pairs (one wave's image)
+constexpr int kBwdGroups = 32;                    // 8-lane groups per 256-thread block
+constexpr int kBwdRun = 16;                       // consecutive points walked per group
+constexpr int kChunkPts = kBwdGroups * kBwdRun;   // 512 points per block and level
+constexpr int kReduceWaves = 4;                   // reduce block: one partition slice per wave
+constexpr int kMaxScatterParts = 4096;            // partitions per level the count/scatter LDS holds
+
+struct BwdPlan {
+    int pbase[kMaxLevels + 1];  // first partition of each level (prefix of ceil(size / kPartEntries))
+    int nchunks;
+    int max_parts;              // partitions of the largest level
+    int slice_cap[kMaxLevels];  // contributions per reduce slice ...
+    int hot_above[kMaxLevels];  // ... and kDenseSlice for partitions holding more than this (hot cells)
+};
+
+// The walk shared by the count and scatter passes: lane k of 8-lane group g
+// owns corner k of the group's kBwdRun consecutive points (both features);
+// emit(entry, v0, v1) is called for every merged contribution, in walk order.
+template <typename Tg, class Emit>
+__device__ __forceinline__ void bwd_walk(int64_t N, int L, int l, const float* __restrict__ x,
+                                         const Tg* __restrict__ gout, const LevelTable& lt, Emit&& emit) {
+    const int k = threadIdx.x & 7;
+    const int64_t first = ((int64_t)blockIdx.x * kBwdGroups + (threadIdx.x >> 3)) * kBwdRun;
+    const uint32_t size = (uint32_t)(lt.offset[l + 1] - lt.offset[l]);
+    const uint32_t res = lt.res[l];
+    const float scale = lt.scale[l];
+    float xi[kBwdRun][3], g0[kBwdRun], g1[kBwdRun];
+#pragma unroll
+    for (int it = 0; it < kBwdRun; ++it) {
+        const int64_t i = first + it;
+        const bool live = i < N;
+        const int64_t ic = live ? i : N - 1;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) xi[it][d] = x[ic * 3 + d];
+        const int64_t gi = ic * (2 * L) + 2 * l;
+        g0[it] = live ? load_f(gout, gi) : 0.0f;
+        g1[it] = live ? load_f(gout, gi + 1) : 0.0f;
+    }
+    uint32_t pe = 0xffffffffu;
+    float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll
+    for (int it = 0; it < kBwdRun; ++it) {
+        const Corner c = locate(xi[it], scale);
+        float wgt = 1.0f;
+        uint32_t gg[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            if (k & (1 << d)) {
+                wgt *= c.pos[d];
+                gg[d] = c.grid[d] + 1;
+            } else {
+                wgt *= 1.0f - c.pos[d];
+                gg[d] = c.grid[d];
+            }
+        }
+        const uint32_t e = grid_index(size, res, gg[0], gg[1], gg[2]);
+        const float v0 = wgt * g0[it], v1 = wgt * g1[it];
+        if (e == pe) {
+            p0 += v0;
+            p1 += v1;
+        } else {
+            if (pe != 0xffffffffu && (p0 != 0.0f || p1 != 0.0f)) emit(pe, p0, p1);
+            pe = e;
+            p0 = v0;
+            p1 = v1;
+        }
+    }
+    if (pe != 0xffffffffu && (p0 != 0.0f || p1 != 0.0f)) emit(pe, p0, p1);
+}
+
+template <typename Tg>
+__global__ __launch_bounds__(256) void hg_bwd_count_kernel(int64_t N, int L, const float* __restrict__ x,
+                                                           const Tg* __restrict__ gout, LevelTable lt,
+                                                           BwdPlan plan, int* __restrict__ counts) {
+    extern __shared__ int cnt_l[];
+    const int l = blockIdx.y;
+    const int P = plan.pbase[l + 1] - plan.pbase[l];
+    for (int p = threadIdx.x; p < P; p += 256) cnt_l[p] = 0;
+    __syncthreads();
+    bwd_walk(N, L, l, x, gout, lt, [&](uint32_t e, float, float) { atomicAdd(&cnt_l[e >> kPartBits], 1); });
+    __syncthreads();
+    for (int p = threadIdx.x; p < P; p += 256)
+        counts[(int64_t)(plan.pbase[l] + p) * plan.nchunks + blockIdx.x] = cnt_l[p];
+}
+
+// one wave per partition: per-chunk counts -> exclusive offsets within the
+// partition (in place), and the partition's total
+__global__ __launch_bounds__(1024) void hg_bwd_scan_kernel(int total_parts, int nchunks, int* __restrict__ counts,
+                                                           int* __restrict__ totals) {
+    const int lane = threadIdx.x & 63;
+    const int p = blockIdx.x * 16 + (threadIdx.x >> 6);
+    if (p >= total_parts) return;
+    int* c = counts + (int64_t)p * nchunks;
+    int carry = 0;
+    for (int c0 = 0; c0 < nchunks; c0 += 64) {
+        const int v = c0 + lane < nchunks ? c[c0 + lane] : 0;
+        int incl = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int o = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += o;
+        }
+        if (c0 + lane < nchunks) c[c0 + lane] = carry + incl - v;
+        carry += __shfl(incl, 63, 64);
+    }
+    if (lane == 0) totals[p] = carry;
+}
+
+// one block: partition starts (exclusive prefix of the totals) and the
+// reduce pass's slices.  Every ray of a batch starts at its listener, so on
+// the dense (coarse) levels a few cells collect contributions from hundreds
+// of rays; their partitions are cut into slices of kDenseSlice contributions
+// (each summed by its own wave, the slices then added with no-return
+// atomics), so no single wave serialises a hot cell's repeats.  Hashed
+// levels keep one slice per partition where possible (plain flush).
+constexpr int kDenseSlice = 1024;
+// tag rounds before the per-key wave sums take over (a round costs about as
+// much as one key's wave sum and serves every distinct key at once: near the
+// listener a wave-load holds ~25 keys repeated up to ~7 times)
+constexpr int kTagRounds = 4;
+constexpr int kHashedSlice = 16384;
+
+__global__ __launch_bounds__(1024) void hg_bwd_plan_kernel(int total_parts, BwdPlan plan,
+                                                           const int* __restrict__ totals,
+                                                           int* __restrict__ part_start,
+                                                           int* __restrict__ slice_base) {
+    __shared__ int ws_t[16], ws_s[16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // thread t owns the `per` consecutive partitions from per * t: one
+    // block-wide scan for all of them
+    const int per = (total_parts + 1 + 1023) / 1024;
+    const int q0 = threadIdx.x * per;
+    int l = 0;
+    int st = 0, ss = 0;  // this thread's sums
+    for (int j = 0; j < per; ++j) {
+        const int q = q0 + j;
+        if (q >= total_parts) break;
+        const int t = totals[q];
+        while (plan.pbase[l + 1] <= q) ++l;
+        const int cap = t > plan.hot_above[l] ? kDenseSlice : plan.slice_cap[l];
+        st += t;
+        ss += max(1, (t + cap - 1) / cap);
+    }
+    int it = st, is = ss;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int ut = __shfl_up(it, off, 64), us = __shfl_up(is, off, 64);
+        if (lane >= off) {
+            it += ut;
+            is += us;
+        }
+    }
+    if (lane == 63) {
+        ws_t[wave] = it;
+        ws_s[wave] = is;
+    }
+    __syncthreads();
+    int pt = 0, ps = 0;
+    for (int w = 0; w < wave; ++w) {
+        pt += ws_t[w];
+        ps += ws_s[w];
+    }
+    int rt = pt + it - st, rs = ps + is - ss;  // exclusive prefixes at q0
+    l = 0;
+    for (int j = 0; j < per; ++j) {
+        const int q = q0 + j;
+        if (q > total_parts) break;
+        part_start[q] = rt;
+        slice_base[q] = rs;
+        if (q == total_parts) break;
+        const int t = totals[q];
+        while (plan.pbase[l + 1] <= q) ++l;
+        const int cap = t > plan.hot_above[l] ? kDenseSlice : plan.slice_cap[l];
+        rt += t;
+        rs += max(1, (t + cap - 1) / cap);
+    }
+}
+
+template <typename Tg>
+__global__ __launch_bounds__(256) void hg_bwd_scatter_kernel(int64_t N, int L, const float* __restrict__ x,
+                                                             const Tg* __restrict__ gout, LevelTable lt,
+                                                             BwdPlan plan, const int* __restrict__ offs,
+                                                             const int* __restrict__ part_start,
+                                                             uint32_t* __restrict__ keys,
+                                                             float2* __restrict__ vals) {
+    extern __shared__ int scat_l[];  // base[P], slot[P]
+    const int l = blockIdx.y;
+    const int pb = plan.pbase[l];
+    const int P = plan.pbase[l + 1] - pb;
+    int* base = scat_l;
+    int* slot = scat_l + P;
+    for (int q = threadIdx.x; q < P; q += 256) {
+        base[q] = part_start[pb + q] + offs[(int64_t)(pb + q) * plan.nchunks + blockIdx.x];
+        slot[q] = 0;
+    }
+    __syncthreads();
+    bwd_walk(N, L, l, x, gout, lt, [&](uint32_t e, float v0, float v1) {
+        const int part = (int)(e >> kPartBits);
+        const int pos = base[part] + atomicAdd(&slot[part], 1);
+        keys[pos] = e & (kPartEntries - 1);
+        vals[pos] = make_float2(v0, v1);
+    });
+}
+
+// Sum of x over the wave, uniform (DPP within rows of 16, then the four row
+// sums read as scalars: no LDS round trip, unlike __shfl_xor)
+template <int C>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), C, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_total(float x) {
+    x += dpp_f<0xB1>(x);   // quad_perm [1,0,3,2]
+    x += dpp_f<0x4E>(x);   // quad_perm [2,3,0,1]
+    x += dpp_f<0x141>(x);  // row_half_mirror
+    x += dpp_f<0x140>(x);  // row_mirror
+    const int xi = __float_as_int(x);
+    return (__int_as_float(__builtin_amdgcn_readlane(xi, 0)) + __int_as_float(__builtin_amdgcn_readlane(xi, 16))) +
+           (__int_as_float(__builtin_amdgcn_readlane(xi, 32)) + __int_as_float(__builtin_amdgcn_readlane(xi, 48)));
+}
+
+// One wave per partition slice, with the partition's image in the wave's own
+// LDS (no other wave touches it).  LDS float atomics measured slow on this
+// path (the reduce pass took ~160 of 330 us with ds_add_f32), so each
+// contribution is added with a plain read-add-write, made safe by a tag
+// round: every pending lane writes its lane id into tag[key], reads it back,
+// and only the lanes that find their own id add (their keys are distinct);
+// the others are summed per key across the wave and added once per key.
+// Keys repeat within one wave-load only where many rays cross the same
+// cells (coarse levels), so the tag round alone is the rule.
+__global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L, LevelTable lt, BwdPlan plan,
+                                                                         int total_parts,
+                                                                         const int* __restrict__ totals,
+                                                                         const int* __restrict__ part_start,
+                                                                         const int* __restrict__ slice_base,
+                                                                         const uint32_t* __restrict__ keys,
+                                                                         const float2* __restrict__ vals,
+                                                                         float* __restrict__ gparams, int dbg,
+                                                                         unsigned long long* __restrict__ dbg_out) {
+    __shared__ float2 img_all[kReduceWaves][kPartEntries];
+    __shared__ uint8_t tag_all[kReduceWaves][kPartEntries];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float2* img = img_all[wave];
+    uint8_t* tag = tag_all[wave];
+    const int b = blockIdx.x * kReduceWaves + wave;
+    if (b >= slice_base[total_parts]) return;  // the grid is sized for the worst case
+    // partition p: slice_base[p] <= b < slice_base[p + 1]
+    int lo = 0, hi = total_parts - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (slice_base[mid] <= b) lo = mid; else hi = mid - 1;
+    }
+    const int p = lo;
+    const int ns = slice_base[p + 1] - slice_base[p], sl = b - slice_base[p];
+    const int n = totals[p];
+    if (n == 0) return;  // wave-uniform
+    const unsigned long long t_start = (dbg & 4) ? __builtin_readcyclecounter() : 0ull;
+    unsigned long long n_iter = 0;
+    const int i0 = part_start[p] + (int)((int64_t)n * sl / ns);
+    const int i1 = part_start[p] + (int)((int64_t)n * (sl + 1) / ns);
+    int l = 0;
+    while (plan.pbase[l + 1] <= p) ++l;
+    const int64_t e0 = (int64_t)(p - plan.pbase[l]) * kPartEntries;
+    // level sizes are multiples of 8 entries: ne is, and the partition's
+    // 2*ne floats start 16-byte aligned
+    const int ne = (int)min((int64_t)kPartEntries, lt.offset[l + 1] - lt.offset[l] - e0);
+    for (int i = lane; i < ne; i += 64) img[i] = make_float2(0.f, 0.f);
+    constexpr int U = 8;
+    for (int i = i0; i < i1; i += 64 * U) {
+        uint32_t kk[U];
+        float2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = i + 64 * u + lane;
+            kk[u] = j < i1 ? keys[j] : 0u;
+            v[u] = j < i1 ? vals[j] : make_float2(0.f, 0.f);
+        }
+        if (dbg & 1) {  // timing experiment: no adds
+            float t = 0.f;
+#pragma unroll
+            for (int u = 0; u < U; ++u) t += v[u].x + v[u].y + (float)kk[u];
+            if (t == 12345.f) img[0].x = t;
+            continue;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            bool todo = i + 64 * u + lane < i1;
+            // up to kTagRounds rounds: each adds one lane per distinct pending key
+            for (int round = 0; round < kTagRounds; ++round) {
+                if (todo) tag[kk[u]] = (uint8_t)lane;
+                // compiler barrier: the read-back must not be folded into the
+                // lane's own write (LDS keeps one wave's accesses in order)
+                asm volatile("" ::: "memory");
+                if (todo && tag[kk[u]] == (uint8_t)lane) {
+                    float2 a = img[kk[u]];
+                    a.x += v[u].x;
+                    a.y += v[u].y;
+                    img[kk[u]] = a;
+                    todo = false;
+                }
+                asm volatile("" ::: "memory");
+                if (!__ballot(todo)) break;
+            }
+            // lanes whose key another lane of this load also holds: sum each
+            // such key's values across the wave (DPP sums) and add once.
+            // One iteration per distinct repeated key: none on the hashed
+            // levels as a rule, a few where many rays cross one coarse cell
+            uint64_t rest = __ballot(todo);
+            while (rest) {
+                const int first = __ffsll((unsigned long long)rest) - 1;
+                const uint32_t lead = (uint32_t)__builtin_amdgcn_readlane((int)kk[u], first);
+                const bool mine = todo && kk[u] == lead;
+                const float s0 = wave_total(mine ? v[u].x : 0.0f);
+                const float s1 = wave_total(mine ? v[u].y : 0.0f);
+                if (lane == first) {
+                    float2 a = img[lead];
+                    a.x += s0;
+                    a.y += s1;
+                    img[lead] = a;
+                }
+                asm volatile("" ::: "memory");
+                todo = todo && !mine;
+                rest = __ballot(todo);
+                ++n_iter;
+            }
+        }
+    }
+    if ((dbg & 4) && lane == 0) {  // diagnostics: slowest slice, butterfly iterations
+        const unsigned long long dt = __builtin_readcyclecounter() - t_start;
+        atomicMax(dbg_out, (dt << 24) | (unsigned long long)b);
+        atomicAdd(dbg_out + 1, n_iter);
+        atomicAdd(dbg_out + 2, (unsigned long long)(i1 - i0));
+    }
+    float* dstf = gparams + 2 * (lt.offset[l] + e0);
+    if (dbg & 2) return;  // timing experiment: no flush
+    const float4* img4 = reinterpret_cast<const float4*>(img);
+    if (ns == 1) {  // the wave owns these entries: plain read-add-write
+        float4* dst = reinterpret_cast<float4*>(dstf);
+        for (int i = lane; i < ne / 2; i += 64) {
+            float4 a = dst[i];
+            const float4 c = img4[i];
+            a.x += c.x;
+            a.y += c.y;
+            a.z += c.z;
+            a.w += c.w;
+            dst[i] = a;
+        }
+    } else {  // several slices: no-return atomics of the touched entries
+        const float* imgf = reinterpret_cast<const float*>(img);
+        for (int i = lane; i < 2 * ne; i += 64)
+            if (imgf[i] != 0.0f) atomicAdd(dstf + i, imgf[i]);
+    }
+}
+
+struct BwdLayout {
+    BwdPlan plan;
+    int total_parts;
+    int64_t counts, totals, part_start, slice_base, keys, vals, dbg, bytes;  // byte offsets in the workspace
+    int max_slices;  // reduce grid: total_parts + maxc / kDenseSlice bounds the slice count
+    bool scatter_ok; // the largest level's partition table fits the count/scatter LDS
+};
+
+int bwd_layout(int64_t N, int L, const int64_t* off, const int32_t* res, BwdLayout* o) {
+    if (L < 1 || L > kMaxLevels) return fail(AVR_E_ARG, "hashgrid: n_levels out of range (1..32)");
+    BwdLayout b{};
+    bool res_dense[kMaxLevels];
+    for (int l = 0; l < L; ++l) {  // dense level: the grid fits the table (grid_index's rule)
+        const double cells = res ? (double)res[l] * res[l] * res[l] : 1e300;
+        res_dense[l] = cells <= (double)(off[l + 1] - off[l]);
+    }
+    b.plan.pbase[0] = 0;
+    b.plan.max_parts = 0;
+    for (int l = 0; l < L; ++l) {
+        const int64_t size = off[l + 1] - off[l];
+        if (size <= 0 || size % 8) return fail(AVR_E_ARG, "hashgrid: level sizes must be positive multiples of 8");
+        const int64_t P = (size + kPartEntries - 1) / kPartEntries;
+        if (b.plan.pbase[l] + P > (1 << 24)) return fail(AVR_E_ARG, "hashgrid: tables too large");
+        b.plan.pbase[l + 1] = b.plan.pbase[l] + (int)P;
+        // a hashed level spreads N * 8 contributions over its partitions; one
+        // holding 1.5x its share has hot cells.  Dense levels are hot by nature
+        b.plan.slice_cap[l] = res_dense[l] ? kDenseSlice : kHashedSlice;
+        const double share = (double)N * 8.0 * (double)std::min<int64_t>(size, kPartEntries) / (double)size;
+        b.plan.hot_above[l] = res_dense[l] ? 0 : (int)std::min(1.5 * share + 64.0, 2.0e9);
+        b.plan.max_parts = std::max(b.plan.max_parts, (int)P);
+    }
+    const int64_t nchunks = (N + kChunkPts - 1) / kChunkPts;
+    const int64_t maxc = N * L * 8;
+    if (maxc >= (int64_t(1) << 31) || nchunks > 65535)
+        return fail(AVR_E_ARG, "hashgrid: too many points for the partitioned backward");
+    b.plan.nchunks = (int)std::max<int64_t>(nchunks, 1);
+    b.total_parts = b.plan.pbase[L];
+    auto al = [](int64_t v) { return (v + 255) & ~(int64_t)255; };
+    int64_t o0 = 0;
+    b.counts = o0;
+    o0 += al((int64_t)b.total_parts * b.plan.nchunks * 4);
+    b.totals = o0;
+    o0 += al((int64_t)b.total_parts * 4);
+    b.part_start = o0;
+    o0 += al((int64_t)(b.total_parts + 1) * 4);
+    b.slice_base = o0;
+    o0 += al((int64_t)(b.total_parts + 1) * 4);
+    b.max_slices = b.total_parts + (int)(maxc / kDenseSlice) + 1;
+    b.scatter_ok = b.plan.max_parts <= kMaxScatterParts;
+    b.keys = o0;
+    o0 += al(maxc * 4);
+    b.vals = o0;
+    o0 += al(maxc * 8);
+    b.dbg = o0;  // 3 counters of the reduce pass's diagnostics (AVR_HG_BWD_DBG & 4)
+    o0 += 256;
+    b.bytes = o0;
+    *o = b;
     return 0;
 }
 
@@ -447,14 +918,11 @@ extern "C" int avr_hashgrid_bwd(int64_t N, int32_t n_levels, const float* x, con
     if (N == 0) return 0;
     LevelTable lt;
     if (int e = make_table(n_levels, level_offset, level_scale, level_res, &lt)) return e;
-    const dim3 grid((unsigned)((N + 15) / 16), (unsigned)n_levels);  // 16 lanes per point
     hipStream_t st = as_stream(stream);
     if (grad_dtype == AVR_DTYPE_F32)
-        hipLaunchKernelGGL(hashgrid_bwd_kernel<float>, grid, dim3(256), 0, st, N, (int)n_levels, x,
-                           (const float*)grad_out, lt, grad_params);
+        launch_bwd<float>(st, N, (int)n_levels, x, (const float*)grad_out, lt, grad_params);
     else if (grad_dtype == AVR_DTYPE_F16)
-        hipLaunchKernelGGL(hashgrid_bwd_kernel<__half>, grid, dim3(256), 0, st, N, (int)n_levels,
-                           x, (const __half*)grad_out, lt, grad_params);
+        launch_bwd<__half>(st, N, (int)n_levels, x, (const __half*)grad_out, lt, grad_params);
     else
         return fail(AVR_E_ARG, "avr_hashgrid_bwd: unknown grad dtype");
     return check_launch("avr_hashgrid_bwd");
@@ -615,4 +1083,86 @@ extern "C" int avr_ray_pose_bias(int32_t B, int32_t R, int32_t S, const float* v
     else
         return fail(AVR_E_ARG, "avr_ray_pose_bias: unknown param dtype");
     return check_launch("avr_ray_pose_bias");
+}
+
+// Below this many points the atomic kernel is cheaper than the five
+// partitioned launches (the per-ray and per-pose grids of the training step)
+constexpr int64_t kPartitionedMinPoints = 16384;
+
+extern "C" int avr_hashgrid_bwd_workspace(int64_t N, int32_t n_levels, const int64_t* level_offset,
+                                          int64_t* bytes) {
+    AVR_REQUIRE(N >= 0 && level_offset && bytes, "avr_hashgrid_bwd_workspace: bad args");
+    if (N < kPartitionedMinPoints) {
+        *bytes = 256;
+        return 0;
+    }
+    BwdLayout b;
+    if (int e = bwd_layout(N, n_levels, level_offset, nullptr, &b)) return e;
+    *bytes = b.bytes;
+    return 0;
+}
+
+extern "C" int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const float* x, const void* grad_out,
+                                            int32_t grad_dtype, const int64_t* level_offset,
+                                            const float* level_scale, const int32_t* level_res,
+                                            float* grad_params, void* workspace, int64_t workspace_bytes,
+                                            void* stream) {
+    AVR_REQUIRE(N >= 0 && x && grad_out && level_offset && level_scale && level_res && grad_params && workspace,
+                "avr_hashgrid_bwd_partitioned: bad args");
+    AVR_REQUIRE(reinterpret_cast<uintptr_t>(grad_params) % 16 == 0 && reinterpret_cast<uintptr_t>(workspace) % 256 == 0,
+                "avr_hashgrid_bwd_partitioned: grad_params must be 16-byte, workspace 256-byte aligned");
+    AVR_REQUIRE(grad_dtype == AVR_DTYPE_F32 || grad_dtype == AVR_DTYPE_F16,
+                "avr_hashgrid_bwd_partitioned: unknown grad dtype");
+    if (N == 0) return 0;
+    LevelTable lt;
+    if (int e = make_table(n_levels, level_offset, level_scale, level_res, &lt)) return e;
+    hipStream_t st = as_stream(stream);
+    const int L = n_levels;
+    if (N < kPartitionedMinPoints) {  // few points: the atomic kernel (same += result)
+        if (grad_dtype == AVR_DTYPE_F32)
+            launch_bwd<float>(st, N, L, x, (const float*)grad_out, lt, grad_params);
+        else
+            launch_bwd<__half>(st, N, L, x, (const __half*)grad_out, lt, grad_params);
+        return check_launch("avr_hashgrid_bwd_partitioned");
+    }
+    BwdLayout b;
+    if (int e = bwd_layout(N, n_levels, level_offset, level_res, &b)) return e;
+    AVR_REQUIRE(workspace_bytes >= b.bytes, "avr_hashgrid_bwd_partitioned: workspace too small");
+    char* ws = static_cast<char*>(workspace);
+    int* counts = reinterpret_cast<int*>(ws + b.counts);
+    int* totals = reinterpret_cast<int*>(ws + b.totals);
+    uint32_t* keys = reinterpret_cast<uint32_t*>(ws + b.keys);
+    float2* vals = reinterpret_cast<float2*>(ws + b.vals);
+    const dim3 grid((unsigned)b.plan.nchunks, (unsigned)L);
+    const size_t lds_count = (size_t)b.plan.max_parts * 4, lds_scat = (size_t)b.plan.max_parts * 8;
+    if (!b.scatter_ok) {  // > 2^22 entries in a level: the atomic kernel (same += result)
+        if (grad_dtype == AVR_DTYPE_F32)
+            launch_bwd<float>(st, N, L, x, (const float*)grad_out, lt, grad_params);
+        else
+            launch_bwd<__half>(st, N, L, x, (const __half*)grad_out, lt, grad_params);
+        return check_launch("avr_hashgrid_bwd_partitioned");
+    }
+    if (grad_dtype == AVR_DTYPE_F32)
+        hipLaunchKernelGGL(hg_bwd_count_kernel<float>, grid, dim3(256), lds_count, st, N, L, x,
+                           (const float*)grad_out, lt, b.plan, counts);
+    else
+        hipLaunchKernelGGL(hg_bwd_count_kernel<__half>, grid, dim3(256), lds_count, st, N, L, x,
+                           (const __half*)grad_out, lt, b.plan, counts);
+    int* part_start = reinterpret_cast<int*>(ws + b.part_start);
+    int* slice_base = reinterpret_cast<int*>(ws + b.slice_base);
+    hipLaunchKernelGGL(hg_bwd_scan_kernel, dim3((unsigned)((b.total_parts + 15) / 16)), dim3(1024), 0, st,
+                       b.total_parts, b.plan.nchunks, counts, totals);
+    hipLaunchKernelGGL(hg_bwd_plan_kernel, dim3(1), dim3(1024), 0, st, b.total_parts, b.plan, totals, part_start,
+                       slice_base);
+    if (grad_dtype == AVR_DTYPE_F32)
+        hipLaunchKernelGGL(hg_bwd_scatter_kernel<float>, grid, dim3(256), lds_scat, st, N, L, x,
+                           (const float*)grad_out, lt, b.plan, counts, part_start, keys, vals);
+    else
+        hipLaunchKernelGGL(hg_bwd_scatter_kernel<__half>, grid, dim3(256), lds_scat, st, N, L, x,
+                           (const __half*)grad_out, lt, b.plan, counts, part_start, keys, vals);
+    hipLaunchKernelGGL(hg_bwd_reduce_kernel, dim3((unsigned)((b.max_slices + kReduceWaves - 1) / kReduceWaves)),
+                       dim3(64 * kReduceWaves), 0, st, L, lt, b.plan, b.total_parts, totals, part_start, slice_base,
+                       keys, vals, grad_params, getenv("AVR_HG_BWD_DBG") ? atoi(getenv("AVR_HG_BWD_DBG")) : 0,
+                       reinterpret_cast<unsigned long long*>(ws + b.dbg));
+    return check_launch("avr_hashgrid_bwd_partitioned");
 }

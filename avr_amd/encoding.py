@@ -19,7 +19,9 @@ initialised U(-1e-4, 1e-4).
 """
 from __future__ import annotations
 
+import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -80,9 +82,19 @@ class _HashGridFn(torch.autograd.Function):
             g = g.float()
         gp = torch.zeros(enc.n_params, dtype=torch.float32, device=x.device)
         st = torch.cuda.current_stream(x.device).cuda_stream
-        _lib.call("avr_hashgrid_bwd", x.size(0), enc.n_levels, x.data_ptr(), g.data_ptr(),
-                  _code(g.dtype), enc._off.ctypes.data, enc._scale.ctypes.data,
-                  enc._res.ctypes.data, gp.data_ptr(), st)
+        N = x.size(0)
+        if os.environ.get("AVR_HASHGRID_BWD", "partitioned") == "atomic":
+            _lib.call("avr_hashgrid_bwd", N, enc.n_levels, x.data_ptr(), g.data_ptr(),
+                      _code(g.dtype), enc._off.ctypes.data, enc._scale.ctypes.data,
+                      enc._res.ctypes.data, gp.data_ptr(), st)
+            return None, gp, None, None
+        # partitioned (no global atomics): workspace from the caching allocator
+        nbytes = ctypes.c_int64()
+        _lib.call("avr_hashgrid_bwd_workspace", N, enc.n_levels, enc._off.ctypes.data, ctypes.byref(nbytes))
+        ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=x.device)
+        _lib.call("avr_hashgrid_bwd_partitioned", N, enc.n_levels, x.data_ptr(), g.data_ptr(),
+                  _code(g.dtype), enc._off.ctypes.data, enc._scale.ctypes.data, enc._res.ctypes.data,
+                  gp.data_ptr(), ws.data_ptr(), nbytes.value, st)
         return None, gp, None, None
 
 

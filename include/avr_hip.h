@@ -279,6 +279,19 @@ int avr_hashgrid_bwd(int64_t N, int32_t n_levels, const float* x, const void* gr
                      int32_t grad_dtype, const int64_t* level_offset, const float* level_scale,
                      const int32_t* level_res, float* grad_params, void* stream);
 
+/* The same gradient without global atomics (what training uses): the merged
+ * corner contributions are counted and scattered by table partition (8192
+ * entries of one level) into `workspace`, then one block per partition sums
+ * them in LDS and adds the partition to grad_params (fp32, += : zero it first
+ * for a plain gradient).  grad_params 16-byte aligned; workspace 256-byte
+ * aligned, of avr_hashgrid_bwd_workspace bytes (12 B per possible
+ * contribution, N * n_levels * 8).  Level sizes must be multiples of 8. */
+int avr_hashgrid_bwd_workspace(int64_t N, int32_t n_levels, const int64_t* level_offset, int64_t* bytes);
+int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const float* x, const void* grad_out,
+                                 int32_t grad_dtype, const int64_t* level_offset, const float* level_scale,
+                                 const int32_t* level_res, float* grad_params, void* workspace,
+                                 int64_t workspace_bytes, void* stream);
+
 /* ---- a6: weight gradient of the networks' bias-free linear layers -------
  * grad_w[M][K] (fp32) = sum_n grad_y[n][M] * x[n][K], both operands bf16,
  * row-major, 16-byte aligned, M and K multiples of 8.  Replaces the wgrad

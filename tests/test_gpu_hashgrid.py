@@ -48,7 +48,12 @@ def test_forward_matches_restatement(dtype, n):
         np.testing.assert_allclose(out, ref, rtol=2e-6, atol=2e-6)
 
 
-def test_backward_matches_restatement():
+BWD_IMPLS = ["partitioned", "atomic"]  # avr_hashgrid_bwd_partitioned (training's) and avr_hashgrid_bwd
+
+
+@pytest.mark.parametrize("impl", BWD_IMPLS)
+def test_backward_matches_restatement(impl, monkeypatch):
+    monkeypatch.setenv("AVR_HASHGRID_BWD", impl)
     cfg = dict(CFG, n_levels=8, log2_hashmap_size=14)
     enc = HashGridEncoding(3, cfg, dtype=torch.float32, seed=6).to(DEV)
     x = _points(2048, 1)
@@ -115,9 +120,10 @@ def _ray_points(n_rays, n_samples, seed, step=1.3e-3):
     return np.clip(o + d * t, 0, 1).reshape(-1, 3).astype(np.float32)
 
 
+@pytest.mark.parametrize("impl", BWD_IMPLS)
 @pytest.mark.parametrize("log2", [18, 20])
 @pytest.mark.parametrize("gdtype", [torch.float32, torch.float16])
-def test_backward_reference_size_tables(log2, gdtype):
+def test_backward_reference_size_tables(log2, gdtype, impl, monkeypatch):
     """The backward where it runs: 20 levels at the reference's table sizes
     (2^18 everywhere, 2^20 for MeshRIR's direction grid,
     config_files/avr_meshrir.yml:56-61), ray-ordered points (equal
@@ -125,10 +131,14 @@ def test_backward_reference_size_tables(log2, gdtype):
     atomics both exercised) plus random ones (hash collisions on the fine
     levels), with fp32 and fp16 upstream gradients (an fp16 encoding's
     grad_out is fp16), against the float64 scatter-add of the restatement.
-    fp32 atomics in any order: 1e-5 relative to the gradient's scale."""
+    fp32 sums in any order: 1e-5 relative to the gradient's scale.  The
+    first samples of 300 rays sit on one point (every ray of a pose starts at
+    the listener): hundreds of adds into the same entries."""
+    monkeypatch.setenv("AVR_HASHGRID_BWD", impl)
     cfg = dict(CFG, log2_hashmap_size=log2)
     enc = HashGridEncoding(3, cfg, dtype=gdtype, seed=9).to(DEV)
-    x = np.concatenate([_ray_points(48, 256, 4), _points(8192, 5)])
+    x = np.concatenate([_ray_points(48, 256, 4), _points(8192, 5), _ray_points(300, 16, 7, step=2e-3)[:1].repeat(300, 0),
+                        _points(37, 8)])
     xt = torch.from_numpy(x).to(DEV)
     out = enc(xt)
     assert out.dtype == gdtype
@@ -145,3 +155,34 @@ def test_backward_reference_size_tables(log2, gdtype):
     assert err < 1e-5, err
     # every touched entry is touched in both, and no other
     np.testing.assert_array_equal(got != 0, ref != 0)
+
+
+@pytest.mark.parametrize("n", [1, 3000, 16384, 16897, 40000])
+def test_partitioned_backward_accumulates(n):
+    """avr_hashgrid_bwd_partitioned adds into grad_params (+=) and equals the
+    atomic kernel: one point and 3000 (below 16384 points it runs the atomic
+    kernel itself), and the partitioned passes at 16384, a ragged last chunk
+    (16897 = 33 x 512 + 1) and 40000 random points."""
+    import ctypes
+
+    from avr_amd import _lib
+    from avr_amd.encoding import _code
+
+    enc = HashGridEncoding(3, dict(CFG, log2_hashmap_size=16), dtype=torch.float16, seed=10).to(DEV)
+    x = torch.from_numpy(_points(max(n, 8), 11)[-n:].copy()).to(DEV)
+    L = enc.n_levels
+    g = torch.randn(n, 2 * L, device=DEV).half()
+    st = torch.cuda.current_stream(DEV).cuda_stream
+    meta = (enc._off.ctypes.data, enc._scale.ctypes.data, enc._res.ctypes.data)
+    a = torch.zeros(enc.n_params, device=DEV)
+    _lib.call("avr_hashgrid_bwd", n, L, x.data_ptr(), g.data_ptr(), _code(g.dtype), *meta, a.data_ptr(), st)
+    nb = ctypes.c_int64()
+    _lib.call("avr_hashgrid_bwd_workspace", n, L, enc._off.ctypes.data, ctypes.byref(nb))
+    ws = torch.empty(nb.value, dtype=torch.uint8, device=DEV)
+    base = torch.randn(enc.n_params, device=DEV)
+    b = base.clone()
+    _lib.call("avr_hashgrid_bwd_partitioned", n, L, x.data_ptr(), g.data_ptr(), _code(g.dtype), *meta,
+              b.data_ptr(), ws.data_ptr(), nb.value, st)
+    torch.cuda.synchronize()
+    scale = float(a.abs().max())
+    assert float((b - base - a).abs().max()) <= 1e-5 * scale + 1e-6
