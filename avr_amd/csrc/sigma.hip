@@ -420,7 +420,7 @@ void sigma_meshrir_kernel(Args a) {
 // (32 samples x 64 columns, 4 KB) goes through a per-wave LDS area (16-byte
 // chunks XOR-swizzled by row: conflict-free) and leaves as 4 instructions
 // of 8 rows x 128 contiguous bytes (full cache lines).
-template <typename E, int NT, bool STORE = true>
+template <typename E, int NT, bool STORE = true, bool BIAS = true>
 __device__ __forceinline__ void store_h1(const Args& a, const f32x16 (&acc)[NT][4], int64_t n0, int lane, int c,
                                          char* tr) {
     const int h = lane >> 5, r = lane & 31;
@@ -436,7 +436,8 @@ __device__ __forceinline__ void store_h1(const Args& a, const f32x16 (&acc)[NT][
                 const int ot = 2 * p + j;
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const f32x4 b = *reinterpret_cast<const f32x4*>(brow + 32 * ot + 8 * g + 4 * h);
+                    const f32x4 b = BIAS ? *reinterpret_cast<const f32x4*>(brow + 32 * ot + 8 * g + 4 * h)
+                                         : f32x4{0.f, 0.f, 0.f, 0.f};
                     const f32x16& v = acc[nt][ot];
                     const uint32_t w0 = pack2<E>(relu(v[4 * g] + b[0]), relu(v[4 * g + 1] + b[1]));
                     const uint32_t w1 = pack2<E>(relu(v[4 * g + 2] + b[2]), relu(v[4 * g + 3] + b[3]));
@@ -521,7 +522,7 @@ void sigma_meshrir_h1_kernel(Args a) {
     for (int c = 0; c < 4; ++c) {
         f32x16 acc[NT][4];
         dense<E, NT, 8, 4, 4>(st, lane, xs, acc);
-        store_h1<E, NT, !(DBG & 4)>(a, acc, n0, lane, c, lds + 2 * kChunk + wave * 4096);
+        store_h1<E, NT, !(DBG & 4), !(DBG & 8)>(a, acc, n0, lane, c, lds + 2 * kChunk + wave * 4096);
     }
 }
 
@@ -671,6 +672,10 @@ int dispatch(const avr_sigma_desc* d, Args& a, bool h1, bool two, hipStream_t st
         // 2, 3: the same with plain stores (130 us)
         a.nt_store = d->tile_cfg < 2;
         if (d->tile_cfg == 1 || d->tile_cfg == 3) return launch_meshrir_h1<E, 1, 8, 1>(a, st);
+        // 4, 5: 64 samples per wave (each weight fragment feeds two MFMAs),
+        // 1 or 2 waves per SIMD (experiments)
+        if (d->tile_cfg == 4) return launch_meshrir_h1<E, 2, 4, 1>(a, st);
+        if (d->tile_cfg == 5) return launch_meshrir_h1<E, 2, 4, 2>(a, st);
         // timing experiments (results are garbage): no barrier / no weight
         // staging / no h1 stores (bf16 builds only)
         if constexpr (std::is_same<E, __bf16>::value) {
@@ -678,6 +683,7 @@ int dispatch(const avr_sigma_desc* d, Args& a, bool h1, bool two, hipStream_t st
             if (d->tile_cfg == 17) return launch_meshrir_h1<E, 1, 4, 2, 2>(a, st);
             if (d->tile_cfg == 18) return launch_meshrir_h1<E, 1, 4, 2, 4>(a, st);
             if (d->tile_cfg == 19) return launch_meshrir_h1<E, 1, 4, 2, 7>(a, st);
+            if (d->tile_cfg == 20) return launch_meshrir_h1<E, 1, 4, 2, 8>(a, st);  // no bias loads
         }
         return launch_meshrir_h1<E, 1, 4, 2>(a, st);
     }

@@ -23,11 +23,12 @@ def main():
     ap.add_argument("--n", type=int, default=262144)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--cfgs", default="0,1,2")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     v = a.variant
     ws = [torch.randn(M, K, device=dev) * np.sqrt(2.0 / K) for M, K, _, _ in sigma.SCHEDULE[v]]
-    packed = sigma.pack_layers(v, ws)
+    packed = sigma.pack_layers(v, ws, torch.float16 if a.dtype == "fp16" else torch.bfloat16)
     N, S, RS = a.n, 256, 262144
     B = -(-N // RS)
     bias = None
@@ -60,7 +61,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / a.iters
-        print(json.dumps({"variant": v, "tile_cfg": cfg, "n": N, "us": us,
+        print(json.dumps({"variant": v, "dtype": a.dtype, "tile_cfg": cfg, "n": N, "us": us,
                           "tflops": flops / (us * 1e-6) / 1e12}))
 
 
