@@ -31,6 +31,8 @@
 // [B][S][T] (n_split = 1 for avr_dft_phase_fwd), zero at t >= T-1-shift_s.
 #include "common.h"
 
+#include <algorithm>
+
 using namespace avr;
 
 namespace {
@@ -423,7 +425,13 @@ __device__ __forceinline__ void dma_row16(const void* g, uint32_t lds) {
                  : "memory", "m0");
 }
 
-template <typename E, int TR, int NBUF, int DBG = 0>
+// PERSIST: one workgroup per CU for the whole launch instead of one per
+// (column, t-block) item: each workgroup keeps one t-block (its W fragments
+// are loaded once, not once per item) and walks columns of its XCD's
+// contiguous column range with a stride; the t-blocks of a column run on one
+// XCD (its h rows shared through that L2).  Removes the per-item W prologue
+// and the workgroup turnover of the one-item form.
+template <typename E, int TR, int NBUF, int DBG = 0, bool PERSIST = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void head_exact_dma_kernel(
     avr_render_params pp, int B, int R, int K, const E* __restrict__ h, const E* __restrict__ W,
     const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
@@ -439,33 +447,34 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     float* wl = reinterpret_cast<float*>(pl + (R + TR - 1) / TR * TR);
 
     const int T = pp.T, S = pp.n_samples;
-    const int64_t total = (int64_t)B * S * ntb;
-    const int64_t L = (int64_t)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-    if (L >= total) return;
-    const int64_t col = L / ntb;
-    const int tb = (int)(L % ntb);
-    const int s = (int)(col % S), b = (int)(col / S);
-    const int lim = tail_limit(pp, s);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int half = lane >> 5, j = lane & 31;
+    const int64_t ncol = (int64_t)B * S;
+    // this workgroup's items: (first column, column stride, column end, t-block)
+    int64_t c_first, c_step, c_end;
+    int tb;
+    if constexpr (PERSIST) {
+        // per_xcd = workgroups per XCD (a multiple of ntb); XCD x owns columns
+        // [x * cpx, (x + 1) * cpx)
+        const int x = blockIdx.x & 7, m = blockIdx.x >> 3;
+        const int nq = per_xcd / ntb;
+        const int64_t cpx = (ncol + 7) / 8;
+        tb = m % ntb;
+        c_first = (int64_t)x * cpx + m / ntb;
+        c_step = nq;
+        c_end = min(ncol, (int64_t)(x + 1) * cpx);
+    } else {
+        const int64_t total = ncol * ntb;
+        const int64_t L = (int64_t)(blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+        if (L >= total) return;
+        c_first = L / ntb;
+        c_step = 1;
+        c_end = c_first + 1;
+        tb = (int)(L % ntb);
+    }
     const int t0 = tb * TB + wave * 32;
     const int t = t0 + j;
-    float* zcol = z + col * T;
-    const int tlast = min(tb * TB + TB, lim) - 1;
-    if (tlast < tb * TB) {
-        for (int i = threadIdx.x; i < TB; i += NT)
-            if (tb * TB + i < T) zcol[tb * TB + i] = 0.0f;
-        return;
-    }
-    const int* ccol = cnt + col * T;
-    const int nblk = ccol[tlast];
-    const int cnt_t = (t < lim) ? ccol[t] : 0;
-    const int cwave = (t0 < lim) ? ccol[min(t0 + 31, lim - 1)] : 0;
-    // rays live at EVERY t of this wave's tile (cnt is nondecreasing in t):
-    // a 32-ray sub-tile below it needs no mask in its epilogue
-    const int cfull = __builtin_amdgcn_readfirstlane((t0 + 31 < lim) ? ccol[t0] : 0);
-    const int ntile = (nblk + TR - 1) / TR;
 
     frag8 wf[KS];
     {
@@ -478,152 +487,171 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(wf[ks]));
     }
-    for (int p = threadIdx.x; p < ntile * TR; p += NT) {
-        const bool in = p < nblk;
-        pl[p] = perm[col * R + (in ? p : nblk - 1)];
-        wl[p] = in ? ws[col * R + p] : 0.0f;
-    }
-    __syncthreads();
     const int64_t hstride = (int64_t)S * K;
-    const E* hcol = h + ((int64_t)b * R * S + s) * K + 8 * lane;
 
-    // rows wave*RPW .. +RPW-1 of tile `tile` into buffer tile % NBUF; the
-    // wave's RPW ray indices come from LDS in one vector read
-    auto issue = [&](int tile) {
-        const int p0 = tile * TR + wave * RPW;
-        char* a = abuf + (tile % NBUF) * TR * ROWB + wave * RPW * ROWB;
-        int ray[RPW];
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) ray[r] = pl[p0 + r];
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            const int rr = __builtin_amdgcn_readfirstlane(ray[r]);
-            const int64_t off = (DBG & 2) ? (int64_t)(r & 7) * hstride : (int64_t)rr * hstride;
-            dma_row16(hcol + off, (uint32_t)(uintptr_t)(a + r * ROWB));
+    for (int64_t col = c_first; col < c_end; col += c_step) {
+        if (PERSIST && col != c_first) __syncthreads();  // the previous column's LDS reads are done
+        const int s = (int)(col % S), b = (int)(col / S);
+        const int lim = tail_limit(pp, s);
+        float* zcol = z + col * T;
+        const int tlast = min(tb * TB + TB, lim) - 1;
+        if (tlast < tb * TB) {
+            for (int i = threadIdx.x; i < TB; i += NT)
+                if (tb * TB + i < T) zcol[tb * TB + i] = 0.0f;
+            continue;
         }
-    };
+        const int* ccol = cnt + col * T;
+        const int nblk = ccol[tlast];
+        const int cnt_t = (t < lim) ? ccol[t] : 0;
+        const int cwave = (t0 < lim) ? ccol[min(t0 + 31, lim - 1)] : 0;
+        // rays live at EVERY t of this wave's tile (cnt is nondecreasing in t):
+        // a 32-ray sub-tile below it needs no mask in its epilogue
+        const int cfull = __builtin_amdgcn_readfirstlane((t0 + 31 < lim) ? ccol[t0] : 0);
+        const int ntile = (nblk + TR - 1) / TR;
+        for (int p = threadIdx.x; p < ntile * TR; p += NT) {
+            const bool in = p < nblk;
+            pl[p] = perm[col * R + (in ? p : nblk - 1)];
+            wl[p] = in ? ws[col * R + p] : 0.0f;
+        }
+        __syncthreads();
+        const E* hcol = h + ((int64_t)b * R * S + s) * K + 8 * lane;
 
-    float zl = 0.0f;
-    constexpr int kDepth = 8;  // A fragments read this many k-steps ahead of their MFMA
-    auto epilogue = [&](const f32x16& acc, int p0) {
-        if constexpr (DBG & 4) {  // no epilogue: keep the MFMA result alive only
-            zl += acc[0];
-            return;
-        }
-        if (p0 + 32 <= cfull) {  // every (ray, t) pair of the sub-tile is live
+        // rows wave*RPW .. +RPW-1 of tile `tile` into buffer tile % NBUF; the
+        // wave's RPW ray indices come from LDS in one vector read
+        auto issue = [&](int tile) {
+            const int p0 = tile * TR + wave * RPW;
+            char* a = abuf + (tile % NBUF) * TR * ROWB + wave * RPW * ROWB;
+            int ray[RPW];
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) ray[r] = pl[p0 + r];
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                const int rr = __builtin_amdgcn_readfirstlane(ray[r]);
+                const int64_t off = (DBG & 2) ? (int64_t)(r & 7) * hstride : (int64_t)rr * hstride;
+                dma_row16(hcol + off, (uint32_t)(uintptr_t)(a + r * ROWB));
+            }
+        };
+
+        float zl = 0.0f;
+        constexpr int kDepth = 8;  // A fragments read this many k-steps ahead of their MFMA
+        auto epilogue = [&](const f32x16& acc, int p0) {
+            if constexpr (DBG & 4) {  // no epilogue: keep the MFMA result alive only
+                zl += acc[0];
+                return;
+            }
+            if (p0 + 32 <= cfull) {  // every (ray, t) pair of the sub-tile is live
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float4 wv = *reinterpret_cast<const float4*>(wl + p0 + 8 * g + 4 * half);
+                    zl = fmaf(wv.x, round16<E>(acc[4 * g + 0]), zl);
+                    zl = fmaf(wv.y, round16<E>(acc[4 * g + 1]), zl);
+                    zl = fmaf(wv.z, round16<E>(acc[4 * g + 2]), zl);
+                    zl = fmaf(wv.w, round16<E>(acc[4 * g + 3]), zl);
+                }
+                return;
+            }
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const float4 wv = *reinterpret_cast<const float4*>(wl + p0 + 8 * g + 4 * half);
-                zl = fmaf(wv.x, round16<E>(acc[4 * g + 0]), zl);
-                zl = fmaf(wv.y, round16<E>(acc[4 * g + 1]), zl);
-                zl = fmaf(wv.z, round16<E>(acc[4 * g + 2]), zl);
-                zl = fmaf(wv.w, round16<E>(acc[4 * g + 3]), zl);
+                const float w4[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int p = p0 + e + 8 * g + 4 * half;
+                    const float wsel = (p < cnt_t) ? w4[e] : 0.0f;
+                    zl = fmaf(wsel, round16<E>(acc[4 * g + e]), zl);
+                }
             }
-            return;
-        }
+        };
+        // NQ consecutive 32-ray sub-tiles starting at row q0 of the tile in
+        // buffer `buf`: their MFMA chains back to back (the fragment reads of the
+        // next chain run under the previous one's MFMAs), then their epilogues
+        // in sub-tile order (the summation order of the other forms)
+        auto chains = [&](auto nq_tag, int buf, int q0, int p0) {
+            constexpr int NQ = decltype(nq_tag)::value;
+            const char* a = abuf + buf * TR * ROWB + (32 * q0 + j) * ROWB + 16 * half;
+            f32x16 acc[NQ];
+            if constexpr (DBG & 1) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const float4 wv = *reinterpret_cast<const float4*>(wl + p0 + 8 * g + 4 * half);
-            const float w4[4] = {wv.x, wv.y, wv.z, wv.w};
+                for (int q = 0; q < NQ; ++q) {
+                    const frag8 v = *reinterpret_cast<const frag8*>(a + q * 32 * ROWB);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int p = p0 + e + 8 * g + 4 * half;
-                const float wsel = (p < cnt_t) ? w4[e] : 0.0f;
-                zl = fmaf(wsel, round16<E>(acc[4 * g + e]), zl);
+                    for (int i = 0; i < 16; ++i) acc[q][i] = __uint_as_float(v[i & 3]);
+                }
+            } else {
+                constexpr int N = NQ * KS;  // k-steps of all chains, in order
+                auto frag_at = [&](int n) {
+                    return *reinterpret_cast<const frag8*>(a + (n / KS) * 32 * ROWB + 32 * (n % KS));
+                };
+                frag8 fr[kDepth];
+#pragma unroll
+                for (int i = 0; i < kDepth; ++i) fr[i] = frag_at(i);
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) acc[q] = f32x16{};
+#pragma unroll
+                for (int n = 0; n < N; ++n) {
+                    acc[n / KS] = mfma16<E>(fr[n % kDepth], wf[n % KS], acc[n / KS]);
+                    if (n + kDepth < N) fr[n % kDepth] = frag_at(n + kDepth);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x100, kDepth, 0);  // the first kDepth DS reads
+#pragma unroll
+                for (int n = 0; n < N; ++n) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+                    if (n + kDepth < N) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // then one DS read
+                }
             }
-        }
-    };
-    // NQ consecutive 32-ray sub-tiles starting at row q0 of the tile in
-    // buffer `buf`: their MFMA chains back to back (the fragment reads of the
-    // next chain run under the previous one's MFMAs), then their epilogues
-    // in sub-tile order (the summation order of the other forms)
-    auto chains = [&](auto nq_tag, int buf, int q0, int p0) {
-        constexpr int NQ = decltype(nq_tag)::value;
-        const char* a = abuf + buf * TR * ROWB + (32 * q0 + j) * ROWB + 16 * half;
-        f32x16 acc[NQ];
-        if constexpr (DBG & 1) {
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const frag8 v = *reinterpret_cast<const frag8*>(a + q * 32 * ROWB);
-#pragma unroll
-                for (int i = 0; i < 16; ++i) acc[q][i] = __uint_as_float(v[i & 3]);
+            for (int q = 0; q < NQ; ++q) epilogue(acc[q], p0 + 32 * q);
+        };
+        auto compute = [&](int it) {
+            const int p0 = it * TR, buf = it % NBUF;
+            if constexpr (TR == 64) {
+                if (p0 + 32 < cwave)
+                    chains(std::integral_constant<int, 2>{}, buf, 0, p0);
+                else if (p0 < cwave)
+                    chains(std::integral_constant<int, 1>{}, buf, 0, p0);
+            } else {
+                if (p0 < cwave) chains(std::integral_constant<int, 1>{}, buf, 0, p0);
             }
-        } else {
-            constexpr int N = NQ * KS;  // k-steps of all chains, in order
-            auto frag_at = [&](int n) {
-                return *reinterpret_cast<const frag8*>(a + (n / KS) * 32 * ROWB + 32 * (n % KS));
-            };
-            frag8 fr[kDepth];
-#pragma unroll
-            for (int i = 0; i < kDepth; ++i) fr[i] = frag_at(i);
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) acc[q] = f32x16{};
-#pragma unroll
-            for (int n = 0; n < N; ++n) {
-                acc[n / KS] = mfma16<E>(fr[n % kDepth], wf[n % KS], acc[n / KS]);
-                if (n + kDepth < N) fr[n % kDepth] = frag_at(n + kDepth);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x100, kDepth, 0);  // the first kDepth DS reads
-#pragma unroll
-            for (int n = 0; n < N; ++n) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
-                if (n + kDepth < N) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // then one DS read
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) epilogue(acc[q], p0 + 32 * q);
-    };
-    auto compute = [&](int it) {
-        const int p0 = it * TR, buf = it % NBUF;
-        if constexpr (TR == 64) {
-            if (p0 + 32 < cwave)
-                chains(std::integral_constant<int, 2>{}, buf, 0, p0);
-            else if (p0 < cwave)
-                chains(std::integral_constant<int, 1>{}, buf, 0, p0);
-        } else {
-            if (p0 < cwave) chains(std::integral_constant<int, 1>{}, buf, 0, p0);
-        }
-    };
-    // s_waitcnt vmcnt(n) (expcnt / lgkmcnt not waited on; gfx9 encoding)
+        };
+        // s_waitcnt vmcnt(n) (expcnt / lgkmcnt not waited on; gfx9 encoding)
 #define AVR_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 0xF) | (0x7 << 4) | (0xF << 8) | (((N) >> 4) << 14))
-    // this wave's DMAs still allowed in flight once the oldest tile landed:
-    // the RPW rows of each younger tile issued (n of them)
-    auto wait_vm = [](int n) {
-        switch (n) {  // the immediate must be a constant
-            case 0: AVR_VMCNT(0); break;
-            case 1: AVR_VMCNT(RPW); break;
-            case 2: AVR_VMCNT(2 * RPW); break;
-            default: AVR_VMCNT(0); break;
-        }
-    };
+        // this wave's DMAs still allowed in flight once the oldest tile landed:
+        // the RPW rows of each younger tile issued (n of them)
+        auto wait_vm = [](int n) {
+            switch (n) {  // the immediate must be a constant
+                case 0: AVR_VMCNT(0); break;
+                case 1: AVR_VMCNT(RPW); break;
+                case 2: AVR_VMCNT(2 * RPW); break;
+                default: AVR_VMCNT(0); break;
+            }
+        };
 #undef AVR_VMCNT
-    for (int i = 0; i < PD; ++i)
-        if (i < ntile) issue(i);
-    if (ntile > 0) {
-        wait_vm(min(PD, ntile) - 1);  // tile 0 landed (the younger ones may still fly)
-        __builtin_amdgcn_s_barrier();
-    }
-    if constexpr (DBG & 8) {  // no DMA, no barrier: every tile computed from the tile-0 buffer
-        for (int it = 0; it < ((DBG & 16) ? 0 : ntile); ++it) {  // DBG & 16: prologue and output only
-            const int p0 = it * TR;
-            if (p0 < cwave) chains(std::integral_constant<int, 1>{}, 0, 0, p0);
+        for (int i = 0; i < PD; ++i)
+            if (i < ntile) issue(i);
+        if (ntile > 0) {
+            wait_vm(min(PD, ntile) - 1);  // tile 0 landed (the younger ones may still fly)
+            __builtin_amdgcn_s_barrier();
+        }
+        if constexpr (DBG & 8) {  // no DMA, no barrier: every tile computed from the tile-0 buffer
+            for (int it = 0; it < ((DBG & 16) ? 0 : ntile); ++it) {  // DBG & 16: prologue and output only
+                const int p0 = it * TR;
+                if (p0 < cwave) chains(std::integral_constant<int, 1>{}, 0, 0, p0);
+            }
+        } else {
+            for (int it = 0; it < ntile; ++it) {
+                // into the buffer tile it-1 used: every wave left it at the last barrier
+                if (it + PD < ntile) issue(it + PD);
+                compute(it);
+                if (it + 1 < ntile) {
+                    wait_vm(min(PD, ntile - 1 - it) - 1);  // tile it+1's rows from this wave have landed
+                    __builtin_amdgcn_s_waitcnt(0xC07F);     // and every LDS read of tile it is done
+                    __builtin_amdgcn_s_barrier();
+                }
+            }
         }
         const float other = __shfl_xor(zl, 32, 64);
         if (half == 0 && t < T) zcol[t] = (t < lim) ? zl + other : 0.0f;
-        return;
     }
-    for (int it = 0; it < ntile; ++it) {
-        // into the buffer tile it-1 used: every wave left it at the last barrier
-        if (it + PD < ntile) issue(it + PD);
-        compute(it);
-        if (it + 1 < ntile) {
-            wait_vm(min(PD, ntile - 1 - it) - 1);  // tile it+1's rows from this wave have landed
-            __builtin_amdgcn_s_waitcnt(0xC07F);     // and every LDS read of tile it is done
-            __builtin_amdgcn_s_barrier();
-        }
-    }
-    const float other = __shfl_xor(zl, 32, 64);
-    if (half == 0 && t < T) zcol[t] = (t < lim) ? zl + other : 0.0f;
 }
 
 int exact_shape(const avr_render_params& p, int K, int* KS, int* waves) {
@@ -632,12 +660,13 @@ int exact_shape(const avr_render_params& p, int K, int* KS, int* waves) {
     *KS = ks <= 8 ? 8 : (ks <= 16 ? 16 : 32);
     // 0: head_exact_pipe_kernel (one wave per SIMD, 4 waves); 8 / 4: the
     // two-waves-per-SIMD head_exact_fwd_kernel (experiments)
-    // default: the LDS-DMA form with 64-ray tiles for K = 512 (the reference
-    // networks' width), the register-staged form otherwise
-    int w = K == 512 ? 17 : 8;
+    // default: the persistent LDS-DMA form with 64-ray tiles for K = 512 (the
+    // reference networks' width; 243 us against 265 for the one-item form at
+    // config 2 fp16), the register-staged form otherwise
+    int w = K == 512 ? 19 : 8;
     if (const char* e = getenv("AVR_HEAD_EXACT_WAVES")) {
         const int v = atoi(e);
-        w = (v == 4 || v == 8 || (v >= 16 && v <= 18)) ? v : 0;  // 16-18: the LDS-DMA forms (K = 512)
+        w = (v == 4 || v == 8 || (v >= 16 && v <= 19)) ? v : 0;  // 16-19: the LDS-DMA forms (K = 512)
     }
     if (w >= 16 && K != 512) w = 8;
     *waves = w;
@@ -682,14 +711,36 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
     using I32 = std::integral_constant<int, 32>;
     using I8 = std::integral_constant<int, 8>;
     using I4 = std::integral_constant<int, 4>;
-    if (waves >= 16 && KS == 32 && K == 512) {  // LDS-DMA forms (16: 32-ray tiles x 3 buffers, 17: 64 x 2, 18: 32 x 4)
-        const int TRv = waves == 17 ? 64 : 32, NB = waves == 16 ? 3 : (waves == 17 ? 2 : 4);
+    if (waves >= 16 && KS == 32 && K == 512) {  // LDS-DMA forms (16: 32-ray tiles x 3 buffers, 17: 64 x 2, 18: 32 x 4,
+                                                // 19: 64 x 2 persistent)
+        const int TRv = (waves == 17 || waves == 19) ? 64 : 32, NB = waves == 16 ? 3 : (waves == 18 ? 4 : 2);
         const size_t lds = (size_t)NB * TRv * a_row_bytes(32) + 8 * (size_t)((R + TRv - 1) / TRv * TRv);
+        // persistent: per XCD, as many workgroups as CUs hold (one each at
+        // this LDS size), rounded down to whole t-block sets
+        int wg_per_xcd = per_xcd;
+        if (waves == 19) {
+            int cus = 256;
+            int dev = 0;
+            if (hipGetDevice(&dev) == hipSuccess)
+                (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            const int64_t ncol = (int64_t)B * S;
+            const int64_t want = ((ncol + 7) / 8) * ntb;  // one workgroup per item of an XCD
+            wg_per_xcd = (int)std::min<int64_t>(want, std::max(1, cus / 8));
+            wg_per_xcd = std::max(ntb, wg_per_xcd / ntb * ntb);
+        }
+        const dim3 grid_dma((unsigned)(8 * (waves == 19 ? wg_per_xcd : per_xcd)));
         auto go_dma = [&](auto kern, auto hp) {
             allow_lds(kern, lds);
-            hipLaunchKernelGGL(kern, grid, dim3(512), lds, st, *p, (int)B, R, (int)K, hp, (decltype(hp))W, perm, ws,
-                               cnt, z, ntb, per_xcd);
+            hipLaunchKernelGGL(kern, grid_dma, dim3(512), lds, st, *p, (int)B, R, (int)K, hp, (decltype(hp))W, perm,
+                               ws, cnt, z, ntb, waves == 19 ? wg_per_xcd : per_xcd);
         };
+        if (waves == 19) {
+            if (dtype == AVR_DTYPE_F16)
+                go_dma(head_exact_dma_kernel<__half, 64, 2, 0, true>, (const __half*)h);
+            else
+                go_dma(head_exact_dma_kernel<__hip_bfloat16, 64, 2, 0, true>, (const __hip_bfloat16*)h);
+            return check_launch("avr_head_fwd_exact");
+        }
 #define AVR_HD(TRV, NBV)                                                                              \
         if (dtype == AVR_DTYPE_F16) {                                                                 \
             if (dbg == 1) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 1>, (const __half*)h);        \
