@@ -1346,9 +1346,12 @@ extern "C" int avr_render_core_fwd(const avr_render_params* p, int32_t B, const 
     if (int e = avr_dft_phase_fwd(p, B, part, L.n_split, tab->pl_table, tab->shift, tab->phase,
                                   tab->twiddle, L.k_split, spart, stream))
         return e;
-    if (ir) {  // finalize + irfft in one launch
+    if (ir) {
         AVR_REQUIRE(tab->ir_twiddle, "avr_render_core_fwd: ir requested without ir_twiddle");
-        return avr_spectrum_ir(B, L.P, p->T / 2 + 1, spart, tab->ir_twiddle, out, ir, stream);
+        const char* e = getenv("AVR_SPECTRUM_IR");  // 1: finalize + irfft in one launch (experiment)
+        if (e && e[0] == '1') return avr_spectrum_ir(B, L.P, p->T / 2 + 1, spart, tab->ir_twiddle, out, ir, stream);
+        if (int e2 = avr_spectrum_finalize(B, L.P, p->T / 2 + 1, spart, out, stream)) return e2;
+        return avr_irfft(B, p->T / 2 + 1, out, tab->ir_twiddle, ir, stream);
     }
     return avr_spectrum_finalize(B, L.P, p->T / 2 + 1, spart, out, stream);
 }
