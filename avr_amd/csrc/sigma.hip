@@ -160,25 +160,57 @@ __device__ __forceinline__ frag8 load8(const Src& s, int64_t row, int width, int
 // then the loads of chunk c+2 are issued.
 // DBG (timing experiments only, tools/probe_sigma.py tile_cfg >= 16): bit 0
 // drops the barrier, bit 1 the staging loads/writes (results are garbage).
+// Bits 32 and 64 are not experiments but staging modes (the h1 kernel's
+// default uses both, tile_cfg 0; 2-4% faster than register staging).
+// DMA (DBG bit 32): the chunks travel global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, issued as inline asm: the compiler does not
+// track it, so it neither waits on it inside the MFMA chains nor treats it
+// as an LDS write), no staging registers and no ds_write.  Chunk c+2 is
+// issued into buffer c & 1 right after the barrier that ends chunk c; the
+// barrier before chunk c+1 first waits for this wave's DMA (vmcnt(0): the
+// previous chunk's h1 stores, issued after the DMA of chunk c+1, have had a
+// whole chunk of MFMAs to drain).
 template <int WAVES, int DBG = 0>
 struct Stager {
+    static constexpr bool kDma = (DBG & 32) != 0;
     static constexpr int kPer = kChunk / (64 * WAVES * 16);
-    u32x4v r[kPer];
+    u32x4v r[kDma ? 1 : kPer];
     const u32x4v* src;
     char* lds;
     int cur, n_chunks, tid;
+    bool defer = false;  // DMA mode: finish_chunk leaves the next issue to issue_deferred()
+    int pending = -1;
+    __device__ void issue_deferred() {
+        if (pending >= 0) issue(pending);
+        pending = -1;
+    }
     __device__ void issue(int c) {
         const u32x4v* p = src + (int64_t)c * (kChunk / 16);
+        if constexpr (kDma) {
+            const uint32_t base = (uint32_t)(uintptr_t)(lds + (c & 1) * kChunk) + (tid & ~63) * 16;
 #pragma unroll
-        for (int i = 0; i < kPer; ++i) r[i] = p[tid + 64 * WAVES * i];
+            for (int i = 0; i < kPer; ++i) {
+                const uint32_t m = __builtin_amdgcn_readfirstlane(base + 64 * WAVES * 16 * i);
+                asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                             ::"s"(m), "v"(p + tid + 64 * WAVES * i) : "memory", "m0");
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < kPer; ++i) r[i] = p[tid + 64 * WAVES * i];
+        }
     }
     __device__ void write(int c) {
-        u32x4v* d = reinterpret_cast<u32x4v*>(lds + (c & 1) * kChunk);
+        if constexpr (!kDma) {
+            u32x4v* d = reinterpret_cast<u32x4v*>(lds + (c & 1) * kChunk);
 #pragma unroll
-        for (int i = 0; i < kPer; ++i) d[tid + 64 * WAVES * i] = r[i];
+            for (int i = 0; i < kPer; ++i) d[tid + 64 * WAVES * i] = r[i];
+        }
     }
     __device__ static void barrier() {
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if constexpr (kDma)
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
     __device__ void start(const char* wpack, char* lds_base, int chunks) {
         src = reinterpret_cast<const u32x4v*>(wpack);
@@ -186,19 +218,34 @@ struct Stager {
         tid = threadIdx.x;
         n_chunks = chunks;
         cur = 0;
-        issue(0);
-        write(0);
-        if (chunks > 1) issue(1);
+        if constexpr (kDma) {
+            issue(0);
+            if (chunks > 1) issue(1);
+        } else {
+            issue(0);
+            write(0);
+            if (chunks > 1) issue(1);
+        }
         barrier();
     }
     __device__ const char* buffer() const { return lds + (cur & 1) * kChunk; }
     __device__ void finish_chunk() {
-        if constexpr (!(DBG & 2)) {
-            if (cur + 1 < n_chunks) write(cur + 1);
-        }
-        if constexpr (!(DBG & 1)) barrier();
-        if constexpr (!(DBG & 2)) {
-            if (cur + 2 < n_chunks) issue(cur + 2);
+        if constexpr (kDma) {
+            barrier();  // this wave's DMA of chunk cur+1 landed; every wave left buffer cur & 1
+            if (cur + 2 < n_chunks) {
+                if (defer)
+                    pending = cur + 2;
+                else
+                    issue(cur + 2);
+            }
+        } else {
+            if constexpr (!(DBG & 2)) {
+                if (cur + 1 < n_chunks) write(cur + 1);
+            }
+            if constexpr (!(DBG & 1)) barrier();
+            if constexpr (!(DBG & 2)) {
+                if (cur + 2 < n_chunks) issue(cur + 2);
+            }
         }
         ++cur;
     }
@@ -476,7 +523,7 @@ void sigma_meshrir_h1_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) char lds[2 * kChunk + WAVES * 4096];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t n0 = ((int64_t)blockIdx.x * WAVES + wave) * 32 * NT;
-    Stager<WAVES, DBG & 3> st;
+    Stager<WAVES, DBG & 99> st;
     st.start(a.wpack, lds, 12);
 
     frag8 x0[NT][3];
@@ -518,11 +565,16 @@ void sigma_meshrir_h1_kernel(Args a) {
         dense<E, NT, 8, 1, 1>(st, lane, x, acc);
         store_attn<E, NT>(a, acc, n0, lane);
     }
+    // DBG & 64 (with the DMA stager): each h1 chunk's weight DMA is issued
+    // after the previous chunk's epilogue, whose bias loads would otherwise
+    // wait for it (vmcnt counts in order)
+    if constexpr ((DBG & 64) != 0) st.defer = true;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         f32x16 acc[NT][4];
         dense<E, NT, 8, 4, 4>(st, lane, xs, acc);
         store_h1<E, NT, !(DBG & 4), !(DBG & 8)>(a, acc, n0, lane, c, lds + 2 * kChunk + wave * 4096);
+        if constexpr ((DBG & 64) != 0) st.issue_deferred();
     }
 }
 
@@ -675,6 +727,8 @@ int dispatch(const avr_sigma_desc* d, Args& a, bool h1, bool two, hipStream_t st
         // 4, 5: 64 samples per wave (each weight fragment feeds two MFMAs),
         // 1 or 2 waves per SIMD (experiments)
         if (d->tile_cfg == 4) return launch_meshrir_h1<E, 2, 4, 1>(a, st);
+        if (d->tile_cfg == 6) return launch_meshrir_h1<E, 1, 4, 2, 32>(a, st);  // LDS-DMA weight staging
+        if (d->tile_cfg == 7) return launch_meshrir_h1<E, 1, 4, 2, 96>(a, st);  // + h1 DMAs after the epilogue
         if (d->tile_cfg == 5) return launch_meshrir_h1<E, 2, 4, 2>(a, st);
         // timing experiments (results are garbage): no barrier / no weight
         // staging / no h1 stores (bf16 builds only)
@@ -685,7 +739,8 @@ int dispatch(const avr_sigma_desc* d, Args& a, bool h1, bool two, hipStream_t st
             if (d->tile_cfg == 19) return launch_meshrir_h1<E, 1, 4, 2, 7>(a, st);
             if (d->tile_cfg == 20) return launch_meshrir_h1<E, 1, 4, 2, 8>(a, st);  // no bias loads
         }
-        return launch_meshrir_h1<E, 1, 4, 2>(a, st);
+        if (d->tile_cfg == 8) return launch_meshrir_h1<E, 1, 4, 2>(a, st);  // register-staged weights
+        return launch_meshrir_h1<E, 1, 4, 2, 96>(a, st);  // LDS-DMA staging, h1 DMAs after the epilogue
     }
     const int cfg = d->tile_cfg;
     // tile configs (tools/probe_sigma.py, MI355X at config 2): MeshRIR
