@@ -124,6 +124,8 @@ def parse_args(argv=None):
                     help="pose mode: skip the config-2 inference through the reference network")
     ap.add_argument("--poses", type=int, default=16,
                     help="distinct synthetic poses cycled over the steps")
+    ap.add_argument("--graph-ring", type=int, default=12,
+                    help="captured graph instances per stream (GraphedRender ring)")
     ap.add_argument("--streams", type=int, default=2,
                     help="pose mode: HIP streams the independent per-pose renders are issued on "
                          "round-robin, each with its own signal buffer (1 = strictly serial; "
@@ -476,7 +478,7 @@ def bench_pose(args, w, world, rank, dev):
     latency_eager_ms = latency(lambda: step(0))
     from avr_amd.graph import GraphedRender
 
-    graphed = GraphedRender(renderers[0])
+    graphed = GraphedRender(renderers[0], ring=args.graph_ring)
     # poses handed over from the host, as a data loader yields them
     # (avr_runner.py:168): staged in the replay's pinned buffer, no copy
     ro_h, tx_h = rays_o.cpu(), tx.cpu()
@@ -508,7 +510,7 @@ def bench_pose(args, w, world, rank, dev):
     # stages the pose and launches the graph, so it never gates the GPU --
     # not even in the first steps of a short timed region, where eager
     # issue (~75 us of Python per pose) used to leave the GPU idle
-    graphs = [graphed] + [GraphedRender(rr) for rr in renderers[1:]]
+    graphs = [graphed] + [GraphedRender(rr, ring=args.graph_ring) for rr in renderers[1:]]
 
     def run_graph(n, ns):
         for i in range(n):
