@@ -638,8 +638,7 @@ __global__ __launch_bounds__(256) void hg_bwd_scatter_kernel(int64_t N, int L, c
                                                              const Tg* __restrict__ gout, LevelTable lt,
                                                              BwdPlan plan, const int* __restrict__ offs,
                                                              const int* __restrict__ part_start,
-                                                             uint32_t* __restrict__ keys,
-                                                             float2* __restrict__ vals) {
+                                                             uint3* __restrict__ contrib) {
     extern __shared__ int scat_l[];  // base[P], slot[P]
     const int l = blockIdx.y;
     const int pb = plan.pbase[l];
@@ -654,8 +653,8 @@ __global__ __launch_bounds__(256) void hg_bwd_scatter_kernel(int64_t N, int L, c
     bwd_walk(N, L, l, x, gout, lt, [&](uint32_t e, float v0, float v1) {
         const int part = (int)(e >> kPartBits);
         const int pos = base[part] + atomicAdd(&slot[part], 1);
-        keys[pos] = e & (kPartEntries - 1);
-        vals[pos] = make_float2(v0, v1);
+        // one 12-byte store per contribution: (key, v0, v1)
+        contrib[pos] = make_uint3(e & (kPartEntries - 1), __float_as_uint(v0), __float_as_uint(v1));
     });
 }
 
@@ -689,8 +688,7 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
                                                                          const int* __restrict__ totals,
                                                                          const int* __restrict__ part_start,
                                                                          const int* __restrict__ slice_base,
-                                                                         const uint32_t* __restrict__ keys,
-                                                                         const float2* __restrict__ vals,
+                                                                         const uint3* __restrict__ contrib,
                                                                          float* __restrict__ gparams, int dbg,
                                                                          unsigned long long* __restrict__ dbg_out) {
     __shared__ float2 img_all[kReduceWaves][kPartEntries];
@@ -728,8 +726,9 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int j = i + 64 * u + lane;
-            kk[u] = j < i1 ? keys[j] : 0u;
-            v[u] = j < i1 ? vals[j] : make_float2(0.f, 0.f);
+            const uint3 cv = contrib[j < i1 ? j : i0];
+            kk[u] = j < i1 ? cv.x : 0u;
+            v[u] = j < i1 ? make_float2(__uint_as_float(cv.y), __uint_as_float(cv.z)) : make_float2(0.f, 0.f);
         }
         if (dbg & 1) {  // timing experiment: no adds
             float t = 0.f;
@@ -811,7 +810,7 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
 struct BwdLayout {
     BwdPlan plan;
     int total_parts;
-    int64_t counts, totals, part_start, slice_base, keys, vals, dbg, bytes;  // byte offsets in the workspace
+    int64_t counts, totals, part_start, slice_base, contrib, dbg, bytes;  // byte offsets in the workspace
     int max_slices;  // reduce grid: total_parts + maxc / kDenseSlice bounds the slice count
     bool scatter_ok; // the largest level's partition table fits the count/scatter LDS
 };
@@ -857,10 +856,8 @@ int bwd_layout(int64_t N, int L, const int64_t* off, const int32_t* res, BwdLayo
     o0 += al((int64_t)(b.total_parts + 1) * 4);
     b.max_slices = b.total_parts + (int)(maxc / kDenseSlice) + 1;
     b.scatter_ok = b.plan.max_parts <= kMaxScatterParts;
-    b.keys = o0;
-    o0 += al(maxc * 4);
-    b.vals = o0;
-    o0 += al(maxc * 8);
+    b.contrib = o0;  // (key, v0, v1) per contribution
+    o0 += al(maxc * 12);
     b.dbg = o0;  // 3 counters of the reduce pass's diagnostics (AVR_HG_BWD_DBG & 4)
     o0 += 256;
     b.bytes = o0;
@@ -1131,8 +1128,7 @@ extern "C" int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const f
     char* ws = static_cast<char*>(workspace);
     int* counts = reinterpret_cast<int*>(ws + b.counts);
     int* totals = reinterpret_cast<int*>(ws + b.totals);
-    uint32_t* keys = reinterpret_cast<uint32_t*>(ws + b.keys);
-    float2* vals = reinterpret_cast<float2*>(ws + b.vals);
+    uint3* contrib = reinterpret_cast<uint3*>(ws + b.contrib);
     const dim3 grid((unsigned)b.plan.nchunks, (unsigned)L);
     const size_t lds_count = (size_t)b.plan.max_parts * 4, lds_scat = (size_t)b.plan.max_parts * 8;
     if (!b.scatter_ok) {  // > 2^22 entries in a level: the atomic kernel (same += result)
@@ -1156,13 +1152,13 @@ extern "C" int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const f
                        slice_base);
     if (grad_dtype == AVR_DTYPE_F32)
         hipLaunchKernelGGL(hg_bwd_scatter_kernel<float>, grid, dim3(256), lds_scat, st, N, L, x,
-                           (const float*)grad_out, lt, b.plan, counts, part_start, keys, vals);
+                           (const float*)grad_out, lt, b.plan, counts, part_start, contrib);
     else
         hipLaunchKernelGGL(hg_bwd_scatter_kernel<__half>, grid, dim3(256), lds_scat, st, N, L, x,
-                           (const __half*)grad_out, lt, b.plan, counts, part_start, keys, vals);
+                           (const __half*)grad_out, lt, b.plan, counts, part_start, contrib);
     hipLaunchKernelGGL(hg_bwd_reduce_kernel, dim3((unsigned)((b.max_slices + kReduceWaves - 1) / kReduceWaves)),
                        dim3(64 * kReduceWaves), 0, st, L, lt, b.plan, b.total_parts, totals, part_start, slice_base,
-                       keys, vals, grad_params, getenv("AVR_HG_BWD_DBG") ? atoi(getenv("AVR_HG_BWD_DBG")) : 0,
+                       contrib, grad_params, getenv("AVR_HG_BWD_DBG") ? atoi(getenv("AVR_HG_BWD_DBG")) : 0,
                        reinterpret_cast<unsigned long long*>(ws + b.dbg));
     return check_launch("avr_hashgrid_bwd_partitioned");
 }

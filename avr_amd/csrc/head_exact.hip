@@ -431,7 +431,7 @@ __device__ __forceinline__ void dma_row16(const void* g, uint32_t lds) {
 // contiguous column range with a stride; the t-blocks of a column run on one
 // XCD (its h rows shared through that L2).  Removes the per-item W prologue
 // and the workgroup turnover of the one-item form.
-template <typename E, int TR, int NBUF, int DBG = 0, bool PERSIST = false>
+template <typename E, int TR, int NBUF, int DBG = 0, bool PERSIST = false, int MP = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void head_exact_dma_kernel(
     avr_render_params pp, int B, int R, int K, const E* __restrict__ h, const E* __restrict__ W,
     const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
@@ -489,31 +489,82 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     const int64_t hstride = (int64_t)S * K;
 
+    // a column's metadata (cnt at this wave's t and, for MP > 0, the sorted
+    // rays and their weights: R <= 512 * MP), loaded one column ahead into
+    // registers: its loads fly under the previous column's tiles.  MP = 0
+    // (more rays than the registers allow) loads the rays in the column.
+    constexpr int kMP = MP > 0 ? MP : 1;
+    struct Meta {
+        int nblk, cnt_t, cwave, cfull;
+        int pv[kMP];
+        float wv[kMP];
+    };
+    auto fetch = [&](int64_t c, Meta& m) {
+        if (c >= c_end) return;
+        const int sc = (int)(c % S);
+        const int limc = tail_limit(pp, sc);
+        const int tl = min(tb * TB + TB, limc) - 1;
+        if (tl < tb * TB) {
+            m.nblk = -1;  // nothing live in this t-block
+            return;
+        }
+        const int* cc = cnt + c * T;
+        m.nblk = cc[tl];
+        m.cnt_t = (t < limc) ? cc[t] : 0;
+        m.cwave = (t0 < limc) ? cc[min(t0 + 31, limc - 1)] : 0;
+        m.cfull = (t0 + 31 < limc) ? cc[t0] : 0;
+        if constexpr (MP > 0) {
+#pragma unroll
+            for (int jj = 0; jj < kMP; ++jj) {
+                const int pq = (int)threadIdx.x + NT * jj;
+                if (pq < R) {
+                    m.pv[jj] = perm[c * R + pq];
+                    m.wv[jj] = ws[c * R + pq];
+                }
+            }
+        }
+    };
+    Meta m;
+    fetch(c_first, m);
     for (int64_t col = c_first; col < c_end; col += c_step) {
         if (PERSIST && col != c_first) __syncthreads();  // the previous column's LDS reads are done
         const int s = (int)(col % S), b = (int)(col / S);
         const int lim = tail_limit(pp, s);
         float* zcol = z + col * T;
-        const int tlast = min(tb * TB + TB, lim) - 1;
-        if (tlast < tb * TB) {
+        if (m.nblk < 0) {
             for (int i = threadIdx.x; i < TB; i += NT)
                 if (tb * TB + i < T) zcol[tb * TB + i] = 0.0f;
+            fetch(col + c_step, m);
             continue;
         }
-        const int* ccol = cnt + col * T;
-        const int nblk = ccol[tlast];
-        const int cnt_t = (t < lim) ? ccol[t] : 0;
-        const int cwave = (t0 < lim) ? ccol[min(t0 + 31, lim - 1)] : 0;
+        const int nblk = m.nblk, cnt_t = m.cnt_t, cwave = m.cwave;
         // rays live at EVERY t of this wave's tile (cnt is nondecreasing in t):
         // a 32-ray sub-tile below it needs no mask in its epilogue
-        const int cfull = __builtin_amdgcn_readfirstlane((t0 + 31 < lim) ? ccol[t0] : 0);
+        const int cfull = __builtin_amdgcn_readfirstlane(m.cfull);
         const int ntile = (nblk + TR - 1) / TR;
-        for (int p = threadIdx.x; p < ntile * TR; p += NT) {
-            const bool in = p < nblk;
-            pl[p] = perm[col * R + (in ? p : nblk - 1)];
-            wl[p] = in ? ws[col * R + p] : 0.0f;
+        if constexpr (MP > 0) {
+#pragma unroll
+            for (int jj = 0; jj < kMP; ++jj) {
+                const int pq = (int)threadIdx.x + NT * jj;
+                if (pq < nblk) {
+                    pl[pq] = m.pv[jj];
+                    wl[pq] = m.wv[jj];
+                }
+            }
+        } else {
+            for (int pq = threadIdx.x; pq < nblk; pq += NT) {
+                pl[pq] = perm[col * R + pq];
+                wl[pq] = ws[col * R + pq];
+            }
         }
         __syncthreads();
+        // rows past the live ones: the last live ray again, weight 0
+        for (int pq = nblk + (int)threadIdx.x; pq < ntile * TR; pq += NT) {
+            pl[pq] = pl[nblk - 1];
+            wl[pq] = 0.0f;
+        }
+        __syncthreads();
+        fetch(col + c_step, m);  // the next column's metadata, under this column's tiles
         const E* hcol = h + ((int64_t)b * R * S + s) * K + 8 * lane;
 
         // rows wave*RPW .. +RPW-1 of tile `tile` into buffer tile % NBUF; the
@@ -734,11 +785,18 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
             hipLaunchKernelGGL(kern, grid_dma, dim3(512), lds, st, *p, (int)B, R, (int)K, hp, (decltype(hp))W, perm,
                                ws, cnt, z, ntb, waves == 19 ? wg_per_xcd : per_xcd);
         };
-        if (waves == 19) {
-            if (dtype == AVR_DTYPE_F16)
-                go_dma(head_exact_dma_kernel<__half, 64, 2, 0, true>, (const __half*)h);
-            else
-                go_dma(head_exact_dma_kernel<__hip_bfloat16, 64, 2, 0, true>, (const __hip_bfloat16*)h);
+        if (waves == 19) {  // rays prefetched one column ahead while they fit 2 registers per thread
+            if (R <= 1024) {
+                if (dtype == AVR_DTYPE_F16)
+                    go_dma(head_exact_dma_kernel<__half, 64, 2, 0, true, 2>, (const __half*)h);
+                else
+                    go_dma(head_exact_dma_kernel<__hip_bfloat16, 64, 2, 0, true, 2>, (const __hip_bfloat16*)h);
+            } else {
+                if (dtype == AVR_DTYPE_F16)
+                    go_dma(head_exact_dma_kernel<__half, 64, 2, 0, true, 0>, (const __half*)h);
+                else
+                    go_dma(head_exact_dma_kernel<__hip_bfloat16, 64, 2, 0, true, 0>, (const __hip_bfloat16*)h);
+            }
             return check_launch("avr_head_fwd_exact");
         }
 #define AVR_HD(TRV, NBV)                                                                              \

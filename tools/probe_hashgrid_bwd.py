@@ -130,9 +130,10 @@ def main():
             "butterfly_iters": d[1], "contribs": d[2], "total_slices": int(sb[-1]),
             "max_part_total": int(totals.max()), "mean_part_total": float(totals.mean())}
     # the slowest partition's keys, in the order the reduce wave reads them
-    o_keys = o_sb + al((tp + 1) * 4)
+    o_c = o_sb + al((tp + 1) * 4)  # (key, v0, v1) records
     ps = ws[o_ps:o_ps + 4 * (tp + 1)].view(torch.int32).cpu().numpy()
-    k = ws[o_keys + 4 * int(ps[p_slow]):o_keys + 4 * int(ps[p_slow] + totals[p_slow])].view(torch.int32).cpu().numpy()
+    k = ws[o_c + 12 * int(ps[p_slow]):o_c + 12 * int(ps[p_slow] + totals[p_slow])].view(torch.int32).view(-1, 3)[:, 0]
+    k = k.cpu().numpy()
     rep, mx, dist = [], [], []
     for j in range(0, len(k), 64):
         u_, c_ = np.unique(k[j:j + 64], return_counts=True)
