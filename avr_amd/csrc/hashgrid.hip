@@ -1093,9 +1093,11 @@ extern "C" int avr_hashgrid_bwd_workspace(int64_t N, int32_t n_levels, const int
         *bytes = 256;
         return 0;
     }
+    if (n_levels < 1 || n_levels > kMaxLevels) return fail(AVR_E_ARG, "hashgrid: n_levels out of range (1..32)");
     BwdLayout b;
-    if (int e = bwd_layout(N, n_levels, level_offset, nullptr, &b)) return e;
-    *bytes = b.bytes;
+    // shapes the partitioned passes do not take (over 2^31 contributions,
+    // level sizes not multiples of 8) run the atomic kernel: no workspace
+    *bytes = (bwd_layout(N, n_levels, level_offset, nullptr, &b) == 0 && b.scatter_ok) ? b.bytes : 256;
     return 0;
 }
 
@@ -1123,7 +1125,14 @@ extern "C" int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const f
         return check_launch("avr_hashgrid_bwd_partitioned");
     }
     BwdLayout b;
-    if (int e = bwd_layout(N, n_levels, level_offset, level_res, &b)) return e;
+    if (bwd_layout(N, n_levels, level_offset, level_res, &b) != 0 || !b.scatter_ok) {
+        // shapes the partitioned passes do not take: the atomic kernel (same += result)
+        if (grad_dtype == AVR_DTYPE_F32)
+            launch_bwd<float>(st, N, L, x, (const float*)grad_out, lt, grad_params);
+        else
+            launch_bwd<__half>(st, N, L, x, (const __half*)grad_out, lt, grad_params);
+        return check_launch("avr_hashgrid_bwd_partitioned");
+    }
     AVR_REQUIRE(workspace_bytes >= b.bytes, "avr_hashgrid_bwd_partitioned: workspace too small");
     char* ws = static_cast<char*>(workspace);
     int* counts = reinterpret_cast<int*>(ws + b.counts);
@@ -1131,13 +1140,6 @@ extern "C" int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const f
     uint3* contrib = reinterpret_cast<uint3*>(ws + b.contrib);
     const dim3 grid((unsigned)b.plan.nchunks, (unsigned)L);
     const size_t lds_count = (size_t)b.plan.max_parts * 4, lds_scat = (size_t)b.plan.max_parts * 8;
-    if (!b.scatter_ok) {  // > 2^22 entries in a level: the atomic kernel (same += result)
-        if (grad_dtype == AVR_DTYPE_F32)
-            launch_bwd<float>(st, N, L, x, (const float*)grad_out, lt, grad_params);
-        else
-            launch_bwd<__half>(st, N, L, x, (const __half*)grad_out, lt, grad_params);
-        return check_launch("avr_hashgrid_bwd_partitioned");
-    }
     if (grad_dtype == AVR_DTYPE_F32)
         hipLaunchKernelGGL(hg_bwd_count_kernel<float>, grid, dim3(256), lds_count, st, N, L, x,
                            (const float*)grad_out, lt, b.plan, counts);
