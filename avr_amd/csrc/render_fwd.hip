@@ -493,10 +493,20 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
     __shared__ float As[32][kKc + 1];
     const int F = T / 2 + 1;
     const int P = ((S + 31) / 32) * KS;
+    // XCD-aware order: every workgroup of one s-tile (its k-slices x F-blocks)
+    // runs on one XCD (dispatch goes round-robin over the 8 XCDs by
+    // workgroup id), so the tile's z rows and phase rows are fetched into
+    // that XCD's L2 once instead of once per k-slice / F-block
+    (void)P;
+    const int nfb = (F + 127) / 128, nst = (S + 31) / 32;
+    const int L = blockIdx.x, xcd = L & 7, q = L >> 3;
+    const int per = KS * nfb;  // workgroups of one s-tile
+    const int stile = (q / per) * 8 + xcd;
+    if (stile >= nst) return;  // padding workgroups of the 8-way split
+    const int ks = (q % per) / nfb, fblk = (q % per) % nfb;
     const int b = blockIdx.z;
-    const int stile = blockIdx.y / KS, ks = blockIdx.y % KS;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int fbase = blockIdx.x * 128 + wave * 32;
+    const int fbase = fblk * 128 + wave * 32;
     const int f = fbase + (lane & 31);
     const int fm = (f < F) ? f : 0;
     const int half = lane >> 5;
@@ -1175,7 +1185,11 @@ extern "C" int avr_dft_phase_fwd(const avr_render_params* p, int32_t B, const fl
     const int nkc = (T + kKc - 1) / kKc;
     AVR_REQUIRE(k_split >= 1 && k_split <= nkc, "avr_dft_phase_fwd: k_split out of range");
     const int kchunk = ((nkc + k_split - 1) / k_split) * kKc;
-    const dim3 grid((F + 127) / 128, ((S + 31) / 32) * k_split, B);
+    // one dimension of (s-tile, k-slice, F-block) workgroups in the XCD-aware
+    // order the kernel decodes (8 XCDs x ceil(s-tiles / 8) x k-slices x
+    // F-blocks; padding ones exit)
+    const int nst = (S + 31) / 32;
+    const dim3 grid((unsigned)(8 * ((nst + 7) / 8) * k_split * ((F + 127) / 128)), 1, B);
     const size_t lds = (size_t)T * sizeof(float2);
     auto go = [&](auto kern) {
         if (lds > 65536)
