@@ -503,13 +503,16 @@ def bench_pose(args, w, world, rank, dev):
     torch.cuda.synchronize()
     timer.enabled = False
 
-    # throughput (the reported value): K independent single-pose renders,
-    # each replayed from its stream's HIP graph (the same kernels and
-    # results as the eager render, tests/test_gpu_graph.py) with the pose
-    # handed over from the host: per pose the host only draws the jitter,
-    # stages the pose and launches the graph, so it never gates the GPU --
-    # not even in the first steps of a short timed region, where eager
-    # issue (~75 us of Python per pose) used to leave the GPU idle
+    # throughput: K independent single-pose renders on 2 streams, issued
+    # eagerly (the reported value) and, as a second measurement, replayed
+    # from each stream's HIP graph ring (the same kernels and results,
+    # tests/test_gpu_graph.py; host poses staged in pinned memory).  Since
+    # round 3 the eager issue (~75 us of host work per pose) no longer gates
+    # a ~120 us pose, and it keeps each stream's kernels back to back, while
+    # consecutive graph replays on one stream leave 15-23 us between them
+    # (kernel trace): eager measured 0.1186-0.1226 against
+    # 0.1210-0.1308 ms per pose for the replays over 4 runs of the driver's
+    # command (tools/gpu_eager_graph.sh)
     graphs = [graphed] + [GraphedRender(rr, ring=args.graph_ring) for rr in renderers[1:]]
 
     def run_graph(n, ns):
@@ -523,8 +526,8 @@ def bench_pose(args, w, world, rank, dev):
 
     run_graph(max(args.warmup, (graphed.ring + 2) * n_streams), n_streams)  # captures + warm replays
     torch.cuda.synchronize()
-    elapsed_eager, _ = timed(lambda: run(args.steps, n_streams), world, dev)
-    elapsed, t_issue = timed(lambda: run_graph(args.steps, n_streams), world, dev)
+    elapsed, t_issue = timed(lambda: run(args.steps, n_streams), world, dev)
+    elapsed_graph, t_issue_graph = timed(lambda: run_graph(args.steps, n_streams), world, dev)
     value = whole_job_rate(w.ray_samples, world, args.steps, elapsed)
     res = _base_result(args, w, world, value, elapsed, "f32" if dt == torch.float32 else "f16-storage/f32-math")
     res.update({
@@ -532,8 +535,9 @@ def bench_pose(args, w, world, rank, dev):
         "ir_render_path": "HIP-graph replay (avr_amd.graph.GraphedRender), host poses, synchronized per pose",
         "ir_render_ms_per_pose_eager": latency_eager_ms / B,
         "host_issue_ms_per_step": t_issue * 1e3 / args.steps,
-        "throughput_path": "HIP-graph replay per pose (avr_amd.graph.GraphedRender), host poses",
-        "ms_per_step_eager": elapsed_eager * 1e3 / args.steps,
+        "throughput_path": "eager issue, 2 HIP streams round-robin (one ctypes render-core call per pose)",
+        "ms_per_step_graph": elapsed_graph * 1e3 / args.steps,
+        "host_issue_ms_per_step_graph": t_issue_graph * 1e3 / args.steps,
         "streams": n_streams,
         "config": {"workload": w.name, "mode": "pose", "rays": R, "samples": S, "T": T, "freq_bins": w.F,
                    "poses_per_step": B, "distinct_poses": P,

@@ -21,7 +21,7 @@ tail -1 $OUT/smoke.log
 for i in 1 2; do
   step bench$i 400 python bench.py --gpus 1 --steps 20 --warmup 5
   tail -1 $OUT/bench$i.log > $OUT/bench$i.json
-  python -c "import json; d=json.load(open('$OUT/bench$i.json')); print('bench', d['value'], d['ms_per_step'], d['ms_per_step_eager'], d['ir_render_ms_per_pose'], d['roofline']['avg_launch_ms'], d['network_inference']['ms_per_pose'])"
+  python -c "import json; d=json.load(open('$OUT/bench$i.json')); print('bench', d['value'], d['ms_per_step'], d['ms_per_step_graph'], d['ir_render_ms_per_pose'], d['roofline']['avg_launch_ms'], d['network_inference']['ms_per_pose'])"
 done
 step prof 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-network --no-cpu-baseline
 step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --no-network --steps 20 --warmup 3 --streams 1
