@@ -30,6 +30,14 @@
 
 using namespace avr;
 
+namespace avr {
+// head_band.hip: the band form of the forward for 16-bit h
+int head_band_slices(const avr_render_params& p, int K, int es, int kbw);
+int head_band_fwd(const avr_render_params& p, int B, int K, const void* h, const void* Wp, int dtype, int kbw,
+                  const int32_t* perm, const float* ws, const int32_t* cnt, int nq, float* zpart,
+                  hipStream_t st);
+}  // namespace avr
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -990,7 +998,10 @@ extern "C" int avr_head_splits(const avr_render_params* p, int32_t B, int32_t K,
     HeadShape hs;
     const int es = elem_size(dtype);
     if (int e = head_shape(*p, B, n_rays(*p), K, es, &hs)) return e;
-    *n_split = hs.n_kg;
+    int kbf, sb;
+    fwd_block(hs, dtype, &kbf, &sb);
+    const int nq = head_band_slices(*p, K, es, kbf);
+    *n_split = nq > 0 ? nq : hs.n_kg;
     return 0;
 }
 
@@ -1023,13 +1034,17 @@ extern "C" int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, co
     const int R = n_rays(*p);
     HeadShape hs;
     if (int e = head_shape(*p, B, R, K, elem_size(dtype), &hs)) return e;
-    AVR_REQUIRE(n_split == hs.n_kg, "avr_head_fwd: n_split must come from avr_head_splits");
-    const dim3 grid(hs.n_kg, p->n_samples, B);
     hipStream_t st = as_stream(stream);
-    const char* dbg_env = getenv("AVR_HEAD_DBG");  // profiling only: skip phases
-    const int dbg = dbg_env ? atoi(dbg_env) : 0;
     int kbf, sb;
     fwd_block(hs, dtype, &kbf, &sb);
+    if (const int nq = head_band_slices(*p, K, elem_size(dtype), kbf)) {
+        AVR_REQUIRE(n_split == nq, "avr_head_fwd: n_split must come from avr_head_splits");
+        return head_band_fwd(*p, B, K, h, W, dtype, kbf, perm, ws, cnt, nq, zpart, st);
+    }
+    AVR_REQUIRE(n_split == hs.n_kg, "avr_head_fwd: n_split must come from avr_head_splits");
+    const dim3 grid(hs.n_kg, p->n_samples, B);
+    const char* dbg_env = getenv("AVR_HEAD_DBG");  // profiling only: skip phases
+    const int dbg = dbg_env ? atoi(dbg_env) : 0;
     HeadShape hf = hs;
     hf.kb = kbf;
     hf.lds_c = cumsum_lds_bytes(R, kbf);
