@@ -124,9 +124,36 @@ def _zero_bias(n, dtype, device):
     return z
 
 
+# AVR_LINEAR=0 keeps hipBLASLt for the width-512 hidden layers (A/B runs)
+_LINEAR_HIP = os.environ.get("AVR_LINEAR", "1") != "0"
+
+
+def _linear_relu_hip(x, w):
+    """relu(x W^T) for the width-512 hidden layers on the HIP MFMA kernel
+    (csrc/linear_fwd.hip), or None when the shape is not its (16-bit, K = 512,
+    N a multiple of 256)."""
+    if not (_LINEAR_HIP and x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and w.dtype == x.dtype
+            and x.dim() == 2 and x.size(1) == 512 and w.size(1) == 512 and w.size(0) % 256 == 0
+            and x.is_contiguous() and w.is_contiguous() and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0):
+        return None
+    import ctypes
+
+    from . import _lib
+
+    M, N = x.size(0), w.size(0)
+    y = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    if M == 0:
+        return y
+    code = _lib.DTYPE_F16 if x.dtype == torch.float16 else _lib.DTYPE_BF16
+    _lib.call("avr_linear_relu_fwd", M, N, 512, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(w.data_ptr()),
+              code, 1, ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+    return y
+
+
 class _LinearReLU(torch.autograd.Function):
-    """y = relu(x W^T) with the ReLU in the GEMM epilogue (hipBLASLt
-    `_addmm_activation` with a zero bias: one kernel instead of GEMM + an
+    """y = relu(x W^T) with the ReLU in the GEMM epilogue: the HIP MFMA
+    kernel for the width-512 layers (`_linear_relu_hip`), else hipBLASLt's
+    `_addmm_activation` with a zero bias (one kernel instead of GEMM + an
     elementwise pass over the [N, width] activation, bit-identical output).
     The backward is ReLU's own (threshold on the saved output), then the
     same data / weight gradients as `_Linear`."""
@@ -134,7 +161,10 @@ class _LinearReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_master, dtype, cache=False):
         w = cast_weight(w_master, dtype, cache)
-        if x.is_cuda:
+        y = _linear_relu_hip(x, w) if x.is_cuda else None
+        if y is not None:
+            pass
+        elif x.is_cuda:
             y = torch._addmm_activation(_zero_bias(w.size(0), dtype, x.device), x, w.t(),
                                         use_gelu=False)
         else:

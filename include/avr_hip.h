@@ -306,6 +306,12 @@ int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const float* x, co
  * avr_runner.py:190).  Split-K over n: `workspace` holds splits*M*K fp32
  * partials (splits from avr_linear_wgrad_splits), summed deterministically. */
 int avr_linear_wgrad_splits(int64_t N, int32_t M, int32_t K, int32_t* splits);
+/* y = relu(x W^T) (relu != 0) or x W^T: x [M, K] and W [N, K] (nn.Linear
+ * layout) 16-bit (dtype fp16 / bf16), y [M, N] of the same type, fp32
+ * accumulation and one rounding.  K = 512, N a multiple of 256 (the signal
+ * network's hidden layers, model.py:176-180); x and W 16-byte aligned. */
+int avr_linear_relu_fwd(int64_t M, int32_t N, int32_t K, const void* x, const void* W, int32_t dtype,
+                        int32_t relu, void* y, void* stream);
 int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* grad_y, const void* x,
                      float* workspace, int32_t splits, float* grad_w, void* stream);
 

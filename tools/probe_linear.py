@@ -1,0 +1,66 @@
+"""GPU probe: the width-512 hidden layer at config 2 (M = 262,144 rows),
+avr_linear_relu_fwd against hipBLASLt's torch._addmm_activation (the form
+model.py uses), HIP-event timing and agreement.
+
+    python tools/probe_linear.py [--dtype fp16] [--iters 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from avr_amd import _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"])
+    ap.add_argument("--M", type=int, default=262144)
+    ap.add_argument("--N", type=int, default=512)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    dt = torch.float16 if args.dtype == "fp16" else torch.bfloat16
+    code = _lib.DTYPE_F16 if dt == torch.float16 else _lib.DTYPE_BF16
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    M, N, K = args.M, args.N, 512
+    x = torch.relu(torch.randn(M, K, device=dev, generator=g)).to(dt)
+    w = (torch.randn(N, K, device=dev, generator=g) / K ** 0.5).to(dt)
+    bias = torch.zeros(N, dtype=dt, device=dev)
+    y = torch.empty(M, N, dtype=dt, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+
+    def ours():
+        _lib.call("avr_linear_relu_fwd", M, N, K, x.data_ptr(), w.data_ptr(), code, 1, y.data_ptr(), st)
+        return y
+
+    def blas():
+        return torch._addmm_activation(bias, x, w.t(), use_gelu=False)
+
+    for name, fn in (("avr_linear_relu_fwd", ours), ("hipblaslt_addmm_activation", blas)):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iters):
+            fn()
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / args.iters
+        print(json.dumps({"kernel": name, "dtype": args.dtype, "M": M, "N": N, "K": K, "us": ms * 1e3,
+                          "pflops": 2 * M * N * K / (ms * 1e-3) / 1e15}), flush=True)
+    a, b = ours().float(), blas().float()
+    print(json.dumps({"equal_fraction": float((a == b).float().mean()),
+                      "max_rel": float(((a - b).abs() / b.abs().clamp_min(1e-3)).max())}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
