@@ -6,7 +6,12 @@
 // Shape: x [M, 512], W [N, 512] (nn.Linear layout, so both operands are
 // contiguous in k), y [M, N] with N a multiple of 256 and M ~ 262,144 rows
 // at config 2.  hipBLASLt's solution for it (MT256x256x32, 16x16 MFMAs) runs
-// at 0.80 PFLOP/s; its bytes need ~85 us at HBM speed.
+// at 0.80-0.85 PFLOP/s; its bytes need ~85 us at HBM speed.
+//
+// Status: bit-identical to hipBLASLt and as fast (162-169 us
+// against 161-162 us warmed up, interleaved in one process), so it is opt-in
+// (AVR_LINEAR=1).  Its streaming skeleton alone (no MFMA, no stores) takes
+// ~110 us: both N-slices of a tile DMA it (536 MB through LDS-DMA per layer).
 //
 // Work: persistent workgroups of 8 waves, one per CU.  A workgroup owns a
 // 256-wide slice of N: wave w's 32 rows of W are its MFMA B operand, held
@@ -55,6 +60,10 @@ __device__ __forceinline__ void ldma16(const void* g, uint32_t lds) {
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(g)
                  : "memory", "m0");
 }
+__device__ __forceinline__ void ldma16_nt(const void* g, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt" ::"s"(lds), "v"(g)
+                 : "memory", "m0");
+}
 
 template <typename E>
 __device__ __forceinline__ unsigned short to16(float v) {
@@ -101,7 +110,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int rr = 0; rr < RPW; ++rr) {
             const int64_t row = min(m0 + wave * RPW + rr, M - 1);
-            ldma16(x + row * kLK + 8 * lane, (uint32_t)(uintptr_t)(a + rr * ROWB));
+            if (dbg & 4)  // experiment: non-temporal policy on the x stream
+                ldma16_nt(x + row * kLK + 8 * lane, (uint32_t)(uintptr_t)(a + rr * ROWB));
+            else
+                ldma16(x + row * kLK + 8 * lane, (uint32_t)(uintptr_t)(a + rr * ROWB));
         }
     };
     // vector-memory bookkeeping (uniform): operations issued by this wave
@@ -199,7 +211,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 const int row = 8 * g + 4 * half + 2 * pq + (odd ? 1 : 0);
                 const int col = n0 + (j & ~1);
                 // dbg & 1 (timing experiment): every store offset out of range (dropped)
-                __builtin_amdgcn_raw_buffer_store_b32(word, rsrc, (dbg & 1) ? 0x7ffffff0 : (row * N + col) * 2, 0, 0);
+                // non-temporal (aux 2): 162-169 us against 164-176 plain
+                __builtin_amdgcn_raw_buffer_store_b32(word, rsrc, (dbg & 1) ? 0x7ffffff0 : (row * N + col) * 2, 0, 2);
             }
         issued += kStores;
         __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LDS reads of tile i are done

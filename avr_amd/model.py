@@ -124,8 +124,9 @@ def _zero_bias(n, dtype, device):
     return z
 
 
-# AVR_LINEAR=0 keeps hipBLASLt for the width-512 hidden layers (A/B runs)
-_LINEAR_HIP = os.environ.get("AVR_LINEAR", "1") != "0"
+# AVR_LINEAR=1 runs the width-512 hidden layers on csrc/linear_fwd.hip
+# (opt-in: as fast as hipBLASLt, not faster)
+_LINEAR_HIP = os.environ.get("AVR_LINEAR", "0") == "1"
 
 
 def _linear_relu_hip(x, w):
@@ -151,10 +152,11 @@ def _linear_relu_hip(x, w):
 
 
 class _LinearReLU(torch.autograd.Function):
-    """y = relu(x W^T) with the ReLU in the GEMM epilogue: the HIP MFMA
-    kernel for the width-512 layers (`_linear_relu_hip`), else hipBLASLt's
+    """y = relu(x W^T) with the ReLU in the GEMM epilogue: hipBLASLt's
     `_addmm_activation` with a zero bias (one kernel instead of GEMM + an
-    elementwise pass over the [N, width] activation, bit-identical output).
+    elementwise pass over the [N, width] activation, bit-identical output),
+    or with AVR_LINEAR=1 the HIP MFMA kernel for the width-512 layers
+    (`_linear_relu_hip`, bit-identical to hipBLASLt on the probe).
     The backward is ReLU's own (threshold on the saved output), then the
     same data / weight gradients as `_Linear`."""
 

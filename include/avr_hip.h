@@ -309,7 +309,8 @@ int avr_linear_wgrad_splits(int64_t N, int32_t M, int32_t K, int32_t* splits);
 /* y = relu(x W^T) (relu != 0) or x W^T: x [M, K] and W [N, K] (nn.Linear
  * layout) 16-bit (dtype fp16 / bf16), y [M, N] of the same type, fp32
  * accumulation and one rounding.  K = 512, N a multiple of 256 (the signal
- * network's hidden layers, model.py:176-180); x and W 16-byte aligned. */
+ * network's hidden layers, model.py:176-180); x and W 16-byte aligned.
+ * Used by avr_amd.model only with AVR_LINEAR=1 (as fast as hipBLASLt). */
 int avr_linear_relu_fwd(int64_t M, int32_t N, int32_t K, const void* x, const void* W, int32_t dtype,
                         int32_t relu, void* y, void* stream);
 int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* grad_y, const void* x,

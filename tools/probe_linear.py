@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--M", type=int, default=262144)
     ap.add_argument("--N", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--dbgs", default="0", help="AVR_LINEAR_DBG values, interleaved --reps times")
+    ap.add_argument("--reps", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=200)
     args = ap.parse_args()
     dt = torch.float16 if args.dtype == "fp16" else torch.bfloat16
     code = _lib.DTYPE_F16 if dt == torch.float16 else _lib.DTYPE_BF16
@@ -44,7 +47,15 @@ def main():
     def blas():
         return torch._addmm_activation(bias, x, w.t(), use_gelu=False)
 
-    for name, fn in (("avr_linear_relu_fwd", ours), ("hipblaslt_addmm_activation", blas)):
+    for _ in range(args.warmup):  # clocks up before anything is timed
+        ours()
+        blas()
+    torch.cuda.synchronize()
+    runs = []
+    for _ in range(args.reps):
+        runs += [("avr_linear_relu_fwd", ours, d) for d in args.dbgs.split(",")] + [("hipblaslt_addmm_activation", blas, "0")]
+    for name, fn, dbg in runs:
+        os.environ["AVR_LINEAR_DBG"] = dbg
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -55,8 +66,9 @@ def main():
         e1.record()
         e1.synchronize()
         ms = e0.elapsed_time(e1) / args.iters
-        print(json.dumps({"kernel": name, "dtype": args.dtype, "M": M, "N": N, "K": K, "us": ms * 1e3,
+        print(json.dumps({"kernel": name, "dbg": int(dbg), "dtype": args.dtype, "M": M, "N": N, "K": K, "us": ms * 1e3,
                           "pflops": 2 * M * N * K / (ms * 1e-3) / 1e15}), flush=True)
+    os.environ["AVR_LINEAR_DBG"] = "0"
     a, b = ours().float(), blas().float()
     print(json.dumps({"equal_fraction": float((a == b).float().mean()),
                       "max_rel": float(((a - b).abs() / b.abs().clamp_min(1e-3)).max())}), flush=True)
