@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--forms", default="1,0")
     ap.add_argument("--rings", default="0", help="AVR_HEAD_BAND_RING values to time the band form at")
     ap.add_argument("--dbgs", default="0", help="AVR_HEAD_BAND_DBG values (timing experiments)")
+    ap.add_argument("--reps", type=int, default=1, help="repetitions of the whole set, interleaved")
+    ap.add_argument("--warmup", type=int, default=0, help="untimed renders of each form before any timing")
     args = ap.parse_args()
     dt = torch.float16 if args.dtype == "fp16" else torch.bfloat16
     dev = torch.device("cuda", 0)
@@ -47,7 +49,12 @@ def main():
     outs = {}
     with torch.no_grad():
         runs = [(f, rg, d) for f in args.forms.split(",") for rg in (args.rings.split(",") if f == "1" else ["0"])
-                for d in (args.dbgs.split(",") if f == "1" else ["0"])]
+                for d in (args.dbgs.split(",") if f == "1" else ["0"])] * args.reps
+        for _ in range(args.warmup):  # clocks up before anything is timed
+            for f in args.forms.split(","):
+                os.environ["AVR_HEAD_BAND"] = f
+                r.render_from_hidden(attn, h, W, dt, geom)
+        torch.cuda.synchronize()
         for form, ring, dbg in runs:
             os.environ["AVR_HEAD_BAND"] = form
             os.environ["AVR_HEAD_BAND_RING"] = ring
