@@ -29,11 +29,11 @@
 // into registers, kD tiles ahead.  Every sum runs in a fixed order: results
 // are bitwise reproducible.
 //
-// Status: correct and opt-in (AVR_HEAD_BAND=1); at config 2
-// fp16 it runs 140 us against 142 us for head_fwd_kernel, so the latter stays
-// the default.  Measured bounds: the streaming skeleton alone (no C terms,
-// no band products) takes 63-66 us, the compute adds ~75 us that the two or
-// three workgroups per CU do not hide.
+// Status: the default for 16-bit h; at config 2 fp16 it runs
+// 139.4 us against 141.6 us for head_fwd_kernel (warmed up, interleaved), and
+// is closer to a float64 sum.  Measured bounds: the streaming skeleton alone
+// (no C terms, no band products) takes 63-66 us, the compute adds ~75 us that
+// the two or three workgroups per CU do not hide.
 #include "common.h"
 
 #include <algorithm>
@@ -336,13 +336,12 @@ void allow_lds(Kern k, size_t lds) {
 namespace avr {
 
 // Feature slices of the band forward for this shape (the DFT's n_split), or 0
-// when it is not selected or does not apply.  Opt-in: AVR_HEAD_BAND=1 (it is
-// not faster than head_fwd_kernel yet, header note).  Applies to 16-bit h, K a
-// multiple of 128 with K/128 a power of two <= 16, W packed in blocks of >= 8
-// features, <= 4096 rays and T.
+// when it does not apply: 16-bit h, K a multiple of 128 with K/128 a power of
+// two <= 16, W packed in blocks of >= 8 features, <= 4096 rays and T.
+// AVR_HEAD_BAND=0 selects head_fwd_kernel (A/B runs, tests).
 int head_band_slices(const avr_render_params& p, int K, int es, int kbw) {
-    const char* e = getenv("AVR_HEAD_BAND");
-    if (!e || atoi(e) != 1) return 0;
+    if (const char* e = getenv("AVR_HEAD_BAND"))
+        if (atoi(e) == 0) return 0;
     if (es != 2 || K % kSliceK != 0 || kbw % 8 != 0) return 0;
     const int nq = K / kSliceK;
     if (nq > 16 || (nq & (nq - 1)) != 0) return 0;

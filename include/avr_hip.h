@@ -416,10 +416,11 @@ int avr_head_sort(const avr_render_params* p, int32_t B, const float* w, const i
  * contiguously.  Wp is avr_head_fwd's W argument. */
 int avr_head_pack_w(const avr_render_params* p, int32_t B, int32_t K, const void* W, int32_t dtype,
                     void* Wp, void* stream);
-/* W: the packed weight from avr_head_pack_w (same p, B, K, dtype).  With
- * AVR_HEAD_BAND=1 in the environment, 16-bit h and K a multiple of 128 run
- * the delay-band form (csrc/head_band.hip; n_split = K/128, which
- * avr_head_splits then returns); same sums in another fp32 order. */
+/* W: the packed weight from avr_head_pack_w (same p, B, K, dtype).  16-bit
+ * h with K a multiple of 128 runs the delay-band form (csrc/head_band.hip;
+ * n_split = K/128, which avr_head_splits then returns); AVR_HEAD_BAND=0 in
+ * the environment selects the feature-block form (same sums, another fp32
+ * order). */
 int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* W,
                  int32_t dtype, const int32_t* perm, const float* ws, const int32_t* cnt,
                  int32_t n_split, float* zpart, void* stream);
