@@ -106,8 +106,8 @@ __device__ __forceinline__ float row_sum16(float x) {
 constexpr int kBandWaves = 4;
 constexpr int kBandBuf = 4;  // chunk ring: 3 chunks in flight ahead of the one in use
 
-__host__ __device__ constexpr size_t band_lds_bytes(int R, int T) {
-    return (size_t)kBandBuf * kChunkB + 8 * (size_t)((R + 31) / 32 * 32) + 4 * (size_t)((T + 3) / 4 * 4) +
+__host__ __device__ constexpr size_t band_lds_bytes(int R, int T, int nbuf = kBandBuf) {
+    return (size_t)nbuf * kChunkB + 8 * (size_t)((R + 31) / 32 * 32) + 4 * (size_t)((T + 3) / 4 * 4) +
            4 * 2 * kBandWaves * 32;
 }
 
@@ -126,12 +126,12 @@ __device__ __forceinline__ float swap32_sum(float x) {
 // dbg (AVR_HEAD_BAND_DBG, timing experiments only; results then wrong):
 // 1 waits for every DMA, 2 skips the C terms, 8 the band products, 16 the
 // chunk barriers, 32 the tile barriers
-template <typename E>
+template <typename E, int NBUF = kBandBuf>
 __global__ __launch_bounds__(64 * kBandWaves) void head_band_fwd_kernel(
     avr_render_params pp, int B, int R, int K, int nq, int kbw, const E* __restrict__ h, const E* __restrict__ Wp,
     const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
     float* __restrict__ zpart, int dbg) {
-    constexpr int NBUF = kBandBuf, PD = NBUF - 1, WV = kBandWaves;
+    constexpr int PD = NBUF - 1, WV = kBandWaves;
     constexpr int KS = 8 / WV;   // k-steps of 16 per wave
     constexpr int IPW = 8 / WV;  // DMA instructions per wave per 32-row block
     extern __shared__ __attribute__((aligned(16))) char lds_b[];
@@ -358,17 +358,27 @@ int head_band_fwd(const avr_render_params& p, int B, int K, const void* h, const
     AVR_REQUIRE(items <= 0x7fffffff, "avr_head_fwd: too many columns");
     const char* dbg_env = getenv("AVR_HEAD_BAND_DBG");  // experiments only
     const int dbg = dbg_env ? atoi(dbg_env) : 0;
-    const size_t lds = band_lds_bytes(R, T);
+    // AVR_HEAD_BAND_BUF=3: a 3-slot chunk ring (experiments)
+    const char* buf_env = getenv("AVR_HEAD_BAND_BUF");
+    const int nbuf = (buf_env && atoi(buf_env) == 3) ? 3 : kBandBuf;
+    const size_t lds = band_lds_bytes(R, T, nbuf);
     auto go = [&](auto kern, auto e) {
         using E = decltype(e);
         allow_lds(kern, lds);
         hipLaunchKernelGGL(kern, dim3((unsigned)items), dim3(64 * kBandWaves), lds, st, p, B, R, K, nq, kbw,
                            (const E*)h, (const E*)Wp, perm, ws, cnt, zpart, dbg);
     };
-    if (dtype == AVR_DTYPE_F16)
-        go(head_band_fwd_kernel<__half>, __half{});
-    else
-        go(head_band_fwd_kernel<__hip_bfloat16>, __hip_bfloat16{});
+    if (dtype == AVR_DTYPE_F16) {
+        if (nbuf == 3)
+            go(head_band_fwd_kernel<__half, 3>, __half{});
+        else
+            go(head_band_fwd_kernel<__half>, __half{});
+    } else {
+        if (nbuf == 3)
+            go(head_band_fwd_kernel<__hip_bfloat16, 3>, __hip_bfloat16{});
+        else
+            go(head_band_fwd_kernel<__hip_bfloat16>, __hip_bfloat16{});
+    }
     return check_launch("avr_head_fwd (band)");
 }
 

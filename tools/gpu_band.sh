@@ -1,5 +1,5 @@
 #!/bin/bash
-# Band-form linear head: partial check, head tests, probe timing (rings) and
+# Band-form linear head: partial check, head tests, probe timing and
 # kernel stats at config 2.  Stops at the first failing step.
 set -u
 OUT=gpurun_out/band

@@ -29,10 +29,10 @@ def main():
     ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"])
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--forms", default="1,0")
-    ap.add_argument("--rings", default="0", help="AVR_HEAD_BAND_RING values to time the band form at")
     ap.add_argument("--dbgs", default="0", help="AVR_HEAD_BAND_DBG values (timing experiments)")
     ap.add_argument("--reps", type=int, default=1, help="repetitions of the whole set, interleaved")
     ap.add_argument("--warmup", type=int, default=0, help="untimed renders of each form before any timing")
+    ap.add_argument("--bufs", default="4", help="AVR_HEAD_BAND_BUF values for the band form")
     args = ap.parse_args()
     dt = torch.float16 if args.dtype == "fp16" else torch.bfloat16
     dev = torch.device("cuda", 0)
@@ -48,7 +48,7 @@ def main():
     W = torch.randn(T, K, device=dev, generator=g) / K ** 0.5
     outs = {}
     with torch.no_grad():
-        runs = [(f, rg, d) for f in args.forms.split(",") for rg in (args.rings.split(",") if f == "1" else ["0"])
+        runs = [(f, rg, d) for f in args.forms.split(",") for rg in (args.bufs.split(",") if f == "1" else ["4"])
                 for d in (args.dbgs.split(",") if f == "1" else ["0"])] * args.reps
         for _ in range(args.warmup):  # clocks up before anything is timed
             for f in args.forms.split(","):
@@ -57,7 +57,7 @@ def main():
         torch.cuda.synchronize()
         for form, ring, dbg in runs:
             os.environ["AVR_HEAD_BAND"] = form
-            os.environ["AVR_HEAD_BAND_RING"] = ring
+            os.environ["AVR_HEAD_BAND_BUF"] = ring
             os.environ["AVR_HEAD_BAND_DBG"] = dbg
             for _ in range(3):
                 out = r.render_from_hidden(attn, h, W, dt, geom)
@@ -70,7 +70,7 @@ def main():
             e1.synchronize()
             if dbg == "0":
                 outs[form] = out.double().cpu()
-            print(json.dumps({"workload": w.name, "K": K, "dtype": args.dtype, "band": int(form), "ring": int(ring), "dbg": int(dbg),
+            print(json.dumps({"workload": w.name, "K": K, "dtype": args.dtype, "band": int(form), "chunk_slots": int(ring), "dbg": int(dbg),
                               "render_ms": e0.elapsed_time(e1) / args.iters}), flush=True)
     os.environ.pop("AVR_HEAD_BAND", None)
     if "1" in outs and "0" in outs:
