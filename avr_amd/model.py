@@ -164,13 +164,12 @@ class _LinearReLU(torch.autograd.Function):
     def forward(ctx, x, w_master, dtype, cache=False):
         w = cast_weight(w_master, dtype, cache)
         y = _linear_relu_hip(x, w) if x.is_cuda else None
-        if y is not None:
-            pass
-        elif x.is_cuda:
-            y = torch._addmm_activation(_zero_bias(w.size(0), dtype, x.device), x, w.t(),
-                                        use_gelu=False)
-        else:
-            y = torch.relu(x @ w.t())
+        if y is None:
+            if x.is_cuda:
+                y = torch._addmm_activation(_zero_bias(w.size(0), dtype, x.device), x, w.t(),
+                                            use_gelu=False)
+            else:
+                y = torch.relu(x @ w.t())
         ctx.save_for_backward(x, w, y)
         return y
 
