@@ -705,6 +705,170 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 }
 
+// Two t-tiles per wave (AVR_HEAD_EXACT_WAVES 20, K = 512): the persistent
+// LDS-DMA form with 4 waves of 64 t instead of 8 waves of 32, one wave per
+// SIMD.  Each A fragment read from LDS feeds two MFMAs (one per t-tile), so
+// the LDS reads per MFMA halve: in the 8-wave form the row stream (127 us
+// alone) and the MFMA chains (119 us alone) add up at config 2 (254 us),
+// because the chains' fragment reads keep LDS busy while the next tile's
+// DMA wants to land.  W fragments of both tiles stay in registers (256).
+template <typename E>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void head_exact_w2_kernel(
+    avr_render_params pp, int B, int R, int K, const E* __restrict__ h, const E* __restrict__ W,
+    const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
+    float* __restrict__ z, int ntb, int per_xcd) {
+    constexpr int KS = 32, WAVES = 4, NT = 256, TB = 256, TR = 64, RPW = TR / WAVES;
+    constexpr int ROWB = a_row_bytes(KS);
+    extern __shared__ __attribute__((aligned(16))) char lds_x[];
+    char* abuf = lds_x;  // [2][TR][ROWB]
+    int* pl = reinterpret_cast<int*>(lds_x + 2 * TR * ROWB);
+    float* wl = reinterpret_cast<float*>(pl + (R + TR - 1) / TR * TR);
+
+    const int T = pp.T, S = pp.n_samples;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int half = lane >> 5, j = lane & 31;
+    const int64_t ncol = (int64_t)B * S;
+    const int x = blockIdx.x & 7, m = blockIdx.x >> 3;
+    const int nq = per_xcd / ntb;
+    const int64_t cpx = (ncol + 7) / 8;
+    const int tb = m % ntb;
+    const int64_t c_first = (int64_t)x * cpx + m / ntb, c_step = nq;
+    const int64_t c_end = min(ncol, (int64_t)(x + 1) * cpx);
+    const int t0 = tb * TB + wave * 64;
+
+    frag8 wf[2][KS];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const E* wrow = W + (int64_t)min(t0 + 32 * q + j, T - 1) * K + 8 * half;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) wf[q][ks] = *reinterpret_cast<const frag8*>(wrow + 16 * ks);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) asm volatile("" ::"v"(wf[q][ks]));
+    const int64_t hstride = (int64_t)S * K;
+
+    for (int64_t col = c_first; col < c_end; col += c_step) {
+        __syncthreads();  // the previous column's LDS reads are done
+        const int s = (int)(col % S), b = (int)(col / S);
+        const int lim = tail_limit(pp, s);
+        float* zcol = z + col * T;
+        const int tl = min(tb * TB + TB, lim) - 1;
+        if (tl < tb * TB) {
+            for (int i = threadIdx.x; i < TB; i += NT)
+                if (tb * TB + i < T) zcol[tb * TB + i] = 0.0f;
+            continue;
+        }
+        const int* cc = cnt + col * T;
+        const int nblk = cc[tl];
+        int cnt_t[2], cwq[2], cfull[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int tq0 = t0 + 32 * q, tq = tq0 + j;
+            cnt_t[q] = tq < lim ? cc[tq] : 0;
+            cwq[q] = __builtin_amdgcn_readfirstlane(tq0 < lim ? cc[min(tq0 + 31, lim - 1)] : 0);
+            cfull[q] = __builtin_amdgcn_readfirstlane(tq0 + 31 < lim ? cc[tq0] : 0);
+        }
+        const int ntile = (nblk + TR - 1) / TR;
+        for (int pq = threadIdx.x; pq < nblk; pq += NT) {
+            pl[pq] = perm[col * R + pq];
+            wl[pq] = ws[col * R + pq];
+        }
+        __syncthreads();
+        for (int pq = nblk + (int)threadIdx.x; pq < ntile * TR; pq += NT) {
+            pl[pq] = pl[nblk - 1];
+            wl[pq] = 0.0f;
+        }
+        __syncthreads();
+        const E* hcol = h + ((int64_t)b * R * S + s) * K + 8 * lane;
+        auto issue = [&](int tile) {
+            const int p0 = tile * TR + wave * RPW;
+            char* a = abuf + (tile & 1) * TR * ROWB + wave * RPW * ROWB;
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                const int rr = __builtin_amdgcn_readfirstlane(pl[p0 + r]);
+                dma_row16(hcol + (int64_t)rr * hstride, (uint32_t)(uintptr_t)(a + r * ROWB));
+            }
+        };
+        float zl[2] = {0.0f, 0.0f};
+        auto epilogue = [&](const f32x16& acc, int q, int p0) {
+            if (p0 + 32 <= cfull[q]) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const float4 wv = *reinterpret_cast<const float4*>(wl + p0 + 8 * g + 4 * half);
+                    zl[q] = fmaf(wv.x, round16<E>(acc[4 * g + 0]), zl[q]);
+                    zl[q] = fmaf(wv.y, round16<E>(acc[4 * g + 1]), zl[q]);
+                    zl[q] = fmaf(wv.z, round16<E>(acc[4 * g + 2]), zl[q]);
+                    zl[q] = fmaf(wv.w, round16<E>(acc[4 * g + 3]), zl[q]);
+                }
+                return;
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 wv = *reinterpret_cast<const float4*>(wl + p0 + 8 * g + 4 * half);
+                const float w4[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int p = p0 + e + 8 * g + 4 * half;
+                    zl[q] = fmaf((p < cnt_t[q]) ? w4[e] : 0.0f, round16<E>(acc[4 * g + e]), zl[q]);
+                }
+            }
+        };
+        constexpr int kDepth = 4;
+        // one 32-ray sub-tile: both t-tiles' chains from the same fragments
+        // (NQ = 2), or only the second's when the first needs none of these rays
+        auto chain = [&](auto nq_tag, const char* a, int p0) {
+            constexpr int NQ = decltype(nq_tag)::value;
+            f32x16 acc[2];
+            acc[0] = f32x16{};
+            acc[1] = f32x16{};
+            frag8 fr[kDepth];
+#pragma unroll
+            for (int i = 0; i < kDepth; ++i) fr[i] = *reinterpret_cast<const frag8*>(a + 32 * i);
+#pragma unroll
+            for (int n = 0; n < KS; ++n) {
+                if constexpr (NQ == 2) acc[0] = mfma16<E>(fr[n % kDepth], wf[0][n], acc[0]);
+                acc[1] = mfma16<E>(fr[n % kDepth], wf[1][n], acc[1]);
+                if (n + kDepth < KS) fr[n % kDepth] = *reinterpret_cast<const frag8*>(a + 32 * (n + kDepth));
+            }
+            if constexpr (NQ == 2) epilogue(acc[0], 0, p0);
+            epilogue(acc[1], 1, p0);
+        };
+        issue(0);
+#define AVR_W2VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 0xF) | (0x7 << 4) | (0xF << 8) | (((N) >> 4) << 14))
+        AVR_W2VMCNT(0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        for (int it = 0; it < ntile; ++it) {
+            if (it + 1 < ntile) issue(it + 1);  // into the buffer tile it - 1 used
+            const char* a0 = abuf + (it & 1) * TR * ROWB + j * ROWB + 16 * half;
+#pragma unroll
+            for (int q0 = 0; q0 < TR / 32; ++q0) {
+                const int p0 = it * TR + 32 * q0;
+                if (p0 < cwq[0])
+                    chain(std::integral_constant<int, 2>{}, a0 + q0 * 32 * ROWB, p0);
+                else if (p0 < cwq[1])
+                    chain(std::integral_constant<int, 1>{}, a0 + q0 * 32 * ROWB, p0);
+            }
+            if (it + 1 < ntile) {
+                AVR_W2VMCNT(0);                       // tile it + 1's rows from this wave have landed
+                __builtin_amdgcn_s_waitcnt(0xC07F);  // and every LDS read of tile it is done
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+            }
+        }
+#undef AVR_W2VMCNT
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const float other = __shfl_xor(zl[q], 32, 64);
+            const int tq = t0 + 32 * q + j;
+            if (half == 0 && tq < T) zcol[tq] = (tq < lim) ? zl[q] + other : 0.0f;
+        }
+    }
+}
+
 int exact_shape(const avr_render_params& p, int K, int* KS, int* waves) {
     if (K % 16 != 0 || K < 16 || K > 512) return fail(AVR_E_CONFIG, "exact head: K must be a multiple of 16, <= 512");
     const int ks = K / 16;
@@ -717,7 +881,7 @@ int exact_shape(const avr_render_params& p, int K, int* KS, int* waves) {
     int w = K == 512 ? 19 : 8;
     if (const char* e = getenv("AVR_HEAD_EXACT_WAVES")) {
         const int v = atoi(e);
-        w = (v == 4 || v == 8 || (v >= 16 && v <= 19)) ? v : 0;  // 16-19: the LDS-DMA forms (K = 512)
+        w = (v == 4 || v == 8 || (v >= 16 && v <= 20)) ? v : 0;  // 16-20: the LDS-DMA forms (K = 512)
     }
     if (w >= 16 && K != 512) w = 8;
     *waves = w;
@@ -748,7 +912,8 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
     const int64_t total = (int64_t)B * S * ntb;
     const int per_xcd = (int)((total + 7) / 8);
     const dim3 grid((unsigned)(8 * per_xcd));
-    // profiling only: 1 = no MFMA, 2 = no HBM stream (fp16, K = 512, 8 waves)
+    // profiling only: 1 = no MFMA, 2 = no HBM stream, 4 = no epilogue, 5 = the
+    // row stream alone (fp16, K = 512, the LDS-DMA forms 16-18)
     const char* dbg_env = getenv("AVR_HEAD_EXACT_DBG");
     const int dbg = dbg_env ? atoi(dbg_env) : 0;
     hipStream_t st = as_stream(stream);
@@ -762,6 +927,25 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
     using I32 = std::integral_constant<int, 32>;
     using I8 = std::integral_constant<int, 8>;
     using I4 = std::integral_constant<int, 4>;
+    if (waves == 20 && KS == 32 && K == 512) {  // two t-tiles per wave, persistent (one workgroup per CU)
+        const size_t lds = 2 * (size_t)64 * a_row_bytes(32) + 8 * (size_t)((R + 63) / 64 * 64);
+        int cus = 256, dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const int64_t ncol = (int64_t)B * S;
+        const int64_t want = ((ncol + 7) / 8) * ntb;
+        int wg_per_xcd = (int)std::min<int64_t>(want, std::max(1, cus / 8));
+        wg_per_xcd = std::max(ntb, wg_per_xcd / ntb * ntb);
+        auto go_w2 = [&](auto kern, auto hp) {
+            allow_lds(kern, lds);
+            hipLaunchKernelGGL(kern, dim3((unsigned)(8 * wg_per_xcd)), dim3(256), lds, st, *p, (int)B, R, (int)K, hp,
+                               (decltype(hp))W, perm, ws, cnt, z, ntb, wg_per_xcd);
+        };
+        if (dtype == AVR_DTYPE_F16)
+            go_w2(head_exact_w2_kernel<__half>, (const __half*)h);
+        else
+            go_w2(head_exact_w2_kernel<__hip_bfloat16>, (const __hip_bfloat16*)h);
+        return check_launch("avr_head_fwd_exact");
+    }
     if (waves >= 16 && KS == 32 && K == 512) {  // LDS-DMA forms (16: 32-ray tiles x 3 buffers, 17: 64 x 2, 18: 32 x 4,
                                                 // 19: 64 x 2 persistent)
         const int TRv = (waves == 17 || waves == 19) ? 64 : 32, NB = waves == 16 ? 3 : (waves == 18 ? 4 : 2);
@@ -805,6 +989,7 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
             else if (dbg == 2) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 2>, (const __half*)h);   \
             else if (dbg == 3) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 3>, (const __half*)h);   \
             else if (dbg == 4) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 4>, (const __half*)h);   \
+            else if (dbg == 5) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 5>, (const __half*)h);   \
             else if (dbg == 6) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 6>, (const __half*)h);   \
             else if (dbg == 8) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 8>, (const __half*)h);   \
             else if (dbg == 12) go_dma(head_exact_dma_kernel<__half, TRV, NBV, 12>, (const __half*)h); \
