@@ -113,25 +113,11 @@ __device__ __forceinline__ void store_pair<__half>(__half* out, int64_t i, float
 }
 
 // avr_hashgrid_fwd switches to the level-major dispatch from this many points
-// (AVR_HASHGRID_LM_MIN overrides; experiments)
-constexpr int64_t kLevelMajorMinPointsDefault = 16384;
-inline int64_t lm_min_points() {
-    static const int64_t v = [] {
-        const char* e = getenv("AVR_HASHGRID_LM_MIN");
-        return e ? (int64_t)atoll(e) : kLevelMajorMinPointsDefault;
-    }();
-    return v;
-}
+constexpr int64_t kLevelMajorMinPoints = 16384;
+inline int64_t lm_min_points() { return kLevelMajorMinPoints; }
 
-// grouped corner loads in the level-major forward (AVR_HASHGRID_GROUP=0
-// turns them off; experiments)
-inline bool group_loads() {
-    static const bool v = [] {
-        const char* e = getenv("AVR_HASHGRID_GROUP");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
+// grouped corner loads in the level-major forward (fp16 tables, §9b)
+inline bool group_loads() { return true; }
 
 struct Corner {
     float pos[3];
@@ -362,13 +348,8 @@ __global__ __launch_bounds__(256) void hashgrid_bwd_kernel(int64_t N, int L, int
     if (pv != 0.0f) atomicAdd(table + pe, pv);
 }
 
-// points walked per 16-lane group (AVR_HASHGRID_BWD_RUN overrides: 1, 4, 8,
-// 16 or 32; experiments)
-inline int bwd_run() {
-    const char* e = getenv("AVR_HASHGRID_BWD_RUN");
-    const int v = e ? atoi(e) : 16;
-    return (v == 1 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 16;
-}
+// points walked per 16-lane group
+inline int bwd_run() { return 16; }
 
 template <typename Tg>
 void launch_bwd(hipStream_t st, int64_t N, int L, const float* x, const Tg* gout, const LevelTable& lt,
@@ -689,8 +670,7 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
                                                                          const int* __restrict__ part_start,
                                                                          const int* __restrict__ slice_base,
                                                                          const uint3* __restrict__ contrib,
-                                                                         float* __restrict__ gparams, int dbg,
-                                                                         unsigned long long* __restrict__ dbg_out) {
+                                                                         float* __restrict__ gparams) {
     __shared__ float2 img_all[kReduceWaves][kPartEntries];
     __shared__ uint8_t tag_all[kReduceWaves][kPartEntries];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -708,8 +688,6 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
     const int ns = slice_base[p + 1] - slice_base[p], sl = b - slice_base[p];
     const int n = totals[p];
     if (n == 0) return;  // wave-uniform
-    const unsigned long long t_start = (dbg & 4) ? __builtin_readcyclecounter() : 0ull;
-    unsigned long long n_iter = 0;
     const int i0 = part_start[p] + (int)((int64_t)n * sl / ns);
     const int i1 = part_start[p] + (int)((int64_t)n * (sl + 1) / ns);
     int l = 0;
@@ -729,13 +707,6 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
             const uint3 cv = contrib[j < i1 ? j : i0];
             kk[u] = j < i1 ? cv.x : 0u;
             v[u] = j < i1 ? make_float2(__uint_as_float(cv.y), __uint_as_float(cv.z)) : make_float2(0.f, 0.f);
-        }
-        if (dbg & 1) {  // timing experiment: no adds
-            float t = 0.f;
-#pragma unroll
-            for (int u = 0; u < U; ++u) t += v[u].x + v[u].y + (float)kk[u];
-            if (t == 12345.f) img[0].x = t;
-            continue;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -776,18 +747,10 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
                 asm volatile("" ::: "memory");
                 todo = todo && !mine;
                 rest = __ballot(todo);
-                ++n_iter;
             }
         }
     }
-    if ((dbg & 4) && lane == 0) {  // diagnostics: slowest slice, butterfly iterations
-        const unsigned long long dt = __builtin_readcyclecounter() - t_start;
-        atomicMax(dbg_out, (dt << 24) | (unsigned long long)b);
-        atomicAdd(dbg_out + 1, n_iter);
-        atomicAdd(dbg_out + 2, (unsigned long long)(i1 - i0));
-    }
     float* dstf = gparams + 2 * (lt.offset[l] + e0);
-    if (dbg & 2) return;  // timing experiment: no flush
     const float4* img4 = reinterpret_cast<const float4*>(img);
     if (ns == 1) {  // the wave owns these entries: plain read-add-write
         float4* dst = reinterpret_cast<float4*>(dstf);
@@ -810,7 +773,7 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
 struct BwdLayout {
     BwdPlan plan;
     int total_parts;
-    int64_t counts, totals, part_start, slice_base, contrib, dbg, bytes;  // byte offsets in the workspace
+    int64_t counts, totals, part_start, slice_base, contrib, bytes;  // byte offsets in the workspace
     int max_slices;  // reduce grid: total_parts + maxc / kDenseSlice bounds the slice count
     bool scatter_ok; // the largest level's partition table fits the count/scatter LDS
 };
@@ -858,8 +821,6 @@ int bwd_layout(int64_t N, int L, const int64_t* off, const int32_t* res, BwdLayo
     b.scatter_ok = b.plan.max_parts <= kMaxScatterParts;
     b.contrib = o0;  // (key, v0, v1) per contribution
     o0 += al(maxc * 12);
-    b.dbg = o0;  // 3 counters of the reduce pass's diagnostics (AVR_HG_BWD_DBG & 4)
-    o0 += 256;
     b.bytes = o0;
     *o = b;
     return 0;
@@ -1160,7 +1121,6 @@ extern "C" int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const f
                            (const __half*)grad_out, lt, b.plan, counts, part_start, contrib);
     hipLaunchKernelGGL(hg_bwd_reduce_kernel, dim3((unsigned)((b.max_slices + kReduceWaves - 1) / kReduceWaves)),
                        dim3(64 * kReduceWaves), 0, st, L, lt, b.plan, b.total_parts, totals, part_start, slice_base,
-                       contrib, grad_params, getenv("AVR_HG_BWD_DBG") ? atoi(getenv("AVR_HG_BWD_DBG")) : 0,
-                       reinterpret_cast<unsigned long long*>(ws + b.dbg));
+                       contrib, grad_params);
     return check_launch("avr_hashgrid_bwd_partitioned");
 }

@@ -30,14 +30,6 @@
 
 using namespace avr;
 
-namespace avr {
-// head_band.hip: the band form of the forward for 16-bit h
-int head_band_slices(const avr_render_params& p, int K, int es, int kbw);
-int head_band_fwd(const avr_render_params& p, int B, int K, const void* h, const void* Wp, int dtype, int kbw,
-                  const int32_t* perm, const float* ws, const int32_t* cnt, int nq, float* zpart,
-                  hipStream_t st);
-}  // namespace avr
-
 namespace {
 
 constexpr int kThreads = 256;
@@ -579,7 +571,7 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp
                                                             const int* __restrict__ perm,
                                                             const float* __restrict__ ws,
                                                             const int* __restrict__ cnt,
-                                                            float* __restrict__ zpart, int dbg) {
+                                                            float* __restrict__ zpart) {
     extern __shared__ float lds_f[];
     const int T = pp.T, S = pp.n_samples;
     const int kg = blockIdx.x, s = blockIdx.y, b = blockIdx.z;
@@ -605,7 +597,7 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
             const int t = threadIdx.x + kThreads * i;
-            if (t < lim && !(dbg & 4)) {
+            if (t < lim) {
                 float a = zacc[i];
 #pragma unroll
                 for (int k = 0; k < KB; ++k) a = fmaf(wt[i][k], C[k * RS + 3 + ct[i]], a);
@@ -619,7 +611,7 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp
         Raw<Th, KB> hv[RPT];
         load_sorted_rows<Th, KB, RPT>(hv, h, hrow0, hstride, kbeg, own);
         for (int k0 = kbeg; k0 < kend; k0 += KB) {
-            if (!(dbg & 1)) build_cumsum<Th, KB, RPT>(C, R, own.n, own.spt, own.w, hv, wtotf);
+            build_cumsum<Th, KB, RPT>(C, R, own.n, own.spt, own.w, hv, wtotf);
             if (k0 + KB < kend) load_sorted_rows<Th, KB, RPT>(hv, h, hrow0, hstride, k0 + KB, own);
             lds_barrier();
             contract(k0);
@@ -641,7 +633,7 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp
                 for (int u = 0; u < RPT; ++u)
 #pragma unroll
                     for (int d = 0; d < ND; ++d) hv[u].d[d] = big[u].d[sb * ND + d];
-                if (!(dbg & 1)) build_cumsum<Th, KB, RPT>(C, R, own.n, own.spt, own.w, hv, wtotf);
+                build_cumsum<Th, KB, RPT>(C, R, own.n, own.spt, own.w, hv, wtotf);
                 lds_barrier();
                 contract(k0 + sb * KB);
             }
@@ -951,16 +943,13 @@ void dw_groups(const HeadShape& hs, int B, int S, int K, int* n_sg, int* s_per) 
 // feature blocks of <= 8 (C[kb][RS] of 33 KB: 4 workgroups per CU instead of
 // 2) and SB blocks per row load (4 while the t slots leave the registers:
 // NT <= 4, else 2): config 2 0.36 -> 0.24 ms, config 3 0.17 -> 0.16 ms for
-// the render with the head.  AVR_HEAD_KB / AVR_HEAD_SB override (experiments).
+// the render with the head.
 void fwd_block(const HeadShape& hs, int dtype, int* kb, int* sb) {
     int kbf = hs.kb, s = 1;
     if (elem_size(dtype) == 2 && hs.rpt <= 8) {
         kbf = hs.kb > 8 ? 8 : hs.kb;
         s = hs.nt <= 4 ? 4 : 2;
-        if (const char* e = getenv("AVR_HEAD_KB")) kbf = atoi(e);
-        if (const char* e = getenv("AVR_HEAD_SB")) s = atoi(e);
-        if ((kbf != 4 && kbf != 8 && kbf != 16) || kbf > hs.kb) kbf = hs.kb;
-        if ((s != 1 && s != 2 && s != 4) || hs.kg % (s * kbf) != 0) s = 1;
+        if (hs.kg % (s * kbf) != 0) s = 1;
     }
     *kb = kbf;
     *sb = s;
@@ -996,12 +985,8 @@ extern "C" int avr_head_splits(const avr_render_params* p, int32_t B, int32_t K,
                                int32_t* n_split) {
     AVR_REQUIRE(p && n_split, "avr_head_splits: bad args");
     HeadShape hs;
-    const int es = elem_size(dtype);
-    if (int e = head_shape(*p, B, n_rays(*p), K, es, &hs)) return e;
-    int kbf, sb;
-    fwd_block(hs, dtype, &kbf, &sb);
-    const int nq = head_band_slices(*p, K, es, kbf);
-    *n_split = nq > 0 ? nq : hs.n_kg;
+    if (int e = head_shape(*p, B, n_rays(*p), K, elem_size(dtype), &hs)) return e;
+    *n_split = hs.n_kg;
     return 0;
 }
 
@@ -1037,21 +1022,15 @@ extern "C" int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, co
     hipStream_t st = as_stream(stream);
     int kbf, sb;
     fwd_block(hs, dtype, &kbf, &sb);
-    if (const int nq = head_band_slices(*p, K, elem_size(dtype), kbf)) {
-        AVR_REQUIRE(n_split == nq, "avr_head_fwd: n_split must come from avr_head_splits");
-        return head_band_fwd(*p, B, K, h, W, dtype, kbf, perm, ws, cnt, nq, zpart, st);
-    }
     AVR_REQUIRE(n_split == hs.n_kg, "avr_head_fwd: n_split must come from avr_head_splits");
     const dim3 grid(hs.n_kg, p->n_samples, B);
-    const char* dbg_env = getenv("AVR_HEAD_DBG");  // profiling only: skip phases
-    const int dbg = dbg_env ? atoi(dbg_env) : 0;
     HeadShape hf = hs;
     hf.kb = kbf;
     hf.lds_c = cumsum_lds_bytes(R, kbf);
     auto go = [&](auto kern, auto hp, auto wp) {
         allow_lds(kern, hf.lds_c);
         hipLaunchKernelGGL(kern, grid, dim3(kThreads), hf.lds_c, st, *p, (int)B, R, (int)K, hf.kg, hp, wp,
-                           perm, ws, cnt, zpart, dbg);
+                           perm, ws, cnt, zpart);
     };
 #define AVR_HF(TH, KBV, NTV, RP)                                                                   \
     if (hf.kb == KBV && hf.nt == NTV && hf.rpt == RP) {                                            \
@@ -1132,9 +1111,7 @@ extern "C" int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, co
                                (const float*)W, (float*)Wb);
     }
     // 16-bit h: h loads / grad_h stores 2 feature blocks (32 B) per row
-    // (AVR_HEAD_BSB=1 restores one block; experiments)
-    int bsb = (elem_size(dtype) == 2 && hs.kg % (2 * hs.kb) == 0) ? 2 : 1;
-    if (const char* e = getenv("AVR_HEAD_BSB")) bsb = (atoi(e) == 2 && hs.kg % (2 * hs.kb) == 0) ? 2 : 1;
+    const int bsb = (elem_size(dtype) == 2 && hs.kg % (2 * hs.kb) == 0) ? 2 : 1;
     auto go_h = [&](auto kern, auto hp, auto wp, auto gp) {
         allow_lds(kern, hs.lds_q);
         hipLaunchKernelGGL(kern, dim3(hs.n_kg, S, B), dim3(kThreads), hs.lds_q, st, *p, (int)B, R, (int)K,

@@ -206,14 +206,9 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(int64_t MK, int spl
     }
 }
 
-int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return v && *v ? atoi(v) : dflt;
-}
-
 int wgrad_splits(int64_t N, int M, int K) {
     const int tiles = ((M + kTile - 1) / kTile) * ((K + kTile - 1) / kTile);
-    const int target = env_int("AVR_WGRAD_WGS", 512);  // ~2 workgroups per CU
+    const int target = 512;  // ~2 workgroups per CU
     int splits = (target + tiles - 1) / tiles;
     const int64_t max_by_rows = N / 256 > 1 ? N / 256 : 1;  // >= 8 slabs per split
     return (int)(splits < max_by_rows ? splits : max_by_rows);
@@ -240,7 +235,7 @@ extern "C" int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* gra
     const int used = (int)((N + rows - 1) / rows);
     hipStream_t st = as_stream(stream);
     const int tiles = ((K + kTile - 1) / kTile) * ((M + kTile - 1) / kTile);
-    const int xcd_map = env_int("AVR_WGRAD_XCD", 1);
+    const int xcd_map = 1;  // all tiles of a split on one XCD (its rows re-read from that L2)
     const int64_t blocks = xcd_map ? (int64_t)tiles * ((used + 7) / 8 * 8) : (int64_t)tiles * used;
     hipLaunchKernelGGL(linear_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, N, (int)M, (int)K, rows,
                        used, xcd_map, (const __hip_bfloat16*)grad_y, (const __hip_bfloat16*)x, workspace);

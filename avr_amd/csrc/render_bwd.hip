@@ -426,8 +426,7 @@ int launch_rb(const avr_render_params* p, int B, const void* sig, const float* g
     const int64_t wps = (int64_t)groups * B * (threads / 64);
     // no partials in the backward, so splits cost only a gz re-read from L2:
     // take many (best at the 256-split cap, profiles/r01_tune_bwd_*.jsonl)
-    int64_t waves_target = 262144;
-    if (const char* e = getenv("AVR_RB_WAVES")) waves_target = atoll(e);  // tuning override
+    const int64_t waves_target = 262144;
     auto rps_of = [&](int k) { return (R + k - 1) / k; };
     while (n < 256 && (n * wps < waves_target || rps_of(n) * G > kMaxRbRays) && rps_of(2 * n) >= 4) n *= 2;
     const int rps = rps_of(n);
@@ -437,8 +436,7 @@ int launch_rb(const avr_render_params* p, int B, const void* sig, const float* g
     const size_t lds = (size_t)3 * G * max(rps, 1) * 4;
     const Tin* x = (const Tin*)sig;
     Tin* gx = (Tin*)gsig;
-    const char* nts_env = getenv("AVR_RB_NTS");  // tuning override: 0 = plain stores
-    const bool nts = !(nts_env && atoi(nts_env) == 0);
+    const bool nts = true;  // streaming grad_x stores (profiles/r01_tune_bwd_*.jsonl)
 #define AVR_RB_L(C, GG, MT, NTS)                                                                   \
     hipLaunchKernelGGL((ray_reduce_bwd_kernel<Tin, VECTOR, C, GG, MT, NTS>), grid, dim3(threads),  \
                        lds, st, *p, x, gz, w, delay, gx, gw, B, R, S, T, rps, total)

@@ -1031,13 +1031,10 @@ extern "C" int avr_weights_fwd(const avr_render_params* p, int32_t B, const void
 }
 
 namespace {
-// Streaming variant of the reduction: rows in flight per lane with
-// non-temporal loads.  AVR_REDUCE_VARIANT="u8nt" selects 8 rows for tuning
-// runs; the default "u4nt" is the best of the sweeps (profiles/r01_tune*).
-int reduce_variant() {
-    const char* v = getenv("AVR_REDUCE_VARIANT");
-    return (v && std::string(v) == "u8nt") ? 3 : 2;
-}
+// Streaming variant of the reduction: 4 rows in flight per lane with
+// non-temporal loads, the best of the sweeps (profiles/r01_tune*; 8 rows is
+// variant 3).
+int reduce_variant() { return 2; }
 
 struct ReduceShape {
     int G, cpt, threads;
@@ -1052,10 +1049,6 @@ ReduceShape reduce_shape(int S, int T) {
     // round-2 sweeps (profiles/r02_sweepG_*.jsonl: config 2 fp32 111.8 vs
     // 115.7 us per launch); fewer w/delay selects per loaded element
     sh.G = 1;
-    if (const char* g = getenv("AVR_REDUCE_G")) {  // tuning override (1, 2 or 4)
-        const int v = atoi(g);
-        if ((v == 1 || v == 2 || v == 4) && v <= S) sh.G = v;
-    }
     int max_phase = 0;  // group starts are s0 = multiples of G; S*T % VEC == 0
     for (int s0 = 0; s0 < S && s0 < VEC * sh.G; s0 += sh.G)
         max_phase = max(max_phase, (int)(((int64_t)s0 * T) % VEC));
@@ -1126,9 +1119,13 @@ extern "C" int avr_reduce_splits(const avr_render_params* p, int32_t B, int32_t 
     const int vec = (sig_dtype == AVR_DTYPE_F16 || sig_dtype == AVR_DTYPE_BF16) ? 8 : 4;
     const ReduceShape sh = vec == 8 ? reduce_shape<8>(S, T) : reduce_shape<4>(S, T);
     const int groups = (S + sh.G - 1) / sh.G;
-    if (const char* f = getenv("AVR_NSPLIT")) {  // tuning override
-        *n_split = atoi(f);
-        return 0;
+    auto rps = [&](int k) { return (R + k - 1) / k; };
+    if (const char* f = getenv("AVR_NSPLIT")) {  // validated tuning knob: 1, 2, 4, 8 or 16 ray splits
+        const int v = atoi(f);
+        if ((v == 1 || v == 2 || v == 4 || v == 8 || v == 16) && v <= R && rps(v) * sh.G <= kMaxGroupRays) {
+            *n_split = v;
+            return 0;
+        }
     }
     // power of two <= 16 (the DFT staging is templated on it) giving ~8 (fp32)
     // or ~16 (fp16: twice the VALU work per byte) resident waves per CU, and
@@ -1137,7 +1134,6 @@ extern "C" int avr_reduce_splits(const avr_render_params* p, int32_t B, int32_t 
     const int64_t waves_target = (vec == 8) ? 4096 : 1536;
     const int64_t waves_per_split = (int64_t)groups * B * (sh.threads / 64);
     int n = 1;
-    auto rps = [&](int k) { return (R + k - 1) / k; };
     while (n < 16 && (n * waves_per_split < waves_target || rps(n) * sh.G > kMaxGroupRays) &&
            rps(2 * n) >= 8)
         n *= 2;
@@ -1293,7 +1289,7 @@ CoreLayout core_layout(const avr_render_params* p, int B, int sig_dtype) {
     L.n_split = ns;
     const int nkc = (int)((T + kKc - 1) / kKc);
     int ks = 1;
-    if (const char* f = getenv("AVR_KSPLIT")) {
+    if (const char* f = getenv("AVR_KSPLIT")) {  // validated tuning knob: DFT k-slices, clamped to [1, T/kKc]
         ks = atoi(f);
     } else {
         const int64_t base = ((F + 127) / 128) * ((S + 31) / 32) * B;
@@ -1362,8 +1358,6 @@ extern "C" int avr_render_core_fwd(const avr_render_params* p, int32_t B, const 
         return e;
     if (ir) {
         AVR_REQUIRE(tab->ir_twiddle, "avr_render_core_fwd: ir requested without ir_twiddle");
-        const char* e = getenv("AVR_SPECTRUM_IR");  // 1: finalize + irfft in one launch (experiment)
-        if (e && e[0] == '1') return avr_spectrum_ir(B, L.P, p->T / 2 + 1, spart, tab->ir_twiddle, out, ir, stream);
         if (int e2 = avr_spectrum_finalize(B, L.P, p->T / 2 + 1, spart, out, stream)) return e2;
         return avr_irfft(B, p->T / 2 + 1, out, tab->ir_twiddle, ir, stream);
     }

@@ -125,29 +125,41 @@ def _zero_bias(n, dtype, device):
 
 
 # AVR_LINEAR=1 runs the width-512 hidden layers on csrc/linear_fwd.hip
-# (opt-in: as fast as hipBLASLt, not faster)
+# (opt-in until it measures faster than hipBLASLt)
 _LINEAR_HIP = os.environ.get("AVR_LINEAR", "0") == "1"
 
 
-def _linear_relu_hip(x, w):
+def _linear_relu_hip(x, w, w_master=None, cache=False):
     """relu(x W^T) for the width-512 hidden layers on the HIP MFMA kernel
     (csrc/linear_fwd.hip), or None when the shape is not its (16-bit, K = 512,
-    N a multiple of 256)."""
+    N a multiple of 32).  W is packed into MFMA-fragment order
+    (avr_linear_pack_w), cached on the master weight like its cast."""
     if not (_LINEAR_HIP and x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and w.dtype == x.dtype
-            and x.dim() == 2 and x.size(1) == 512 and w.size(1) == 512 and w.size(0) % 256 == 0
+            and x.dim() == 2 and x.size(1) == 512 and w.size(1) == 512 and w.size(0) % 32 == 0
             and x.is_contiguous() and w.is_contiguous() and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0):
         return None
     import ctypes
 
     from . import _lib
+    from .wcache import cache_lookup, cache_store, capturing
 
     M, N = x.size(0), w.size(0)
     y = torch.empty(M, N, dtype=x.dtype, device=x.device)
     if M == 0:
         return y
     code = _lib.DTYPE_F16 if x.dtype == torch.float16 else _lib.DTYPE_BF16
-    _lib.call("avr_linear_relu_fwd", M, N, 512, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(w.data_ptr()),
-              code, 1, ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+    st = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    owner = w_master if w_master is not None else w
+    key = (w.data_ptr(), owner._version, code)
+    use_cache = cache and not capturing()
+    wf = cache_lookup(owner, "_avr_linpack", key) if use_cache else None
+    if wf is None:
+        wf = torch.empty_like(w)
+        _lib.call("avr_linear_pack_w", N, 512, ctypes.c_void_p(w.data_ptr()), code, ctypes.c_void_p(wf.data_ptr()), st)
+        if use_cache:
+            cache_store(owner, "_avr_linpack", key, wf)
+    _lib.call("avr_linear_relu_fwd", M, N, 512, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(wf.data_ptr()),
+              code, 1, ctypes.c_void_p(y.data_ptr()), st)
     return y
 
 
@@ -163,7 +175,7 @@ class _LinearReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_master, dtype, cache=False):
         w = cast_weight(w_master, dtype, cache)
-        y = _linear_relu_hip(x, w) if x.is_cuda else None
+        y = _linear_relu_hip(x, w, w_master, cache) if x.is_cuda else None
         if y is None:
             if x.is_cuda:
                 y = torch._addmm_activation(_zero_bias(w.size(0), dtype, x.device), x, w.t(),

@@ -114,13 +114,11 @@ class RayShardedRender(nn.Module):
         try:
             u = broadcast_jitter(draw_jitter(r.n_azi, r.n_ele), self.group, rays_o.device,
                                  keep_on_device=rays_o.is_cuda)
-            pts, view, tx, dtx, geom = r.sample(rays_o, position_tx, direction_tx, u_azi=u)
-            kw = {} if ch_idx is None else {"ch_idx": ch_idx}
-            if dtx is not None:
-                attn, signal = r.network_fn(pts, view, tx, dtx, **kw)
-            else:
-                attn, signal = r.network_fn(pts, view, tx, **kw)
-            partial = r.render_from_network_output(attn, signal, geom)
+            # the renderer's own path on this rank's rays: the network is told
+            # the shard's ray layout (per-ray / per-pose encodings once) and a
+            # fused-head network renders through FusedHeadCore (the exact
+            # 16-bit head), exactly as an unsharded render
+            partial = r._render(rays_o, position_tx, direction_tx, ch_idx, None, u_azi=u)
         finally:
             r.ray_range = None
         if world == 1:

@@ -317,6 +317,21 @@ def _packed_head_weight(w_master, W, cache, pref, shape_key, st):
     return cache_store(w_master, "_avr_headpack", key, Wp) if cache else Wp
 
 
+def _packed_exact_weight(w_master, W, cache, pref, shape_key, nbytes, st):
+    """W in the exact head's MFMA-fragment order (avr_head_pack_w_exact),
+    cached on the master weight like _packed_head_weight."""
+    key = (W.data_ptr(), w_master._version, shape_key)
+    cache = cache and not capturing()
+    if cache:
+        hit = cache_lookup(w_master, "_avr_exactpack", key)
+        if hit is not None:
+            return hit
+    K, code = shape_key[1], shape_key[2]
+    Wf = torch.empty(nbytes // 2, dtype=W.dtype, device=W.device)
+    _lib.call("avr_head_pack_w_exact", pref, K, _ptr(W), code, _ptr(Wf), st)
+    return cache_store(w_master, "_avr_exactpack", key, Wf) if cache else Wf
+
+
 class FusedHeadCore(torch.autograd.Function):
     """Render core with the signal network's last linear layer folded in
     (kernels in csrc/head.hip).
@@ -346,10 +361,13 @@ class FusedHeadCore(torch.autograd.Function):
         if exact:
             # every signal element formed and rounded to the 16-bit type, as
             # the unfused layer (the reference network) outputs it
-            n_split = 1
-            part = torch.empty(1, B, S, T, dtype=torch.float32, device=dev)
-            _lib.call("avr_head_fwd_exact", pref, B, K, _ptr(h), _ptr(W), code, _ptr(perm), _ptr(ws), _ptr(cnt),
-                      _ptr(part), st)
+            ns, wbytes = ctypes.c_int32(0), ctypes.c_int64(0)
+            _lib.call("avr_head_exact_layout", pref, B, K, code, ctypes.byref(ns), ctypes.byref(wbytes))
+            n_split = ns.value
+            part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
+            Wf = _packed_exact_weight(w_master, W, cache, pref, (p.T, K, code), wbytes.value, st)
+            _lib.call("avr_head_fwd_exact", pref, B, K, _ptr(h), _ptr(Wf), code, _ptr(perm), _ptr(ws), _ptr(cnt),
+                      n_split, _ptr(part), st)
         else:
             ns = ctypes.c_int32(0)
             _lib.call("avr_head_splits", pref, B, K, code, ctypes.byref(ns))
@@ -649,8 +667,18 @@ class AVRRender(nn.Module):
         p = self._params(weight.size(0), geom["n_rays"])
         code = {torch.bfloat16: DTYPE_BF16, torch.float16: DTYPE_F16}.get(dtype, DTYPE_F32)
         n = ctypes.c_int32(0)
-        return _lib.load().avr_head_splits(ctypes_ref(p), geom["B"], h.size(-1), code,
-                                           ctypes.byref(n)) == 0
+        lib = _lib.load()
+        if lib.avr_head_splits(ctypes_ref(p), geom["B"], h.size(-1), code, ctypes.byref(n)) != 0:
+            return False
+        if self._exact_for(dtype, h.size(-1)):
+            nb = ctypes.c_int64(0)
+            return lib.avr_head_exact_layout(ctypes_ref(p), geom["B"], h.size(-1), code, ctypes.byref(n),
+                                             ctypes.byref(nb)) == 0
+        return True
+
+    def _exact_for(self, dtype, K):
+        """The output-rounding-exact head runs for 16-bit networks (csrc/head_exact.hip)."""
+        return self.exact_head and dtype in (torch.float16, torch.bfloat16) and K % 16 == 0 and K <= 512
 
     def render_from_hidden(self, attn, h, weight, dtype, geom):
         """Render core with the signal head fused (FusedHeadCore): `h` is the
@@ -671,8 +699,7 @@ class AVRRender(nn.Module):
         with _on(dev):
             tables = get_tables(p, dev)
             check_config(p, tables)
-            exact = (self.exact_head and dtype in (torch.float16, torch.bfloat16) and K % 16 == 0
-                     and K <= 512)
+            exact = self._exact_for(dtype, K)
             out = FusedHeadCore.apply(attn, h, weight, dtype, p, tables, geom["rays_o"],
                                       geom["position_tx"], geom["dirs"], not torch.is_grad_enabled(), exact)
             if self.propagate_nonfinite:
@@ -698,8 +725,11 @@ class AVRRender(nn.Module):
         out = self._render(rays_o, position_tx, direction_tx, ch_idx, None if grad else ir)
         return out, (ir[0] if ir else spectrum_to_ir(out))
 
-    def _render(self, rays_o, position_tx, direction_tx, ch_idx, ir_slot):
-        pts, view, tx, dtx, geom = self.sample(rays_o, position_tx, direction_tx)
+    def _render(self, rays_o, position_tx, direction_tx, ch_idx, ir_slot, u_azi=None):
+        """Sampling -> network -> render core; `u_azi` (the azimuth jitter,
+        host or device) replaces the CPU draw, as RayShardedRender passes
+        rank 0's broadcast draw so every ray shard sees one sphere."""
+        pts, view, tx, dtx, geom = self.sample(rays_o, position_tx, direction_tx, u_azi=u_azi)
         kw = {} if ch_idx is None else {"ch_idx": ch_idx}
         if getattr(self.network_fn, "accepts_ray_layout", False):
             # our own networks: tell them which inputs repeat over samples /

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import torch
 
-_CACHE_ATTRS = ("_avr_cast", "_avr_bias_cols", "_avr_headpack")
+_CACHE_ATTRS = ("_avr_cast", "_avr_bias_cols", "_avr_headpack", "_avr_exactpack", "_avr_linpack")
 
 
 def capturing() -> bool:

@@ -308,10 +308,12 @@ int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const float* x, co
 int avr_linear_wgrad_splits(int64_t N, int32_t M, int32_t K, int32_t* splits);
 /* y = relu(x W^T) (relu != 0) or x W^T: x [M, K] and W [N, K] (nn.Linear
  * layout) 16-bit (dtype fp16 / bf16), y [M, N] of the same type, fp32
- * accumulation and one rounding.  K = 512, N a multiple of 256 (the signal
- * network's hidden layers, model.py:176-180); x and W 16-byte aligned.
- * Used by avr_amd.model only with AVR_LINEAR=1 (as fast as hipBLASLt). */
-int avr_linear_relu_fwd(int64_t M, int32_t N, int32_t K, const void* x, const void* W, int32_t dtype,
+ * accumulation and one rounding.  K = 512, N a multiple of 32 (the signal
+ * network's hidden layers, model.py:176-180).  avr_linear_pack_w packs W
+ * into Wf (N*K 16-bit values, MFMA fragment order; once per weight update);
+ * x, Wf and y 16-byte aligned (csrc/linear_fwd.hip). */
+int avr_linear_pack_w(int32_t N, int32_t K, const void* W, int32_t dtype, void* Wf, void* stream);
+int avr_linear_relu_fwd(int64_t M, int32_t N, int32_t K, const void* x, const void* Wf, int32_t dtype,
                         int32_t relu, void* y, void* stream);
 int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* grad_y, const void* x,
                      float* workspace, int32_t splits, float* grad_w, void* stream);
@@ -416,24 +418,28 @@ int avr_head_sort(const avr_render_params* p, int32_t B, const float* w, const i
  * contiguously.  Wp is avr_head_fwd's W argument. */
 int avr_head_pack_w(const avr_render_params* p, int32_t B, int32_t K, const void* W, int32_t dtype,
                     void* Wp, void* stream);
-/* W: the packed weight from avr_head_pack_w (same p, B, K, dtype).  16-bit
- * h with K a multiple of 128 runs the delay-band form (csrc/head_band.hip;
- * n_split = K/128, which avr_head_splits then returns); AVR_HEAD_BAND=0 in
- * the environment selects the feature-block form (same sums, another fp32
- * order). */
+/* W: the packed weight from avr_head_pack_w (same p, B, K, dtype); the
+ * linear-algebra head (exact products, no per-element rounding). */
 int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* W,
                  int32_t dtype, const int32_t* perm, const float* ws, const int32_t* cnt,
                  int32_t n_split, float* zpart, void* stream);
 /* Output-rounding-exact forward for 16-bit networks (fp16 / bf16 h and W,
- * W the plain [T][K] weight, K a multiple of 16, <= 512): every element of
- * x = h W^T is formed on the matrix cores and rounded to the 16-bit type, as
- * the unfused layer's (the reference network's) output is, before the masked
- * weighted ray sum.  z [B][S][T] is ONE slab (n_split = 1 for
- * avr_dft_phase_fwd), zero for t >= T-1-shift_s.  perm / ws / cnt from
- * avr_head_sort; <= 4096 rays per shard. */
-int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* W,
-                       int32_t dtype, const int32_t* perm, const float* ws, const int32_t* cnt, float* z,
-                       void* stream);
+ * K a multiple of 16, <= 512; T <= 4096, <= 4096 rays per shard): every
+ * element of x = h W^T is formed on the matrix cores and rounded to the
+ * 16-bit type, as the unfused layer's (the reference network's) output is,
+ * before the masked weighted ray sum (csrc/head_exact.hip).
+ * avr_head_exact_layout gives n_split (the number of 256-ray slabs, a power
+ * of two <= 16, for avr_dft_phase_fwd) and the size of the packed weight;
+ * avr_head_pack_w_exact packs W [T][K] into Wf (MFMA B-fragment order, once
+ * per weight update); avr_head_fwd_exact writes zpart [n_split][B][S][T],
+ * zero for t >= T-1-shift_s.  perm / ws / cnt from avr_head_sort. */
+int avr_head_exact_layout(const avr_render_params* p, int32_t B, int32_t K, int32_t dtype,
+                          int32_t* n_split, int64_t* wpack_bytes);
+int avr_head_pack_w_exact(const avr_render_params* p, int32_t K, const void* W, int32_t dtype, void* Wf,
+                          void* stream);
+int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* Wf,
+                       int32_t dtype, const int32_t* perm, const float* ws, const int32_t* cnt,
+                       int32_t n_split, float* zpart, void* stream);
 /* Backward: gz [B][S][T] (avr_dft_phase_bwd) -> grad_h [B][R][S][K] (dtype),
  * grad_w [B][R][S] fp32 (to avr_weights_bwd) and grad_W [T][K] fp32.
  * `workspace` holds avr_head_bwd_workspace() bytes of fp32 partials. */

@@ -2,7 +2,9 @@
 device tensors) each driving the HIP render on cuda:0, so the multi-rank
 decomposition runs through the real kernels rather than the CPU oracle:
 
-* ray-sharded inference (RayShardedRender) == the unsharded render;
+* ray-sharded inference (RayShardedRender) == the unsharded render, for a
+  stub network and for an fp16 AVRModel_complex (the shards take the
+  renderer's own path: ray-layout dedup and the exact fused head);
 * ray-sharded training: SUM-all-reduced parameter gradients
   (allreduce_grads_sum) == the unsharded render's gradients;
 * DDP over pose shards (avr_runner_ddp.py:37-46,98): gradients after the
@@ -83,6 +85,36 @@ def _worker(rank, world, port, q):
             shd = RayShardedRender(rr)(ro, txp)
         res["infer_rel"] = _rel(shd, full)
 
+        # 1b. ray shards of a 16-bit network go through the renderer's own
+        # path: the shard's ray layout reaches the network (per-ray / per-pose
+        # encodings once) and the exact fused head renders; the all-reduced
+        # shards equal the unsharded fused render
+        cfg16 = dict(RAF, n_azi=8, n_ele=4, n_samples=16)
+        torch.manual_seed(0)
+        m16 = AVRModel_complex(dict(RAF_MODEL, signal_output_dim=800), mlp_dtype=torch.float16).to(dev)
+        seen = []
+        orig_fused = m16.forward_fused
+
+        def spy(*a, **k):
+            seen.append(k.get("ray_layout"))
+            return orig_fused(*a, **k)
+
+        m16.forward_fused = spy
+        r16 = AVRRender(m16, **cfg16).to(dev)
+        g16 = torch.Generator(device=dev).manual_seed(17)
+        rx16 = torch.rand(2, 3, device=dev, generator=g16) * 2 - 1
+        tx16 = torch.rand(2, 3, device=dev, generator=g16) * 2 - 1
+        dtx16 = torch.nn.functional.normalize(torch.randn(2, 3, device=dev, generator=g16), dim=-1)
+        with torch.no_grad():
+            torch.manual_seed(4)
+            full16 = r16(rx16, tx16, dtx16)
+            torch.manual_seed(4)
+            shd16 = RayShardedRender(r16)(rx16, tx16, dtx16)
+        R16 = 8 * 4 + 2
+        r0, r1 = shard_range(R16, rank, world)
+        res["fp16_shard_rel"] = _rel(shd16, full16)
+        res["fp16_layouts"] = seen == [(2, R16, 16), (2, r1 - r0, 16)]
+
         # 2. ray-sharded training gradients (SUM over ranks)
         cfg = dict(RAF, n_azi=8, n_ele=4, n_samples=16)
 
@@ -162,6 +194,8 @@ def test_world2_gloo_on_one_gpu_hip_path():
     for rank, res in out.items():
         assert "error" not in res, (rank, res)
         assert res["infer_rel"] < 1e-5, res
+        assert res["fp16_shard_rel"] < 1e-6, res
+        assert res["fp16_layouts"], res
         assert res["ray_grad_rel"] < 1e-3, res
         assert res["ddp_grad_rel"] < 1e-3, res
         assert res["ddp_weights_equal"], res

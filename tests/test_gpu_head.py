@@ -368,55 +368,34 @@ def test_fused_head_config2_fp16_matches_oracle_rounded_signal():
     assert e_exact < 1e-4 and emax < 1e-4, (e_exact, emax, e_linear)
 
 
-BAND_CASES = [c for c in CASES if c[6] % 128 == 0]
+# K = 512 with more rays than one 256-ray slab of the exact head holds:
+# config 4's RAF-E sphere (1154 rays: 5 slabs, n_split 8) and config 5's
+# full 89 x 46 + 2 = 4096-ray sphere (16 slabs)
+MANY_RAY_CASES = [
+    ("raf_e_k512", RAF, 48, 24, 16, 510, 512, 2),
+    ("sphere4096_k512", SIMU, 89, 46, 8, 254, 512, 1),
+]
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
-@pytest.mark.parametrize("case", BAND_CASES, ids=[c[0] for c in BAND_CASES])
-def test_band_forward_matches_feature_block_forward(case, dtype, monkeypatch):
-    """The linear head's forward for 16-bit h runs by delay bands
-    (csrc/head_band.hip) when the hidden width is a multiple of 128; the
-    feature-block kernel (AVR_HEAD_BAND=0) computes the same sums in another
-    fp32 order.  Both against each other at 2e-5 (L2 and max-norm), the band
-    form twice bitwise equal, on every head shape with such a width (ragged
-    windows, 5 m offset, T = 4094, 650 rays)."""
+@pytest.mark.parametrize("case", MANY_RAY_CASES, ids=[c[0] for c in MANY_RAY_CASES])
+def test_exact_head_many_rays(case, dtype):
+    """The exact head with K = 512 beyond 1024 rays: against the CPU oracle
+    on the rounded signal (1e-4, L2 and max-norm) and the plain render of it
+    (2e-5); repeat renders bitwise equal."""
     cfg, ro, tx, attn, h, W, _ = _operands(case, dtype)
-    r = AVRRender(None, exact_head=False, **cfg)
+    r = AVRRender(None, **cfg)
     torch.manual_seed(5)
     _, _, _, _, geom = r.sample(ro, tx)
     with torch.no_grad():
-        monkeypatch.setenv("AVR_HEAD_BAND", "1")
-        band = r.render_from_hidden(attn, h, W, dtype, geom)
+        fused = r.render_from_hidden(attn, h, W, dtype, geom)
         again = r.render_from_hidden(attn, h, W, dtype, geom)
-        monkeypatch.setenv("AVR_HEAD_BAND", "0")
-        blocks = r.render_from_hidden(attn, h, W, dtype, geom)
-    assert torch.equal(band, again)
-    assert _rel(band, blocks) < 2e-5, (case[0], _rel(band, blocks))
-    assert float((band - blocks).abs().max() / blocks.abs().max().clamp_min(1e-30)) < 2e-5
-
-
-def test_band_forward_config2_full_size(monkeypatch):
-    """Config 2 at full size (1024 rays x 256 samples, T = 1022, K = 512, fp16):
-    the band forward against the feature-block forward and against the plain
-    render of the unrounded product h @ W^T."""
-    from avr_amd.workloads import WORKLOADS
-
-    w = WORKLOADS["c2_meshrir_1024x256x512"]
-    B, R, S, T, K = w.batch, w.n_rays, w.n_samples, w.T, 512
-    g = torch.Generator(device=DEV).manual_seed(11)
-    ro = torch.rand(B, 3, device=DEV, generator=g) * 4 - 2
-    tx = torch.rand(B, 3, device=DEV, generator=g) * 4 - 2
-    attn = torch.rand(B, R * S, 1, device=DEV, generator=g) * 2
-    h = torch.relu(torch.randn(B, R * S, K, device=DEV, generator=g)).to(torch.float16)
-    W = torch.randn(T, K, device=DEV, generator=g) / K ** 0.5
-    r = AVRRender(None, exact_head=False, **w.render)
+        sig = (h.float() @ W.to(dtype).float().t()).to(dtype).float()
+        plain = r.render_from_network_output(attn, sig, geom)
+    assert torch.equal(fused, again)
+    assert _rel(fused, plain) < 2e-5, (case[0], _rel(fused, plain))
     torch.manual_seed(5)
-    _, _, _, _, geom = r.sample(ro, tx)
-    with torch.no_grad():
-        monkeypatch.setenv("AVR_HEAD_BAND", "1")
-        band = r.render_from_hidden(attn, h, W, torch.float16, geom)
-        monkeypatch.setenv("AVR_HEAD_BAND", "0")
-        blocks = r.render_from_hidden(attn, h, W, torch.float16, geom)
-        plain = r.render_from_network_output(attn, h.float() @ W.to(torch.float16).float().t(), geom)
-    assert _rel(band, blocks) < 2e-5, _rel(band, blocks)
-    assert _rel(band, plain) < 2e-5, _rel(band, plain)
+    ref = orc.render_spectrum(orc.RenderConfig.from_kwargs(**cfg), orc.StubNetwork(attn.cpu(), sig.cpu()),
+                              ro.cpu(), tx.cpu())
+    assert _rel(fused.cpu(), ref) < 1e-4, (case[0], _rel(fused.cpu(), ref))
+    assert float((fused.cpu() - ref).abs().max() / ref.abs().max()) < 1e-4

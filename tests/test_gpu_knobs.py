@@ -1,0 +1,33 @@
+"""GPU: the library's only environment knobs (AVR_NSPLIT, the ray-reduction
+splits; AVR_KSPLIT, the DFT k-slices) are validated performance settings:
+every value, legal or not, leaves the spectrum within the north-star 1e-4 of
+the reference's golden vectors.  Nothing else in csrc/ reads the
+environment (tests/test_lib_abi.py checks the sources)."""
+import functools
+
+import pytest
+
+from golden_util import Case, rel_l2, rel_max
+from test_gpu_render import hip_render
+
+pytestmark = pytest.mark.gpu
+
+KNOBS = [("AVR_NSPLIT", v) for v in ("1", "2", "4", "8", "16", "3", "0", "-4", "junk")] + \
+        [("AVR_KSPLIT", v) for v in ("1", "2", "5", "64", "100000", "0", "-1", "junk")]
+
+
+@functools.lru_cache(maxsize=None)
+def _case(name):
+    case = Case(name)
+    return case, case.inputs()
+
+
+@pytest.mark.parametrize("name", ["c1_s1", "c3_s0", "edge_ragged_s3"])
+@pytest.mark.parametrize("knob,value", KNOBS, ids=[f"{k}={v}" for k, v in KNOBS])
+def test_knob_keeps_golden(name, knob, value, monkeypatch):
+    monkeypatch.setenv(knob, value)
+    case, inp = _case(name)
+    out, *_ = hip_render(case, inp, case.seed)
+    o = out.detach().cpu().numpy()
+    assert rel_l2(o, case["out"]) < 1e-4, (knob, value, rel_l2(o, case["out"]))
+    assert rel_max(o, case["out"]) < 1e-4, (knob, value, rel_max(o, case["out"]))

@@ -21,15 +21,17 @@ def _run(x, w, relu=True):
     M, K = x.shape
     N = w.size(0)
     y = torch.empty(M, N, dtype=x.dtype, device=DEV)
+    wf = torch.empty_like(w)
     st = torch.cuda.current_stream(DEV).cuda_stream
-    _lib.call("avr_linear_relu_fwd", M, N, K, x.data_ptr(), w.data_ptr(), CODE[x.dtype],
+    _lib.call("avr_linear_pack_w", N, K, w.data_ptr(), CODE[x.dtype], wf.data_ptr(), st)
+    _lib.call("avr_linear_relu_fwd", M, N, K, x.data_ptr(), wf.data_ptr(), CODE[x.dtype],
               int(relu), y.data_ptr(), st)
     return y
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["fp16", "bf16"])
 @pytest.mark.parametrize("M,N,relu", [(64, 256, True), (1000, 512, True), (4096 + 37, 512, False),
-                                      (262144, 512, True)])
+                                      (300, 96, True), (262144, 512, True)])
 def test_linear_relu_matches_fp32_statement(dtype, M, N, relu):
     g = torch.Generator(device=DEV).manual_seed(M + N)
     x = torch.relu(torch.randn(M, 512, device=DEV, generator=g)).to(dtype)
@@ -55,5 +57,9 @@ def test_linear_relu_rejects_unsupported_shapes():
     w = torch.zeros(256, 256, dtype=torch.float16, device=DEV)
     y = torch.empty(64, 256, dtype=torch.float16, device=DEV)
     lib = _lib.load()
-    assert lib.avr_linear_relu_fwd(64, 256, 256, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(w.data_ptr()), _lib.DTYPE_F16, 1,
-                                   ctypes.c_void_p(y.data_ptr()), None) != 0
+    p = ctypes.c_void_p
+    assert lib.avr_linear_relu_fwd(64, 256, 256, p(x.data_ptr()), p(w.data_ptr()), _lib.DTYPE_F16, 1,
+                                   p(y.data_ptr()), None) != 0  # K != 512
+    assert lib.avr_linear_relu_fwd(64, 40, 512, p(x.data_ptr()), p(w.data_ptr()), _lib.DTYPE_F16, 1,
+                                   p(y.data_ptr()), None) != 0  # N not a multiple of 32
+    assert lib.avr_linear_pack_w(40, 512, p(w.data_ptr()), _lib.DTYPE_F16, p(y.data_ptr()), None) != 0

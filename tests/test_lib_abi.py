@@ -59,3 +59,15 @@ def test_argument_errors_are_reported_without_gpu(lib):
 def test_code_object_targets_gfx950(lib):
     blob = open(_lib.LIB_PATH, "rb").read()
     assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_only_validated_knobs_read_the_environment():
+    """The shipped library reads exactly two environment variables, both
+    validated tuning knobs (tests/test_gpu_knobs.py renders the golden vectors
+    under every value); no debug or experiment switch can change results."""
+    csrc = os.path.join(ROOT, "avr_amd", "csrc")
+    names = set()
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".cpp", ".h")):
+            names |= set(re.findall(r'getenv\("([A-Z_0-9]+)"\)', open(os.path.join(csrc, f)).read()))
+    assert names == {"AVR_NSPLIT", "AVR_KSPLIT"}, names

@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--M", type=int, default=262144)
     ap.add_argument("--N", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--dbgs", default="0", help="AVR_LINEAR_DBG values, interleaved --reps times")
+    ap.add_argument("--waves", default="8,4", help="AVR_LINEAR_WAVES_PROBE values, interleaved --reps times")
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=200)
     args = ap.parse_args()
@@ -39,9 +39,11 @@ def main():
     bias = torch.zeros(N, dtype=dt, device=dev)
     y = torch.empty(M, N, dtype=dt, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
+    wf = torch.empty_like(w)
+    _lib.call("avr_linear_pack_w", N, K, w.data_ptr(), code, wf.data_ptr(), st)
 
     def ours():
-        _lib.call("avr_linear_relu_fwd", M, N, K, x.data_ptr(), w.data_ptr(), code, 1, y.data_ptr(), st)
+        _lib.call("avr_linear_relu_fwd", M, N, K, x.data_ptr(), wf.data_ptr(), code, 1, y.data_ptr(), st)
         return y
 
     def blas():
@@ -53,9 +55,9 @@ def main():
     torch.cuda.synchronize()
     runs = []
     for _ in range(args.reps):
-        runs += [("avr_linear_relu_fwd", ours, d) for d in args.dbgs.split(",")] + [("hipblaslt_addmm_activation", blas, "0")]
+        runs += [("avr_linear_relu_fwd", ours, d) for d in args.waves.split(",")] + [("hipblaslt_addmm_activation", blas, "0")]
     for name, fn, dbg in runs:
-        os.environ["AVR_LINEAR_DBG"] = dbg
+        os.environ["AVR_LINEAR_WAVES_PROBE"] = dbg
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -66,9 +68,8 @@ def main():
         e1.record()
         e1.synchronize()
         ms = e0.elapsed_time(e1) / args.iters
-        print(json.dumps({"kernel": name, "dbg": int(dbg), "dtype": args.dtype, "M": M, "N": N, "K": K, "us": ms * 1e3,
+        print(json.dumps({"kernel": name, "waves": int(dbg), "dtype": args.dtype, "M": M, "N": N, "K": K, "us": ms * 1e3,
                           "pflops": 2 * M * N * K / (ms * 1e-3) / 1e15}), flush=True)
-    os.environ["AVR_LINEAR_DBG"] = "0"
     a, b = ours().float(), blas().float()
     print(json.dumps({"equal_fraction": float((a == b).float().mean()),
                       "max_rel": float(((a - b).abs() / b.abs().clamp_min(1e-3)).max())}), flush=True)
