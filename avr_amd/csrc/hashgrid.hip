@@ -770,6 +770,8 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
     }
 }
 
+constexpr int64_t kMaxBwdWorkspaceBytes = int64_t(1) << 31;  // 2 GiB (config 4: 283 MB)
+
 struct BwdLayout {
     BwdPlan plan;
     int total_parts;
@@ -822,6 +824,9 @@ int bwd_layout(int64_t N, int L, const int64_t* off, const int32_t* res, BwdLayo
     b.contrib = o0;  // (key, v0, v1) per contribution
     o0 += al(maxc * 12);
     b.bytes = o0;
+    // the workspace comes from the caller's allocator on every backward: past
+    // this size the atomic kernel runs instead (no workspace, same += result)
+    if (b.bytes > kMaxBwdWorkspaceBytes) b.scatter_ok = false;
     *o = b;
     return 0;
 }

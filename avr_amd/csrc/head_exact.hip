@@ -36,10 +36,14 @@
 // Items are ordered block-major (every column's first block first: the
 // longest items start first and the short ones fill the tail).
 #include "common.h"
+#include "probe.h"
+#include "stationary.h"
 
 #include <algorithm>
 
 using namespace avr;
+
+AVR_PROBE_TU(avr_probe_set_exact)
 
 namespace {
 
@@ -81,38 +85,52 @@ __device__ __forceinline__ void dma_row16(const void* g, uint32_t lds) {
 // s_waitcnt vmcnt(n) (expcnt / lgkmcnt not waited on; gfx9 encoding)
 #define AVR_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 0xF) | (0x7 << 4) | (0xF << 8) | (((N) >> 4) << 14))
 
-constexpr int kXRays = 256;  // sorted rays per work item
-constexpr int kXRing = 4;    // W tiles in the LDS ring (3 in flight)
+// s_waitcnt vmcnt(n) for a run-time n (one case per value; above 31 the
+// wait is for 31, a longer wait than asked)
+__device__ __forceinline__ void wait_vm(int n) {
+    switch (n) {
+#define AVR_VMC(K) case K: AVR_VMCNT(K); break;
+        AVR_VMC(0) AVR_VMC(1) AVR_VMC(2) AVR_VMC(3) AVR_VMC(4) AVR_VMC(5) AVR_VMC(6) AVR_VMC(7)
+        AVR_VMC(8) AVR_VMC(9) AVR_VMC(10) AVR_VMC(11) AVR_VMC(12) AVR_VMC(13) AVR_VMC(14) AVR_VMC(15)
+        AVR_VMC(16) AVR_VMC(17) AVR_VMC(18) AVR_VMC(19) AVR_VMC(20) AVR_VMC(21) AVR_VMC(22) AVR_VMC(23)
+        AVR_VMC(24) AVR_VMC(25) AVR_VMC(26) AVR_VMC(27) AVR_VMC(28) AVR_VMC(29) AVR_VMC(30) AVR_VMC(31)
+#undef AVR_VMC
+        default: AVR_VMCNT(31); break;
+    }
+}
 
 // bytes of one 32-t W tile in fragment order: KSM k-steps x 64 lanes x 16 B
 __host__ __device__ constexpr int xs_tile_bytes(int KSM) { return KSM * 1024; }
-__host__ __device__ constexpr size_t xs_lds_bytes(int KSM, int T, int waves) {
-    return (size_t)kXRing * xs_tile_bytes(KSM) + 4 * (size_t)((T + 3) / 4 * 4) + 4 * (size_t)kXRays +
-           4 * (size_t)(2 * waves * 32) + 4 * 8 + 16;
+__host__ __device__ constexpr size_t xs_lds_bytes(int KSM, int T, int waves, int rays, int nb, int nc) {
+    return (size_t)nb * nc * xs_tile_bytes(KSM) + 4 * (size_t)((T + 3) / 4 * 4) + 4 * (size_t)rays +
+           4 * (size_t)(2 * waves * 32 * nc) + 4 * (size_t)waves + 16;
 }
 
-// WAVES = 4: one wave per SIMD, 64 rays (two 32-ray A tiles, 256 VGPRs at
-// K = 512) per wave, one B fragment read per two MFMAs.  WAVES = 8: two waves
-// per SIMD, 32 rays per wave; one wave's epilogue runs beside its SIMD
-// partner's MFMA chain.
-template <typename E, int KSM, int WAVES, bool NT_H = false>
-__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES / 4, WAVES / 4))) void
-head_exact_hs_kernel(avr_render_params pp, int B, int R, int K, const E* __restrict__ h, const frag8* __restrict__ Wf,
-                     const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
-                     float* __restrict__ zpart) {
-    constexpr int NT = 64 * WAVES, NB = kXRing, TILE = xs_tile_bytes(KSM);
-    constexpr int RPW = kXRays / WAVES;  // rays per wave
+// One work item: RAYS consecutive sorted rays of one column (b, s), WAVES
+// waves of RPW = RAYS / WAVES rays (NQ = RPW / 32 MFMA A tiles each), a ring
+// of NB W tiles.  <8, 256, 4>: one workgroup per CU (two waves per SIMD);
+// <4, 128, 2>: half the item and ~70 KB of LDS, so two workgroups share a CU
+// and one's prologue and barriers overlap the other's MFMA chains.
+template <typename E, int KSM, int WAVES, int RAYS, int NB, int NC>
+__global__ __launch_bounds__(64 * WAVES) void head_exact_kernel(
+    avr_render_params pp, int B, int R, int K, const E* __restrict__ h, const frag8* __restrict__ Wf,
+    const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
+    float* __restrict__ zpart) {
+    constexpr int NT = 64 * WAVES, TILE = NC * xs_tile_bytes(KSM);  // a tile: TT = 32 NC values of t
+    constexpr int TT = 32 * NC;
+    constexpr int RPW = RAYS / WAVES;    // rays per wave
     constexpr int NQ = RPW / 32;         // 32-ray A tiles per wave
-    constexpr int DPW = KSM / WAVES;     // 1 KiB DMAs per wave and tile
-    static_assert(KSM % WAVES == 0 && DPW * (NB - 2) <= 63 && NT >= kXRays, "ring");
+    constexpr int DPW = NC * KSM / WAVES;  // 1 KiB DMAs per wave and tile
+    static_assert((NC * KSM) % WAVES == 0 && NQ == 1 && DPW * NB <= 63 && NT >= RAYS, "shape");
+    AVR_PROBE_DECL;
     extern __shared__ __attribute__((aligned(16))) char lds_x[];
     const int T = pp.T, S = pp.n_samples;
     const int Tp = (T + 3) & ~3;
-    char* ring = lds_x;                                           // [NB][TILE]
-    int* cl = reinterpret_cast<int*>(lds_x + NB * TILE);          // cnt of the column [Tp]
-    float* wl = reinterpret_cast<float*>(cl + Tp);                // weights of the item's rays [256]
-    float* zr = wl + kXRays;                                      // wave partials [2][WAVES][32]
-    int* dstart = reinterpret_cast<int*>(zr + 2 * WAVES * 32);    // first live t per wave [WAVES]
+    char* ring = lds_x;                                         // [NB][TILE]
+    int* cl = reinterpret_cast<int*>(lds_x + NB * TILE);        // cnt of the column [Tp]
+    float* wl = reinterpret_cast<float*>(cl + Tp);              // weights of the item's rays [RAYS]
+    float* zr = wl + RAYS;                                      // wave partials [2][WAVES][TT]
+    int* dstart = reinterpret_cast<int*>(zr + 2 * WAVES * TT);  // first live t per wave [WAVES]
 
     const int64_t ncol = (int64_t)B * S;
     const int64_t col = (int64_t)blockIdx.x % ncol;
@@ -125,15 +143,30 @@ head_exact_hs_kernel(avr_render_params pp, int B, int R, int K, const E* __restr
     float* zc = zpart + ((int64_t)blk * ncol + col) * T;
     const int* cc = cnt + col * T;
     const int nk = cc[T - 1];  // kept rays of the column
-    const int p0 = blk * kXRays;
+    const int p0 = blk * RAYS;
     if (p0 >= nk || lim <= 0) {
         for (int t = threadIdx.x; t < T; t += NT) zc[t] = 0.0f;
         return;
     }
+    // the wave's rows first: their DMA flies under the metadata work below
+    // (positions past the kept rays repeat the last kept ray; masked)
+    const int ksn = K / 16;
+    const int pw = p0 + RPW * wave;
+    const bool dma_rows = KSM == 32 && K == 512 && NQ == 1;
+    const E* hrow[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int ray = perm[col * R + min(pw + 32 * q + j, nk - 1)];
+        hrow[q] = h + (((int64_t)b * R + ray) * S + s) * K;
+    }
+    if (dma_rows) {
+        stat_issue_round(reinterpret_cast<const uint16_t*>(hrow[0]), ring + wave * 16384, 0);
+        stat_issue_round(reinterpret_cast<const uint16_t*>(hrow[0]), ring + wave * 16384, 1);
+    }
 
-    // ---- prologue: cnt and the block's weights into LDS; each wave's first live t
+    // ---- prologue: cnt and the item's weights into LDS; each wave's first live t
     for (int t = threadIdx.x; t < T; t += NT) cl[t] = cc[t];
-    if (threadIdx.x < kXRays) {
+    if (threadIdx.x < RAYS) {
         const int p = p0 + (int)threadIdx.x;
         wl[threadIdx.x] = p < nk ? ws[col * R + p] : 0.0f;
     }
@@ -148,15 +181,39 @@ head_exact_hs_kernel(avr_render_params pp, int B, int R, int K, const E* __restr
         }
     }
     __syncthreads();
-    const int tb = dstart[0] >> 5;              // first tile with a live ray of the item
-    const int te = (lim + 31) >> 5;             // tiles holding t < lim
-    const int tw = min(dstart[wave] >> 5, te);  // this wave's first live tile
+    AVR_PROBE_MARK(8);
+    const int tb = dstart[0] / TT;              // first tile with a live ray of the item
+    const int te = (lim + TT - 1) / TT;         // tiles holding t < lim
+    const int tw = min(dstart[wave] / TT, te);  // this wave's first live tile
     for (int t = threadIdx.x; t < T; t += NT)
-        if (t < 32 * tb || t >= 32 * te) zc[t] = 0.0f;
+        if (t < TT * tb || t >= TT * te) zc[t] = 0.0f;
 
-    // W tile `tau` into ring slot `slot`: this wave's DPW 1 KiB pieces
+    // ---- the wave's rays: A fragments (k = 16 ks + 8 half + 0..7), loaded once
+    frag8 a[NQ][KSM];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const E* hr = hrow[q];
+        if (dma_rows) {
+            // whole rows by LDS-DMA through the (still idle) ring, 16 KiB per wave
+            stat_finish_rows512(reinterpret_cast<frag8_t(&)[32]>(a[q]), reinterpret_cast<const uint16_t*>(hr),
+                                ring + wave * 16384);
+        } else {
+#pragma unroll
+            for (int ks = 0; ks < KSM; ++ks)
+                a[q][ks] = *reinterpret_cast<const frag8*>(hr + 8 * half + 16 * min(ks, ksn - 1));
+#pragma unroll
+            for (int ks = 0; ks < KSM; ++ks)
+                if (ks >= ksn) a[q][ks] = frag8{0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int ks = 0; ks < KSM; ++ks) asm volatile("" ::"v"(a[q][ks]));
+            AVR_VMCNT(0);
+        }
+    }
+    AVR_PROBE_MARK(9);
+    __syncthreads();  // every wave is done with the staging area: the ring may fill
+    AVR_PROBE_MARK(10);
     const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
-    auto issue = [&](int tau, int slot) {
+    auto issue = [&](int tau, int slot) {  // W tile tau into ring slot `slot`: this wave's DPW pieces
         const char* src = reinterpret_cast<const char*>(Wf) + (int64_t)tau * TILE + wave * DPW * 1024 + 16 * lane;
         const uint32_t dst = ring_lds + slot * TILE + wave * DPW * 1024;
 #pragma unroll
@@ -164,137 +221,109 @@ head_exact_hs_kernel(avr_render_params pp, int B, int R, int K, const E* __restr
     };
     for (int i = 0; i < NB - 1; ++i)
         if (tb + i < te) issue(tb + i, i);
-
-    // ---- the wave's rays: A fragments (k = 16 ks + 8 half + 0..7), loaded
-    // once; positions past the kept rays repeat the last kept ray (masked)
-    const int ksn = K / 16;
-    frag8 a[NQ][KSM];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int p = min(p0 + RPW * wave + 32 * q + j, nk - 1);
-        const int ray = perm[col * R + p];
-        const E* hr = h + (((int64_t)b * R + ray) * S + s) * K + 8 * half;
-#pragma unroll
-        for (int ks = 0; ks < KSM; ++ks) {
-            const frag8* src = reinterpret_cast<const frag8*>(hr + 16 * min(ks, ksn - 1));
-            if constexpr (NT_H)
-                a[q][ks] = __builtin_nontemporal_load(src);
-            else
-                a[q][ks] = *src;
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-        for (int ks = 0; ks < KSM; ++ks)
-            if (ks >= ksn) a[q][ks] = frag8{0u, 0u, 0u, 0u};
-    // land them here (the compiler waits vmcnt(0): the ring's first tiles too),
-    // so no wait on them is left for the loop, where vmcnt also counts DMAs
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-        for (int ks = 0; ks < KSM; ++ks) asm volatile("" ::"v"(a[q][ks]));
     AVR_VMCNT(0);
     __syncthreads();
+    AVR_PROBE_MARK(2);
 
-    const int pw = p0 + RPW * wave;
-    // NQL live 32-ray tiles of the wave: MFMA chains over K (one B fragment
-    // read per k-step, shared by the chains), then the epilogue
-    auto tile = [&](auto nql_tag, int i, int tau, float& zl) {
-        constexpr int NQL = decltype(nql_tag)::value;
-        const char* bsrc = ring + (i % NB) * TILE + 16 * lane;
+    // the wave's 32 rays against 32-t column group c of the tile in ring slot
+    // `slot`: one MFMA chain over K (A from registers, B read from the ring
+    // D k-steps ahead), then the epilogue (rounded, masked by value:
+    // p < cnt[t], weighted, summed per lane in row order)
+    const float* wq = wl + RPW * wave + 4 * half;
+    auto group = [&](int slot, int tau, int c) {
+        const char* bsrc = ring + slot * TILE + c * xs_tile_bytes(KSM) + 16 * lane;
         constexpr int D = KSM < 8 ? KSM : 8;  // B fragments read ahead
         frag8 bw[D];
 #pragma unroll
         for (int u = 0; u < D; ++u) bw[u] = *reinterpret_cast<const frag8*>(bsrc + u * 1024);
-        f32x16 acc[NQL];
-#pragma unroll
-        for (int q = 0; q < NQL; ++q) acc[q] = f32x16{};
+        f32x16 acc = f32x16{};
 #pragma unroll
         for (int ks = 0; ks < KSM; ++ks) {
-#pragma unroll
-            for (int q = 0; q < NQL; ++q) acc[q] = mfma16<E>(a[q][ks], bw[ks % D], acc[q]);
+            acc = mfma16<E>(a[0][ks], bw[ks % D], acc);
             if (ks + D < KSM) bw[ks % D] = *reinterpret_cast<const frag8*>(bsrc + (ks + D) * 1024);
         }
         __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
 #pragma unroll
         for (int ks = 0; ks < KSM; ++ks) {
-            __builtin_amdgcn_sched_group_barrier(0x008, NQL, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             if (ks + D < KSM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
-        // epilogue: register r of acc[q] is row 32 q + (r & 3) + 8 (r >> 2) + 4 half
-        // of the wave's rays, column t
-        const int t = 32 * tau + j;
-        const int full = __builtin_amdgcn_readfirstlane((32 * tau + 31 < lim) ? cl[32 * tau] : 0);
-        const float* wq = wl + RPW * wave + 4 * half;
-        if (pw + 32 * NQL <= full) {  // every (ray, t) pair of the tiles is live
+        // register r of acc is row (r & 3) + 8 (r >> 2) + 4 half of the wave's
+        // rays, column t = TT tau + 32 c + j
+        const int t0 = TT * tau + 32 * c;
+        const int t = t0 + j;
+        const int full = __builtin_amdgcn_readfirstlane((t0 + 31 < lim) ? cl[t0] : 0);
+        float z = 0.0f;
+        if (pw + 32 <= full) {  // every (ray, t) pair of the group is live
 #pragma unroll
-            for (int q = 0; q < NQL; ++q)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float4 w4 = *reinterpret_cast<const float4*>(wq + 32 * q + 8 * g);
-                    zl = fmaf(w4.x, round16<E>(acc[q][4 * g + 0]), zl);
-                    zl = fmaf(w4.y, round16<E>(acc[q][4 * g + 1]), zl);
-                    zl = fmaf(w4.z, round16<E>(acc[q][4 * g + 2]), zl);
-                    zl = fmaf(w4.w, round16<E>(acc[q][4 * g + 3]), zl);
-                }
+            for (int g = 0; g < 4; ++g) {
+                const float4 w4 = *reinterpret_cast<const float4*>(wq + 8 * g);
+                z = fmaf(w4.x, round16<E>(acc[4 * g + 0]), z);
+                z = fmaf(w4.y, round16<E>(acc[4 * g + 1]), z);
+                z = fmaf(w4.z, round16<E>(acc[4 * g + 2]), z);
+                z = fmaf(w4.w, round16<E>(acc[4 * g + 3]), z);
+            }
         } else {
-            const int ct = t < lim ? cl[t] : 0;
+            const int ct = t < lim ? cl[min(t, T - 1)] : 0;
 #pragma unroll
-            for (int q = 0; q < NQL; ++q)
+            for (int g = 0; g < 4; ++g) {
+                const float4 w4 = *reinterpret_cast<const float4*>(wq + 8 * g);
+                const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float4 w4 = *reinterpret_cast<const float4*>(wq + 32 * q + 8 * g);
-                    const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const float v = round16<E>(acc[q][4 * g + e]);
-                        zl = fmaf(wv[e], (pw + 32 * q + 8 * g + 4 * half + e < ct) ? v : 0.0f, zl);
-                    }
+                for (int e = 0; e < 4; ++e) {
+                    const float v = round16<E>(acc[4 * g + e]);
+                    z = fmaf(wv[e], (pw + 8 * g + 4 * half + e < ct) ? v : 0.0f, z);
                 }
+            }
         }
+        return z;
     };
     for (int tau = tb; tau < te; ++tau) {
         const int i = tau - tb;
+        AVR_PROBE_BEGIN(comp);
         if (tau + NB - 1 < te) issue(tau + NB - 1, (i + NB - 1) % NB);  // the slot tile tau-1 left
-        float zl = 0.0f;
-        if (tau >= tw) {
-            // rays of the wave live somewhere in the tile: its 32-ray tiles up
-            // to the last one live at the tile's last t
-            const int chi = __builtin_amdgcn_readfirstlane(cl[min(32 * tau + 31, lim - 1)]);
-            if constexpr (NQ == 2) {
-                if (pw + 32 < chi)
-                    tile(std::integral_constant<int, 2>{}, i, tau, zl);
-                else
-                    tile(std::integral_constant<int, 1>{}, i, tau, zl);
-            } else {
-                tile(std::integral_constant<int, 1>{}, i, tau, zl);
-            }
+        float zl[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            // group c holds a live ray of the wave from the wave's first live t
+            // on (cnt is nondecreasing in t), and nothing at or past lim
+            const int t0 = TT * tau + 32 * c;
+            zl[c] = (t0 + 31 >= dstart[wave] && t0 < lim) ? group(i % NB, tau, c) : 0.0f;
         }
+        AVR_PROBE_END(comp, 6);
         // lower + upper lane half (rows 4 half + ...), the same association in every lane
-        {
-            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zl), __float_as_uint(zl), false, false);
-            zl = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const auto r =
+                __builtin_amdgcn_permlane32_swap(__float_as_uint(zl[c]), __float_as_uint(zl[c]), false, false);
+            const float v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+            if (half == 0) zr[(i & 1) * (WAVES * TT) + wave * TT + 32 * c + j] = v;
         }
-        if (half == 0) zr[(i & 1) * (WAVES * 32) + wave * 32 + j] = zl;
-        if (tau + 1 < te) {  // this wave's pieces of tile tau+1 have landed (younger tiles may fly)
-            switch (min(NB - 2, te - 2 - tau)) {
-                case 0: AVR_VMCNT(0); break;
-                case 1: AVR_VMCNT(DPW); break;
-                default: AVR_VMCNT(2 * DPW); break;
-            }
+        AVR_PROBE_BEGIN(dma);
+        if (tau + 1 < te) {
+            // this wave's pieces of tile tau+1 have landed.  Younger in vmcnt:
+            // the ring's later tiles and this wave's partial stores since tile
+            // tau+1 was issued (a wave stores after the barrier of iteration m
+            // when wave == m % WAVES), so no store in flight is waited for
+            int st = 0;
+            for (int m = max(0, i + 2 - NB); m < i; ++m) st += (wave == m % WAVES);
+            wait_vm(min(NB - 2, te - 2 - tau) * DPW + st);
         }
+        AVR_PROBE_END(dma, 4);
+        AVR_PROBE_BEGIN(bar);
         __builtin_amdgcn_s_waitcnt(0xC07F);  // every LDS access of tile tau (and the partials) done
         __builtin_amdgcn_s_barrier();
-        if (wave == (i % WAVES) && half == 0) {  // the wave partials of tile tau, in wave order
-            const float* zz = zr + (i & 1) * (WAVES * 32) + j;
+        AVR_PROBE_END(bar, 5);
+        if (wave == (i % WAVES) && lane < TT) {  // the wave partials of tile tau, in wave order
+            const float* zz = zr + (i & 1) * (WAVES * TT) + lane;
             float v = zz[0];
 #pragma unroll
-            for (int w = 1; w < WAVES; ++w) v += zz[32 * w];
-            const int t = 32 * tau + j;
+            for (int w = 1; w < WAVES; ++w) v += zz[TT * w];
+            const int t = TT * tau + lane;
             if (t < T) zc[t] = v;
         }
     }
+    AVR_PROBE_FLUSH(blockIdx.x * WAVES + wave);
 }
 
 // W [T][K] -> Wf: for t-tile tau and k-step ks, the 64 lanes' 16-byte B
@@ -317,10 +346,14 @@ __global__ __launch_bounds__(256) void head_pack_exact_kernel(int T, int K, int 
 
 int exact_ksm(int K) { return K <= 128 ? 8 : (K <= 256 ? 16 : 32); }
 
-// waves per work item at K = 512 (4: 64 rays per wave, 8: 32); probe only
-int exact_waves() {
-    const char* e = getenv("AVR_EXACT_WAVES_PROBE");
-    return e ? atoi(e) : 8;
+// Work-item shape: 128 rays and two workgroups per CU where the DFT's slab
+// count allows (<= 2048 rays) and two ~70 KB LDS images fit (T <= 1024);
+// 256 rays, one workgroup per CU, otherwise.  AVR_EXACT_RAYS_PROBE=256 forces
+// the latter (probe runs).
+int exact_rays(int R, int T) {
+    const char* e = getenv("AVR_EXACT_RAYS_PROBE");
+    if (e && atoi(e) == 256) return 256;
+    return (R <= 16 * 128 && T <= 1024) ? 128 : 256;
 }
 
 int exact_check(const avr_render_params* p, int32_t K, int32_t dtype) {
@@ -328,13 +361,14 @@ int exact_check(const avr_render_params* p, int32_t K, int32_t dtype) {
     AVR_REQUIRE(dtype == AVR_DTYPE_F16 || dtype == AVR_DTYPE_BF16, "avr_head_fwd_exact: h/W must be fp16 or bf16");
     if (K % 16 != 0 || K < 16 || K > 512) return fail(AVR_E_CONFIG, "exact head: K must be a multiple of 16, <= 512");
     const int R = n_rays(*p);
-    AVR_REQUIRE(R >= 1 && R <= 16 * kXRays && p->T >= 2 && p->T <= 4096 && p->n_samples >= 1,
+    AVR_REQUIRE(R >= 1 && R <= 16 * 256 && p->T >= 2 && p->T <= 4096 && p->n_samples >= 1,
                 "avr_head_fwd_exact: shape out of range (<= 4096 rays per shard, T <= 4096)");
     return 0;
 }
 
-int exact_splits(int R) {
-    const int nb = (R + kXRays - 1) / kXRays;
+int exact_splits(int R, int T) {
+    const int rays = exact_rays(R, T);
+    const int nb = (R + rays - 1) / rays;
     int n = 1;
     while (n < nb) n *= 2;
     return n;
@@ -352,8 +386,9 @@ extern "C" int avr_head_exact_layout(const avr_render_params* p, int32_t B, int3
                                      int32_t* n_split, int64_t* wpack_bytes) {
     AVR_REQUIRE(B >= 1 && n_split && wpack_bytes, "avr_head_exact_layout: bad args");
     if (int e = exact_check(p, K, dtype)) return e;
-    *n_split = exact_splits(n_rays(*p));
-    *wpack_bytes = (int64_t)((p->T + 31) / 32) * xs_tile_bytes(exact_ksm(K));
+    *n_split = exact_splits(n_rays(*p), p->T);
+    // whole 64-t tile pairs (a 64-t tile reads two consecutive 32-t tiles), zero past T
+    *wpack_bytes = (int64_t)((p->T + 63) / 64) * 2 * xs_tile_bytes(exact_ksm(K));
     return 0;
 }
 
@@ -364,7 +399,7 @@ extern "C" int avr_head_pack_w_exact(const avr_render_params* p, int32_t K, cons
     AVR_REQUIRE(reinterpret_cast<uintptr_t>(W) % 16 == 0 && reinterpret_cast<uintptr_t>(Wf) % 16 == 0,
                 "avr_head_pack_w_exact: W and Wf must be 16-byte aligned");
     const int T = p->T, KSM = exact_ksm(K);
-    const int64_t n = (int64_t)((T + 31) / 32) * KSM * 64;
+    const int64_t n = (int64_t)((T + 63) / 64) * 2 * KSM * 64;
     const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
     hipLaunchKernelGGL(head_pack_exact_kernel<__half>, dim3(blocks), dim3(256), 0, as_stream(stream), T, (int)K,
                        KSM, (const uint16_t*)W, (frag8*)Wf, n);
@@ -379,35 +414,37 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
     AVR_REQUIRE(reinterpret_cast<uintptr_t>(h) % 16 == 0 && reinterpret_cast<uintptr_t>(Wf) % 16 == 0,
                 "avr_head_fwd_exact: h and Wf must be 16-byte aligned");
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
-    AVR_REQUIRE(n_split == exact_splits(R), "avr_head_fwd_exact: n_split must be avr_head_exact_layout's");
+    AVR_REQUIRE(n_split == exact_splits(R, T), "avr_head_fwd_exact: n_split must be avr_head_exact_layout's");
     const int64_t items = (int64_t)n_split * B * S;
     AVR_REQUIRE(items < (1ll << 31), "avr_head_fwd_exact: too many columns");
     const int KSM = exact_ksm(K);
     hipStream_t st = as_stream(stream);
-    auto go = [&](auto kern, auto ksm_tag, auto w_tag, auto hp) {
-        constexpr int WV = decltype(w_tag)::value;
-        const size_t lds = xs_lds_bytes(decltype(ksm_tag)::value, T, WV);
-        allow_lds(kern, lds);
-        hipLaunchKernelGGL(kern, dim3((unsigned)items), dim3(64 * WV), lds, st, *p, (int)B, R, (int)K, hp,
-                           (const frag8*)Wf, perm, ws, cnt, zpart);
-    };
-    using I8 = std::integral_constant<int, 8>;
-    using I16 = std::integral_constant<int, 16>;
-    using I32 = std::integral_constant<int, 32>;
-    using W4 = std::integral_constant<int, 4>;
-    const int waves = exact_waves();
-    auto run = [&](auto e_tag, const void* hv) {
+    const bool small = exact_rays(R, T) == 128;
+    const char* tte = getenv("AVR_EXACT_TT_PROBE");
+    const bool tt64 = !small && tte && atoi(tte) == 64;
+    auto run = [&](auto e_tag) {
         using E = decltype(e_tag);
-        const E* hp = (const E*)hv;
-        if (KSM == 8) go(head_exact_hs_kernel<E, 8, 8>, I8{}, I8{}, hp);
-        else if (KSM == 16) go(head_exact_hs_kernel<E, 16, 8>, I16{}, I8{}, hp);
-        else if (waves == 4) go(head_exact_hs_kernel<E, 32, 4>, I32{}, W4{}, hp);
-        else if (waves == 9) go(head_exact_hs_kernel<E, 32, 8, true>, I32{}, I8{}, hp);
-        else go(head_exact_hs_kernel<E, 32, 8>, I32{}, I8{}, hp);
+        auto go = [&](auto kern, int ksm, int waves, int rays, int nb, int nc, const void* hv) {
+            const size_t lds = xs_lds_bytes(ksm, T, waves, rays, nb, nc);
+            allow_lds(kern, lds);
+            hipLaunchKernelGGL(kern, dim3((unsigned)items), dim3(64 * waves), lds, st, *p, (int)B, R, (int)K,
+                               (const E*)hv, (const frag8*)Wf, perm, ws, cnt, zpart);
+        };
+        if (small) {
+            if (KSM == 8) go(head_exact_kernel<E, 8, 4, 128, 2, 1>, 8, 4, 128, 2, 1, h);
+            else if (KSM == 16) go(head_exact_kernel<E, 16, 4, 128, 2, 1>, 16, 4, 128, 2, 1, h);
+            else go(head_exact_kernel<E, 32, 4, 128, 2, 1>, 32, 4, 128, 2, 1, h);
+        } else if (tt64 && KSM == 32) {
+            go(head_exact_kernel<E, 32, 8, 256, 2, 2>, 32, 8, 256, 2, 2, h);
+        } else {
+            if (KSM == 8) go(head_exact_kernel<E, 8, 8, 256, 4, 1>, 8, 8, 256, 4, 1, h);
+            else if (KSM == 16) go(head_exact_kernel<E, 16, 8, 256, 4, 1>, 16, 8, 256, 4, 1, h);
+            else go(head_exact_kernel<E, 32, 8, 256, 4, 1>, 32, 8, 256, 4, 1, h);
+        }
     };
     if (dtype == AVR_DTYPE_F16)
-        run(__half{}, h);
+        run(__half{});
     else
-        run(__hip_bfloat16{}, h);
+        run(__hip_bfloat16{});
     return check_launch("avr_head_fwd_exact");
 }

@@ -24,10 +24,14 @@
 // epilogue (ReLU, one rounding) leaves as 16-byte stores, 32 rows x 32 B per
 // wave-instruction.  No LDS round trip for the output.
 #include "common.h"
+#include "probe.h"
+#include "stationary.h"
 
 #include <algorithm>
 
 using namespace avr;
+
+AVR_PROBE_TU(avr_probe_set_linear)
 
 namespace {
 
@@ -60,78 +64,109 @@ __device__ __forceinline__ void ldma16(const void* g, uint32_t lds) {
 
 #define AVR_LVMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 0xF) | (0x7 << 4) | (0xF << 8) | (((N) >> 4) << 14))
 
-template <typename E, int WAVES>
-__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES / 4, WAVES / 4))) void
-linear_xs_kernel(int64_t M, int N, const E* __restrict__ x, const frag8* __restrict__ Wf, E* __restrict__ y,
-                 int relu) {
-    constexpr int NB = kLRing, RPW = kLRows / WAVES, NQ = RPW / 32, DPW = kLKS / WAVES;
-    static_assert(DPW * (NB - 2) <= 63, "ring");
+// s_waitcnt vmcnt(n) for a run-time n (the immediate is a constant: one
+// case per value; n > 63 is clamped to 63, a shorter wait)
+__device__ __forceinline__ void wait_vm(int n) {
+    switch (n) {
+#define AVR_VMC(K) case K: AVR_LVMCNT(K); break;
+        AVR_VMC(0) AVR_VMC(1) AVR_VMC(2) AVR_VMC(3) AVR_VMC(4) AVR_VMC(5) AVR_VMC(6) AVR_VMC(7)
+        AVR_VMC(8) AVR_VMC(9) AVR_VMC(10) AVR_VMC(11) AVR_VMC(12) AVR_VMC(13) AVR_VMC(14) AVR_VMC(15)
+        AVR_VMC(16) AVR_VMC(17) AVR_VMC(18) AVR_VMC(19) AVR_VMC(20) AVR_VMC(21) AVR_VMC(22) AVR_VMC(23)
+        AVR_VMC(24) AVR_VMC(25) AVR_VMC(26) AVR_VMC(27) AVR_VMC(28) AVR_VMC(29) AVR_VMC(30) AVR_VMC(31)
+#undef AVR_VMC
+        default: AVR_LVMCNT(31); break;
+    }
+}
+
+// CT = 32 or 64 columns per W tile (64: half the barriers and DMA waits per
+// item, two accumulators per wave; the ring then holds 2 tiles of 64 KiB).
+template <typename E, int CT, int WAVES, int NB>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(2, 2))) void linear_xs_kernel(
+    int64_t M, int N, const E* __restrict__ x, const frag8* __restrict__ Wf, E* __restrict__ y, int relu) {
+    constexpr int ROWS = 32 * WAVES;  // rows of x per work item
+    constexpr int NC = CT / 32, TILEB = NC * kLTile;
+    constexpr int DPW = NC * kLKS / WAVES;  // 1 KiB DMAs per wave and tile
+    constexpr int ST = 2 * NC;              // 16-byte stores per wave and tile
+    static_assert(NB >= 2 && DPW * NB <= 63, "ring");
+    AVR_PROBE_DECL;
     extern __shared__ __attribute__((aligned(16))) char lds_l[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int half = lane >> 5, j = lane & 31;
-    const int64_t m0 = (int64_t)blockIdx.x * kLRows + RPW * wave;  // the wave's first row
-    const int nt = N / 32;
+    const int64_t r0 = (int64_t)blockIdx.x * ROWS;  // the item's first row
+    const int nt = N / CT;
 
     const uint32_t ring_lds = (uint32_t)(uintptr_t)lds_l;
     auto issue = [&](int tau, int slot) {  // this wave's DPW pieces of W tile tau
-        const char* src = reinterpret_cast<const char*>(Wf) + (int64_t)tau * kLTile + wave * DPW * 1024 + 16 * lane;
-        const uint32_t dst = ring_lds + slot * kLTile + wave * DPW * 1024;
+        const char* src = reinterpret_cast<const char*>(Wf) + (int64_t)tau * TILEB + wave * DPW * 1024 + 16 * lane;
+        const uint32_t dst = ring_lds + slot * TILEB + wave * DPW * 1024;
 #pragma unroll
         for (int d = 0; d < DPW; ++d) ldma16(src + d * 1024, dst + d * 1024);
     };
+    // the wave's 32 rows (rows past M repeat the last one; their stores are
+    // dropped), whole rows by LDS-DMA through the (still idle) ring
+    frag8 a[kLKS];
+    {
+        const E* xr = x + min(r0 + 32 * wave + j, M - 1) * kLK;
+        stat_load_rows512(reinterpret_cast<frag8_t(&)[32]>(a), reinterpret_cast<const uint16_t*>(xr),
+                          lds_l + wave * 16384);
+    }
+    __syncthreads();  // every wave is done with the staging area: the ring may fill
     for (int i = 0; i < NB - 1; ++i)
         if (i < nt) issue(i, i);
-    // the wave's rows (rows past M repeat the last one; their stores are dropped)
-    frag8 a[NQ][kLKS];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const E* xr = x + min(m0 + 32 * q + j, M - 1) * kLK + 8 * half;
-#pragma unroll
-        for (int ks = 0; ks < kLKS; ++ks) a[q][ks] = *reinterpret_cast<const frag8*>(xr + 16 * ks);
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-        for (int ks = 0; ks < kLKS; ++ks) asm volatile("" ::"v"(a[q][ks]));
     AVR_LVMCNT(0);
     __syncthreads();
+    AVR_PROBE_MARK(2);
+    // the item's rows of y as a buffer resource: stores to rows past M fall
+    // outside it and are dropped without a branch, so every wave issues the
+    // same number of stores (the vmcnt accounting below relies on it)
+    const int64_t nrows = min<int64_t>(ROWS, M - r0);
+    const __amdgpu_buffer_rsrc_t yres =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(y + r0 * N), (short)0, (int)(nrows * N * 2), 0x00020000);
+    const int rl = 32 * wave + j;  // the lane's row within the item
 
     for (int tau = 0; tau < nt; ++tau) {
+        AVR_PROBE_BEGIN(comp);
         if (tau + NB - 1 < nt) issue(tau + NB - 1, (tau + NB - 1) % NB);  // the slot tile tau-1 left
-        const char* bsrc = lds_l + (tau % NB) * kLTile + 16 * lane;
-        constexpr int D = 8;
-        frag8 bw[D];
+        const char* bsrc = lds_l + (tau % NB) * TILEB + 16 * lane;
+        constexpr int D = 8 / NC;  // k-steps of B fragments read ahead
+        frag8 bw[D][NC];
 #pragma unroll
-        for (int u = 0; u < D; ++u) bw[u] = *reinterpret_cast<const frag8*>(bsrc + u * 1024);
-        f32x16 acc[NQ];
+        for (int u = 0; u < D; ++u)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) acc[q] = f32x16{};
+            for (int c = 0; c < NC; ++c) bw[u][c] = *reinterpret_cast<const frag8*>(bsrc + c * kLTile + u * 1024);
+        f32x16 acc[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[c] = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < kLKS; ++ks) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                acc[c] = lmfma<E>(bw[ks % D][c], a[ks], acc[c]);
+                if (ks + D < kLKS) bw[ks % D][c] = *reinterpret_cast<const frag8*>(bsrc + c * kLTile + (ks + D) * 1024);
+            }
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, D * NC, 0);
 #pragma unroll
         for (int ks = 0; ks < kLKS; ++ks) {
 #pragma unroll
-            for (int q = 0; q < NQ; ++q) acc[q] = lmfma<E>(bw[ks % D], a[q][ks], acc[q]);
-            if (ks + D < kLKS) bw[ks % D] = *reinterpret_cast<const frag8*>(bsrc + (ks + D) * 1024);
+            for (int c = 0; c < NC; ++c) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (ks + D < kLKS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
         }
-        __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
-#pragma unroll
-        for (int ks = 0; ks < kLKS; ++ks) {
-            __builtin_amdgcn_sched_group_barrier(0x008, NQ, 0);
-            if (ks + D < kLKS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        // epilogue: register r of acc[q] is column 32 tau + (r & 3) + 8 (r >> 2)
-        // + 4 half of row m0 + 32 q + j.  Group pair (2p, 2p + 1) = columns
+        // epilogue: register r of acc[c] is column CT tau + 32 c + (r & 3) +
+        // 8 (r >> 2) + 4 half of row rl.  Group pair (2p, 2p + 1) = columns
         // 16p + 4 half + 0..3 and 16p + 8 + 4 half + 0..3: after the half swap
         // a lane owns columns 16p + 8 half + 0..7
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int64_t row = m0 + 32 * q + j;
+        for (int c = 0; c < NC; ++c)
 #pragma unroll
             for (int pp = 0; pp < 2; ++pp) {
                 float v[8];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                    v[e] = acc[q][8 * pp + e];
+                    v[e] = acc[c][8 * pp + e];
                     if (relu) v[e] = fmaxf(v[e], 0.0f);
                 }
                 const uint32_t x0 = pack16<E>(v[0], v[1]), x1 = pack16<E>(v[2], v[3]);
@@ -139,20 +174,28 @@ linear_xs_kernel(int64_t M, int N, const E* __restrict__ x, const frag8* __restr
                 const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
                 const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
                 const u32x4 o = u32x4{(uint32_t)s0[0], (uint32_t)s1[0], (uint32_t)s0[1], (uint32_t)s1[1]};
-                if (row < M)
-                    *reinterpret_cast<u32x4*>(y + row * N + 32 * tau + 16 * pp + 8 * half) = o;
+                __builtin_amdgcn_raw_buffer_store_b128(o, yres, (rl * N + CT * tau + 32 * c + 16 * pp + 8 * half) * 2,
+                                                       0, 0);
             }
+        AVR_PROBE_END(comp, 6);
+        AVR_PROBE_BEGIN(dma);
+        if (tau + 1 < nt) {
+            // this wave's pieces of tile tau+1 have landed.  vmcnt counts the
+            // output stores too, in issue order: younger than tile tau+1's
+            // DMAs are the ring's later tiles (at most NB-2) and the stores of
+            // the iterations since tile tau+1 was issued (NB-1 of them, or
+            // 0 .. tau while it came from the prologue), so the wait covers
+            // the DMA only, never a store in flight
+            const int iters = (tau + 2 - NB >= 0) ? NB - 1 : tau + 1;
+            wait_vm(min(NB - 2, nt - 2 - tau) * DPW + iters * ST);
         }
-        if (tau + 1 < nt) {  // this wave's pieces of tile tau+1 have landed (younger tiles may fly)
-            switch (min(NB - 2, nt - 2 - tau)) {
-                case 0: AVR_LVMCNT(0); break;
-                case 1: AVR_LVMCNT(DPW); break;
-                default: AVR_LVMCNT(2 * DPW); break;
-            }
-        }
+        AVR_PROBE_END(dma, 4);
+        AVR_PROBE_BEGIN(bar);
         __builtin_amdgcn_s_waitcnt(0xC07F);  // every LDS read of tile tau done
         __builtin_amdgcn_s_barrier();
+        AVR_PROBE_END(bar, 5);
     }
+    AVR_PROBE_FLUSH(blockIdx.x * WAVES + wave);
 }
 
 // W [N][K] -> Wf: for column tile tau and k-step ks, the 64 lanes' 16-byte
@@ -170,9 +213,14 @@ __global__ __launch_bounds__(256) void linear_pack_w_kernel(const uint16_t* __re
     }
 }
 
-int lin_waves() {
-    const char* e = getenv("AVR_LINEAR_WAVES_PROBE");
-    return (e && atoi(e) == 4) ? 4 : 8;
+// Item shape (probe: AVR_LINEAR_SHAPE_PROBE): 0 = 128 rows, 32-column tiles,
+// two workgroups per CU (one's prologue under the other's MFMAs); 1 = 256
+// rows, 64-column tiles, one workgroup per CU; 2 = 256 rows, 32-column tiles
+int lin_shape(int N) {
+    const char* e = getenv("AVR_LINEAR_SHAPE_PROBE");
+    const int v = e ? atoi(e) : 0;
+    if (v == 1 && N % 64 == 0) return 1;
+    return v == 2 ? 2 : 0;
 }
 
 }  // namespace
@@ -198,22 +246,25 @@ extern "C" int avr_linear_relu_fwd(int64_t M, int32_t N, int32_t K, const void* 
     AVR_REQUIRE(reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(Wf) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(y) % 16 == 0,
                 "avr_linear_relu_fwd: x, Wf and y must be 16-byte aligned");
-    const int64_t items = (M + kLRows - 1) / kLRows;
+    const int shape = lin_shape(N);
+    const int rows = shape == 0 ? 128 : 256;
+    const int64_t items = (M + rows - 1) / rows;
     AVR_REQUIRE(items < (1ll << 31), "avr_linear_relu_fwd: too many rows");
     hipStream_t st = as_stream(stream);
-    auto go = [&](auto kern, auto e, int waves) {
-        using E = decltype(e);
-        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLLds);
-        hipLaunchKernelGGL(kern, dim3((unsigned)items), dim3(64 * waves), kLLds, st, M, (int)N, (const E*)x,
-                           (const frag8*)Wf, (E*)y, (int)relu);
+    auto run = [&](auto e_tag) {
+        using E = decltype(e_tag);
+        auto go = [&](auto kern, int waves, size_t lds) {
+            (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            hipLaunchKernelGGL(kern, dim3((unsigned)items), dim3(64 * waves), lds, st, M, (int)N, (const E*)x,
+                               (const frag8*)Wf, (E*)y, (int)relu);
+        };
+        if (shape == 0) go(linear_xs_kernel<E, 32, 4, 2>, 4, 2 * (size_t)kLTile);
+        else if (shape == 1) go(linear_xs_kernel<E, 64, 8, 2>, 8, 4 * (size_t)kLTile);
+        else go(linear_xs_kernel<E, 32, 8, 4>, 8, 4 * (size_t)kLTile);
     };
-    const bool w4 = lin_waves() == 4;
-    if (dtype == AVR_DTYPE_F16) {
-        if (w4) go(linear_xs_kernel<__half, 4>, __half{}, 4);
-        else go(linear_xs_kernel<__half, 8>, __half{}, 8);
-    } else {
-        if (w4) go(linear_xs_kernel<__hip_bfloat16, 4>, __hip_bfloat16{}, 4);
-        else go(linear_xs_kernel<__hip_bfloat16, 8>, __hip_bfloat16{}, 8);
-    }
+    if (dtype == AVR_DTYPE_F16)
+        run(__half{});
+    else
+        run(__hip_bfloat16{});
     return check_launch("avr_linear_relu_fwd");
 }

@@ -488,7 +488,7 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
     avr_render_params pp, const float* __restrict__ part, const float* __restrict__ pl,
     const int32_t* __restrict__ shift, const float2* __restrict__ phase,
     const float2* __restrict__ twg, float2* __restrict__ spart, int B, int S, int T, int KS,
-    int kchunk) {
+    int kchunk, int xcd_order) {
     extern __shared__ float2 tw[];           // [T]
     __shared__ float As[32][kKc + 1];
     const int F = T / 2 + 1;
@@ -496,13 +496,22 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
     // XCD-aware order: every workgroup of one s-tile (its k-slices x F-blocks)
     // runs on one XCD (dispatch goes round-robin over the 8 XCDs by
     // workgroup id), so the tile's z rows and phase rows are fetched into
-    // that XCD's L2 once instead of once per k-slice / F-block
+    // that XCD's L2 once instead of once per k-slice / F-block.  With fewer
+    // than 8 s-tiles (S < 225: configs 3 and 4) that order would leave XCDs
+    // idle, so the tile's workgroups are spread over all of them instead.
     (void)P;
     const int nfb = (F + 127) / 128, nst = (S + 31) / 32;
-    const int L = blockIdx.x, xcd = L & 7, q = L >> 3;
     const int per = KS * nfb;  // workgroups of one s-tile
-    const int stile = (q / per) * 8 + xcd;
-    if (stile >= nst) return;  // padding workgroups of the 8-way split
+    int stile, q;
+    if (xcd_order) {
+        const int L = blockIdx.x, xcd = L & 7;
+        q = L >> 3;
+        stile = (q / per) * 8 + xcd;
+        if (stile >= nst) return;  // padding workgroups of the 8-way split
+    } else {
+        stile = blockIdx.x / per;
+        q = blockIdx.x;
+    }
     const int ks = (q % per) / nfb, fblk = (q % per) % nfb;
     const int b = blockIdx.z;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1185,7 +1194,9 @@ extern "C" int avr_dft_phase_fwd(const avr_render_params* p, int32_t B, const fl
     // order the kernel decodes (8 XCDs x ceil(s-tiles / 8) x k-slices x
     // F-blocks; padding ones exit)
     const int nst = (S + 31) / 32;
-    const dim3 grid((unsigned)(8 * ((nst + 7) / 8) * k_split * ((F + 127) / 128)), 1, B);
+    const int xcd_order = nst >= 8;
+    const int per = k_split * ((F + 127) / 128);
+    const dim3 grid((unsigned)(xcd_order ? 8 * ((nst + 7) / 8) * per : nst * per), 1, B);
     const size_t lds = (size_t)T * sizeof(float2);
     auto go = [&](auto kern) {
         if (lds > 65536)
@@ -1194,7 +1205,7 @@ extern "C" int avr_dft_phase_fwd(const avr_render_params* p, int32_t B, const fl
         hipLaunchKernelGGL(kern, grid, dim3(kDftThreads), lds, as_stream(stream), *p, part, pl_table,
                            shift, reinterpret_cast<const float2*>(phase),
                            reinterpret_cast<const float2*>(twiddle),
-                           reinterpret_cast<float2*>(spart), (int)B, S, T, (int)k_split, kchunk);
+                           reinterpret_cast<float2*>(spart), (int)B, S, T, (int)k_split, kchunk, xcd_order);
     };
     switch (n_split) {
         case 1: go(dft_phase_fwd_kernel<1>); break;

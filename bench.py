@@ -223,8 +223,8 @@ def pmc_traffic(workload, dtype_name):
     gfx950 FETCH_SIZE x2 correction applied there), or None."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_*.json")))
-    for path in reversed(files):
+    best = None
+    for path in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_*.json")):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
@@ -233,8 +233,11 @@ def pmc_traffic(workload, dtype_name):
             continue
         for k, v in d["kernels"].items():
             if k.startswith("void ray_reduce_fwd_kernel<" + dtype_name):
-                return v["hbm_bytes"], os.path.relpath(path, ROOT)
-    return None, None
+                # newest by the round and time recorded in the summary, not by file name
+                key = (int(d.get("round", 0)), str(d.get("measured_at", "")))
+                if best is None or key > best[0]:
+                    best = (key, v["hbm_bytes"], os.path.relpath(path, ROOT))
+    return (best[1], best[2]) if best else (None, None)
 
 
 def roofline(w, timer, dt):

@@ -11,6 +11,7 @@ from __future__ import annotations
 import csv
 import json
 import os
+import re
 import statistics
 import sys
 
@@ -27,7 +28,12 @@ def per_kernel(path):
 def main(fetch_dir, write_dir, out, workload="c2_meshrir_1024x256x512"):
     f = per_kernel(fetch_dir)
     w = per_kernel(write_dir)
+    import datetime
+    m = re.match(r"r(\d+)_", os.path.basename(out))
     res = {"workload": workload, "unit": "bytes per launch",
+           # bench.py's pmc_traffic takes the newest summary by (round, measured_at)
+           "round": int(m.group(1)) if m else 0,
+           "measured_at": datetime.datetime.now(datetime.timezone.utc).isoformat(timespec="seconds"),
            "correction": "FETCH_SIZE*1024*2 (gfx950 half-count on wide streaming reads), WRITE_SIZE*1024",
            "kernels": {}}
     for k in sorted(set(f) | set(w)):

@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--M", type=int, default=262144)
     ap.add_argument("--N", type=int, default=512)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--waves", default="8,4", help="AVR_LINEAR_WAVES_PROBE values, interleaved --reps times")
+    ap.add_argument("--shapes", default="0,1,2", help="AVR_LINEAR_SHAPE_PROBE values, interleaved --reps times")
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=200)
     args = ap.parse_args()
@@ -55,9 +55,9 @@ def main():
     torch.cuda.synchronize()
     runs = []
     for _ in range(args.reps):
-        runs += [("avr_linear_relu_fwd", ours, d) for d in args.waves.split(",")] + [("hipblaslt_addmm_activation", blas, "0")]
+        runs += [("avr_linear_relu_fwd", ours, d) for d in args.shapes.split(",")] + [("hipblaslt_addmm_activation", blas, "0")]
     for name, fn, dbg in runs:
-        os.environ["AVR_LINEAR_WAVES_PROBE"] = dbg
+        os.environ["AVR_LINEAR_SHAPE_PROBE"] = dbg
         for _ in range(3):
             fn()
         torch.cuda.synchronize()
@@ -68,7 +68,7 @@ def main():
         e1.record()
         e1.synchronize()
         ms = e0.elapsed_time(e1) / args.iters
-        print(json.dumps({"kernel": name, "waves": int(dbg), "dtype": args.dtype, "M": M, "N": N, "K": K, "us": ms * 1e3,
+        print(json.dumps({"kernel": name, "shape": int(dbg), "dtype": args.dtype, "M": M, "N": N, "K": K, "us": ms * 1e3,
                           "pflops": 2 * M * N * K / (ms * 1e-3) / 1e15}), flush=True)
     a, b = ours().float(), blas().float()
     print(json.dumps({"equal_fraction": float((a == b).float().mean()),
