@@ -141,8 +141,8 @@ _SIGS = {
     "avr_head_pack_w": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp, _c_i32, _vp, _vp]),
     "avr_head_exact_layout": (ctypes.c_int, [_vp, _c_i32, _c_i32, _c_i32, _vp, _vp]),
     "avr_head_pack_w_exact": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32, _vp, _vp]),
-    "avr_head_fwd_exact": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _vp, _c_i32, _vp,
-                                          _vp]),
+    "avr_head_fwd_exact": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp, _c_i32,
+                                          _vp, _vp, _vp]),
     "avr_head_fwd": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _vp, _c_i32, _vp,
                                     _vp]),
     "avr_head_bwd_workspace": (ctypes.c_int, [_vp, _c_i32, _c_i32, _c_i32, _vp]),

@@ -16,25 +16,30 @@
 // [rays x t] plane is a staircase.
 //
 // h stationary, W streamed (round 4).  A work item is (ray block, column):
-// 256 consecutive sorted rays of one column (b, s).  Each of the 4 waves (one
-// per SIMD) loads the h rows of its 64 rays ONCE, from HBM straight into
-// registers: 2 x K/16 MFMA A-fragments (256 VGPRs at K = 512).  The item then
-// sweeps t in tiles of 32 from the first ray's delay to the tail limit; W,
-// shared by every column and resident in each XCD's L2, streams through a
-// 4-tile LDS ring by LDS-DMA in fragment order (avr_head_pack_w_exact), one
-// 1 KiB B-fragment per k-step feeding the wave's two 32-ray MFMA chains.
-// h crosses HBM exactly once (268 MB at config 2) and only W's 32 KB per
-// tile moves through LDS-DMA.  A wave whose 64 rays are not live yet in a
-// tile skips its chains (32 x 64 staircase granularity).
+// RAYS consecutive sorted rays of one column (b, s); each wave owns 32 of
+// them and holds their h rows as the A operand of v_mfma_f32_32x32x16 for
+// the whole item (K/16 fragments, 128 VGPRs at K = 512), loaded ONCE: whole
+// 1 KiB rows by LDS-DMA through the (then idle) ring, then into registers
+// (stationary.h).  The item sweeps t in tiles of 32 NC from its first ray's
+// delay to the tail limit; W, shared by every column and resident in each
+// XCD's L2, streams through an NB-tile LDS ring by LDS-DMA in B-fragment
+// order (avr_head_pack_w_exact).  h crosses HBM once (268 MB at config 2);
+// only W's tiles move through LDS-DMA.  A wave whose rays are not live yet in
+// a 32-t group skips its chain (32 x 32 staircase granularity).
 //
 // Per tile every wave rounds, masks (p < cnt[t], select on the VALUE so an
-// overflowed masked product cannot leak 0 * inf) and weights its 32 x 64
+// overflowed masked product cannot leak 0 * inf) and weights its 32 x 32
 // products and sums them per lane in position order; the two lane halves are
-// added, then the 4 waves' partials in wave order.  Each item writes its own
+// added, then the waves' partials in wave order.  Each item writes its own
 // slab zpart[block][b][s][t] (zero outside its live range); avr_dft_phase_fwd
 // sums the n_split slabs in a fixed order, so results are deterministic.
-// Items are ordered block-major (every column's first block first: the
-// longest items start first and the short ones fill the tail).
+//
+// Persistent workgroups (as many as fit: two per CU for 128-ray items) take
+// items from eight work queues, one per XCD's share of the items, in
+// block-major order (every column's first block first: the longest items
+// first, the short ones fill the tail).  The next item's metadata (kept-ray
+// count, rays, cnt, weights, first delay) is loaded while the current item
+// computes, so an item's prologue is its rows' DMA and the first W tile.
 #include "common.h"
 #include "probe.h"
 #include "stationary.h"
@@ -99,11 +104,23 @@ __device__ __forceinline__ void wait_vm(int n) {
     }
 }
 
+// largest T of the 8-wave and the 4-wave items (exact_rays)
+constexpr int kExactMaxT[2] = {4096, 1024};
+
+// threadIdx.x through an empty asm: in a persistent kernel's item loop, the
+// per-lane values derived from it are formed where they are used instead of
+// hoisted out of the loop and held in registers (or spilled) across it
+__device__ __forceinline__ int opaque_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 // bytes of one 32-t W tile in fragment order: KSM k-steps x 64 lanes x 16 B
 __host__ __device__ constexpr int xs_tile_bytes(int KSM) { return KSM * 1024; }
 __host__ __device__ constexpr size_t xs_lds_bytes(int KSM, int T, int waves, int rays, int nb, int nc) {
     return (size_t)nb * nc * xs_tile_bytes(KSM) + 4 * (size_t)((T + 3) / 4 * 4) + 4 * (size_t)rays +
-           4 * (size_t)(2 * waves * 32 * nc) + 4 * (size_t)waves + 16;
+           4 * (size_t)(2 * waves * 32 * nc) + 4 * (size_t)waves + 8;
 }
 
 // One work item: RAYS consecutive sorted rays of one column (b, s), WAVES
@@ -111,11 +128,11 @@ __host__ __device__ constexpr size_t xs_lds_bytes(int KSM, int T, int waves, int
 // of NB W tiles.  <8, 256, 4>: one workgroup per CU (two waves per SIMD);
 // <4, 128, 2>: half the item and ~70 KB of LDS, so two workgroups share a CU
 // and one's prologue and barriers overlap the other's MFMA chains.
-template <typename E, int KSM, int WAVES, int RAYS, int NB, int NC>
-__global__ __launch_bounds__(64 * WAVES) void head_exact_kernel(
+template <typename E, int KSM, int WAVES, int RAYS, int NB, int NC, bool ROWDMA>
+__global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
     avr_render_params pp, int B, int R, int K, const E* __restrict__ h, const frag8* __restrict__ Wf,
     const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
-    float* __restrict__ zpart) {
+    const int32_t* __restrict__ delay, float* __restrict__ zpart, int* __restrict__ queue, int nitems) {
     constexpr int NT = 64 * WAVES, TILE = NC * xs_tile_bytes(KSM);  // a tile: TT = 32 NC values of t
     constexpr int TT = 32 * NC;
     constexpr int RPW = RAYS / WAVES;    // rays per wave
@@ -131,199 +148,279 @@ __global__ __launch_bounds__(64 * WAVES) void head_exact_kernel(
     float* wl = reinterpret_cast<float*>(cl + Tp);              // weights of the item's rays [RAYS]
     float* zr = wl + RAYS;                                      // wave partials [2][WAVES][TT]
     int* dstart = reinterpret_cast<int*>(zr + 2 * WAVES * TT);  // first live t per wave [WAVES]
+    int* qnext = dstart + WAVES;                                // claimed items [2]
 
     const int64_t ncol = (int64_t)B * S;
-    const int64_t col = (int64_t)blockIdx.x % ncol;
-    const int blk = (int)((int64_t)blockIdx.x / ncol);
-    const int s = (int)(col % S), b = (int)(col / S);
-    const int lim = tail_limit(pp, s);
-    const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int half = lane >> 5, j = lane & 31;
-    float* zc = zpart + ((int64_t)blk * ncol + col) * T;
-    const int* cc = cnt + col * T;
-    const int nk = cc[T - 1];  // kept rays of the column
-    const int p0 = blk * RAYS;
-    if (p0 >= nk || lim <= 0) {
-        for (int t = threadIdx.x; t < T; t += NT) zc[t] = 0.0f;
-        return;
-    }
-    // the wave's rows first: their DMA flies under the metadata work below
-    // (positions past the kept rays repeat the last kept ray; masked)
     const int ksn = K / 16;
-    const int pw = p0 + RPW * wave;
-    const bool dma_rows = KSM == 32 && K == 512 && NQ == 1;
-    const E* hrow[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int ray = perm[col * R + min(pw + 32 * q + j, nk - 1)];
-        hrow[q] = h + (((int64_t)b * R + ray) * S + s) * K;
-    }
-    if (dma_rows) {
-        stat_issue_round(reinterpret_cast<const uint16_t*>(hrow[0]), ring + wave * 16384, 0);
-        stat_issue_round(reinterpret_cast<const uint16_t*>(hrow[0]), ring + wave * 16384, 1);
-    }
-
-    // ---- prologue: cnt and the item's weights into LDS; each wave's first live t
-    for (int t = threadIdx.x; t < T; t += NT) cl[t] = cc[t];
-    if (threadIdx.x < RAYS) {
-        const int p = p0 + (int)threadIdx.x;
-        wl[threadIdx.x] = p < nk ? ws[col * R + p] : 0.0f;
-    }
-    if (threadIdx.x < WAVES) dstart[threadIdx.x] = 1 << 30;
-    __syncthreads();
-    for (int t = threadIdx.x; t < lim; t += NT) {  // the delay of sorted ray p0 + RPW w (a kept ray: < lim)
-        const int c = cl[t], cp = t > 0 ? cl[t - 1] : 0;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) {
-            const int pw = p0 + RPW * w;
-            if (c > pw && cp <= pw) dstart[w] = t;
-        }
-    }
-    __syncthreads();
-    AVR_PROBE_MARK(8);
-    const int tb = dstart[0] / TT;              // first tile with a live ray of the item
-    const int te = (lim + TT - 1) / TT;         // tiles holding t < lim
-    const int tw = min(dstart[wave] / TT, te);  // this wave's first live tile
-    for (int t = threadIdx.x; t < T; t += NT)
-        if (t < TT * tb || t >= TT * te) zc[t] = 0.0f;
-
-    // ---- the wave's rays: A fragments (k = 16 ks + 8 half + 0..7), loaded once
-    frag8 a[NQ][KSM];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const E* hr = hrow[q];
-        if (dma_rows) {
-            // whole rows by LDS-DMA through the (still idle) ring, 16 KiB per wave
-            stat_finish_rows512(reinterpret_cast<frag8_t(&)[32]>(a[q]), reinterpret_cast<const uint16_t*>(hr),
-                                ring + wave * 16384);
-        } else {
-#pragma unroll
-            for (int ks = 0; ks < KSM; ++ks)
-                a[q][ks] = *reinterpret_cast<const frag8*>(hr + 8 * half + 16 * min(ks, ksn - 1));
-#pragma unroll
-            for (int ks = 0; ks < KSM; ++ks)
-                if (ks >= ksn) a[q][ks] = frag8{0u, 0u, 0u, 0u};
-#pragma unroll
-            for (int ks = 0; ks < KSM; ++ks) asm volatile("" ::"v"(a[q][ks]));
-            AVR_VMCNT(0);
-        }
-    }
-    AVR_PROBE_MARK(9);
-    __syncthreads();  // every wave is done with the staging area: the ring may fill
-    AVR_PROBE_MARK(10);
+    constexpr bool dma_rows = ROWDMA;  // K == 512: whole 1 KiB rows by LDS-DMA
     const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
-    auto issue = [&](int tau, int slot) {  // W tile tau into ring slot `slot`: this wave's DPW pieces
-        const char* src = reinterpret_cast<const char*>(Wf) + (int64_t)tau * TILE + wave * DPW * 1024 + 16 * lane;
-        const uint32_t dst = ring_lds + slot * TILE + wave * DPW * 1024;
-#pragma unroll
-        for (int d = 0; d < DPW; ++d) dma_row16(src + d * 1024, dst + d * 1024);
-    };
-    for (int i = 0; i < NB - 1; ++i)
-        if (tb + i < te) issue(tb + i, i);
-    AVR_VMCNT(0);
-    __syncthreads();
-    AVR_PROBE_MARK(2);
 
-    // the wave's 32 rays against 32-t column group c of the tile in ring slot
-    // `slot`: one MFMA chain over K (A from registers, B read from the ring
-    // D k-steps ahead), then the epilogue (rounded, masked by value:
-    // p < cnt[t], weighted, summed per lane in row order)
-    const float* wq = wl + RPW * wave + 4 * half;
-    auto group = [&](int slot, int tau, int c) {
-        const char* bsrc = ring + slot * TILE + c * xs_tile_bytes(KSM) + 16 * lane;
-        constexpr int D = KSM < 8 ? KSM : 8;  // B fragments read ahead
-        frag8 bw[D];
+    // ---- work queue: items x, x + 8, x + 16, ... (block-major: longest
+    // first) are served by queue x = blockIdx.x % 8 to its G/8 workgroups;
+    // claims 0, 1 and 2 of workgroup l are l, G/8 + l and 2 G/8 + l, later
+    // ones come from the queue's counter (zeroed by the host before the
+    // launch).  A claim is made two items ahead: thread 0 claims at the start
+    // of item i, publishes it in LDS at the end of item i, and every thread
+    // reads it at the end of item i + 1 (barriers in between; two slots).
+    const int qx = blockIdx.x & 7, gq = gridDim.x >> 3, ql = blockIdx.x >> 3;
+    int* qctr = queue + 32 * qx;  // one 128-byte line per counter
+    auto item_of = [&](int claim) { return qx + 8 * claim; };
+
+    // metadata of an item, loaded one item ahead: every load independent of
+    // the others (a claim past the last item loads a clamped, valid address),
+    // all of them vector loads (lane-varying addresses): a scalar load in
+    // flight would hold up every lgkmcnt wait of the LDS traffic meanwhile
+    constexpr int CLN = (kExactMaxT[WAVES == 4] + NT - 1) / NT;  // cnt values per thread
+    struct Meta {
+        int item, nk, ray, dly;
+        int clv[CLN];
+        float wsv;
+    };
+    auto load_meta = [&](int item, Meta& m) {
+        const int tid = opaque_tid();
+        m.item = item;
+        const int it = min(item, nitems - 1);
+        const int64_t col = (int64_t)it % ncol;
+        const int blk = (int)((int64_t)it / ncol);
+        const int* cc = cnt + col * T;
+        m.nk = cc[T - 1 - (tid >> 12)];  // kept rays of the column (tid < 4096: T - 1)
+        // the ray of each lane's sorted position (avr_head_sort leaves ray 0
+        // past the kept rays: a valid row, masked by weight and count)
+        m.ray = perm[col * R + min(blk * RAYS + RPW * wave + (tid & 31), R - 1)];
 #pragma unroll
-        for (int u = 0; u < D; ++u) bw[u] = *reinterpret_cast<const frag8*>(bsrc + u * 1024);
-        f32x16 acc = f32x16{};
+        for (int u = 0; u < CLN; ++u) m.clv[u] = cc[min(tid + NT * u, T - 1)];
+        m.wsv = ws[col * R + min(blk * RAYS + tid, R - 1)];
+    };
+    // each wave's first live t: the delay of its first sorted ray (sorted by
+    // delay, so cnt[t] > pw from that t on; lane 0's value); issued once
+    // m.ray has landed
+    auto load_dly = [&](Meta& m) {
+        const int it = min(m.item, nitems - 1);
+        const int64_t col = (int64_t)it % ncol;
+        const int s = (int)(col % S), b = (int)(col / S);
+        m.dly = delay[((int64_t)b * R + m.ray) * S + s];
+    };
+    // wait for a prefetched item's loads here (empty asm uses): the compiler
+    // places its wait at the first use, which must not be at the next item's
+    // start, behind that item's own fresh loads
+    auto touch = [&](Meta& m) {
+        asm volatile("" ::"v"(m.nk), "v"(m.ray), "v"(m.dly), "v"(m.wsv));
 #pragma unroll
-        for (int ks = 0; ks < KSM; ++ks) {
-            acc = mfma16<E>(a[0][ks], bw[ks % D], acc);
-            if (ks + D < KSM) bw[ks % D] = *reinterpret_cast<const frag8*>(bsrc + (ks + D) * 1024);
+        for (int u = 0; u < CLN; ++u) asm volatile("" ::"v"(m.clv[u]));
+    };
+
+    Meta cur, nx;
+    int item = item_of(ql), nxt = item_of(gq + ql);
+    load_meta(item, cur);
+    load_dly(cur);
+    if (threadIdx.x == 0) qnext[1] = item_of(2 * gq + ql);
+    __syncthreads();
+    for (int iter = 0; item < nitems; ++iter) {
+        AVR_PROBE_DECL;
+        const int tid = opaque_tid();
+        const int lane = tid & 63, half = lane >> 5, j = lane & 31;
+        const int64_t col = (int64_t)item % ncol;
+        const int blk = (int)((int64_t)item / ncol);
+        const int s = (int)(col % S), b = (int)(col / S);
+        const int lim = tail_limit(pp, s);
+        float* zc = zpart + ((int64_t)blk * ncol + col) * T;
+        const int p0 = blk * RAYS;
+        const int pw = p0 + RPW * wave;
+        const int nk = __builtin_amdgcn_readfirstlane(cur.nk);
+        // a claim two items ahead (kept in thread 0's register until this item ends)
+        int claim = 0;
+        if (tid == 0) {
+            // the counter's offset through an empty asm: not provably uniform,
+            // so the compiler's wave-aggregating atomic rewrite (which waits for
+            // the result on the spot) does not apply; the wait is at the use
+            int zero = 0;
+            asm volatile("" : "+v"(zero));
+            claim = __hip_atomic_fetch_add(qctr + zero, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
-#pragma unroll
-        for (int ks = 0; ks < KSM; ++ks) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            if (ks + D < KSM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        // register r of acc is row (r & 3) + 8 (r >> 2) + 4 half of the wave's
-        // rays, column t = TT tau + 32 c + j
-        const int t0 = TT * tau + 32 * c;
-        const int t = t0 + j;
-        const int full = __builtin_amdgcn_readfirstlane((t0 + 31 < lim) ? cl[t0] : 0);
-        float z = 0.0f;
-        if (pw + 32 <= full) {  // every (ray, t) pair of the group is live
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float4 w4 = *reinterpret_cast<const float4*>(wq + 8 * g);
-                z = fmaf(w4.x, round16<E>(acc[4 * g + 0]), z);
-                z = fmaf(w4.y, round16<E>(acc[4 * g + 1]), z);
-                z = fmaf(w4.z, round16<E>(acc[4 * g + 2]), z);
-                z = fmaf(w4.w, round16<E>(acc[4 * g + 3]), z);
-            }
+        // the next item's metadata: in flight under this item (older than its DMA)
+        load_meta(nxt, nx);
+        bool dly_issued = false, touched = false;
+        if (p0 >= nk || lim <= 0) {
+            for (int t = tid; t < T; t += NT) zc[t] = 0.0f;
+            load_dly(nx);
+            dly_issued = true;
         } else {
-            const int ct = t < lim ? cl[min(t, T - 1)] : 0;
+            // ---- prologue: the wave's rows by LDS-DMA through the (idle) ring
+            const E* hrow = h + (((int64_t)b * R + cur.ray) * S + s) * K;
+            frag8 a[NQ][KSM];
+            if constexpr (dma_rows) {
+                // every fragment defined before the lane-masked round writes:
+                // an undefined start would let the compiler carry the previous
+                // item's fragments into this item's prologue (128 more VGPRs)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float4 w4 = *reinterpret_cast<const float4*>(wq + 8 * g);
-                const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+                for (int ks = 0; ks < KSM; ++ks) a[0][ks] = frag8{0u, 0u, 0u, 0u};
+                stat_issue_round(reinterpret_cast<const uint16_t*>(hrow), ring + wave * 16384, 0);
+                stat_issue_round(reinterpret_cast<const uint16_t*>(hrow), ring + wave * 16384, 1);
+                AVR_PROBE_MARK(8);
+                stat_finish_rows512(reinterpret_cast<frag8_t(&)[32]>(a[0]), reinterpret_cast<const uint16_t*>(hrow),
+                                    ring + wave * 16384);
+            } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float v = round16<E>(acc[4 * g + e]);
-                    z = fmaf(wv[e], (pw + 8 * g + 4 * half + e < ct) ? v : 0.0f, z);
+                for (int ks = 0; ks < KSM; ++ks)
+                    a[0][ks] = *reinterpret_cast<const frag8*>(hrow + 8 * half + 16 * min(ks, ksn - 1));
+#pragma unroll
+                for (int ks = 0; ks < KSM; ++ks)
+                    if (ks >= ksn) a[0][ks] = frag8{0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int ks = 0; ks < KSM; ++ks) asm volatile("" ::"v"(a[0][ks]));
+                AVR_VMCNT(0);
+            }
+            AVR_PROBE_MARK(9);
+            // cnt, the item's weights and the waves' first live t into LDS
+#pragma unroll
+            for (int u = 0; u < CLN; ++u) {
+                const int t = tid + NT * u;
+                if (t < T) cl[t] = cur.clv[u];
+            }
+            if (tid < RAYS) wl[tid] = p0 + tid < nk ? cur.wsv : 0.0f;
+            if (lane == 0) dstart[wave] = pw < nk ? cur.dly : 1 << 30;
+            __syncthreads();  // staging area free: the ring may fill; cl, wl, dstart written
+            AVR_PROBE_MARK(10);
+            const int tb = dstart[0] / TT;       // first tile with a live ray of the item
+            const int te = (lim + TT - 1) / TT;  // tiles holding t < lim
+            for (int t = tid; t < T; t += NT)
+                if (t < TT * tb || t >= TT * te) zc[t] = 0.0f;
+            auto issue = [&](int tau, int slot) {  // W tile tau into ring slot `slot`: this wave's DPW pieces
+                const char* src =
+                    reinterpret_cast<const char*>(Wf) + (int64_t)tau * TILE + wave * DPW * 1024 + 16 * lane;
+                const uint32_t dst = ring_lds + slot * TILE + wave * DPW * 1024;
+#pragma unroll
+                for (int d = 0; d < DPW; ++d) dma_row16(src + d * 1024, dst + d * 1024);
+            };
+            for (int i = 0; i < NB - 1; ++i)
+                if (tb + i < te) issue(tb + i, i);
+            AVR_VMCNT(0);
+            __syncthreads();
+            AVR_PROBE_MARK(2);
+
+            // the wave's 32 rays against 32-t column group c of the tile in
+            // ring slot `slot`: one MFMA chain over K (A from registers, B read
+            // from the ring D k-steps ahead), then the epilogue (rounded,
+            // masked by value: p < cnt[t], weighted, summed per lane in row order)
+            const float* wq = wl + RPW * wave + 4 * half;
+            auto group = [&](int slot, int tau, int c) {
+                const char* bsrc = ring + slot * TILE + c * xs_tile_bytes(KSM) + 16 * lane;
+                constexpr int D = KSM < 8 ? KSM : 8;  // B fragments read ahead
+                frag8 bw[D];
+#pragma unroll
+                for (int u = 0; u < D; ++u) bw[u] = *reinterpret_cast<const frag8*>(bsrc + u * 1024);
+                f32x16 acc = f32x16{};
+#pragma unroll
+                for (int ks = 0; ks < KSM; ++ks) {
+                    acc = mfma16<E>(a[0][ks], bw[ks % D], acc);
+                    if (ks + D < KSM) bw[ks % D] = *reinterpret_cast<const frag8*>(bsrc + (ks + D) * 1024);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
+#pragma unroll
+                for (int ks = 0; ks < KSM; ++ks) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (ks + D < KSM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+                // register r of acc is row (r & 3) + 8 (r >> 2) + 4 half of the
+                // wave's rays, column t = TT tau + 32 c + j
+                const int t0 = TT * tau + 32 * c;
+                const int t = t0 + j;
+                const int full = __builtin_amdgcn_readfirstlane((t0 + 31 < lim) ? cl[t0] : 0);
+                float z = 0.0f;
+                if (pw + 32 <= full) {  // every (ray, t) pair of the group is live
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const float4 w4 = *reinterpret_cast<const float4*>(wq + 8 * g);
+                        z = fmaf(w4.x, round16<E>(acc[4 * g + 0]), z);
+                        z = fmaf(w4.y, round16<E>(acc[4 * g + 1]), z);
+                        z = fmaf(w4.z, round16<E>(acc[4 * g + 2]), z);
+                        z = fmaf(w4.w, round16<E>(acc[4 * g + 3]), z);
+                    }
+                } else {
+                    const int ct = t < lim ? cl[min(t, T - 1)] : 0;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const float4 w4 = *reinterpret_cast<const float4*>(wq + 8 * g);
+                        const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float v = round16<E>(acc[4 * g + e]);
+                            z = fmaf(wv[e], (pw + 8 * g + 4 * half + e < ct) ? v : 0.0f, z);
+                        }
+                    }
+                }
+                return z;
+            };
+            for (int tau = tb; tau < te; ++tau) {
+                const int i = tau - tb;
+                AVR_PROBE_BEGIN(comp);
+                if (tau + NB - 1 < te) issue(tau + NB - 1, (i + NB - 1) % NB);  // the slot tile tau-1 left
+                float zl[NC];
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    // group c holds a live ray of the wave from the wave's first
+                    // live t on (cnt is nondecreasing in t), nothing at or past lim
+                    const int t0 = TT * tau + 32 * c;
+                    zl[c] = (t0 + 31 >= dstart[wave] && t0 < lim) ? group(i % NB, tau, c) : 0.0f;
+                }
+                AVR_PROBE_END(comp, 6);
+                // lower + upper lane half (rows 4 half + ...), the same association in every lane
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zl[c]), __float_as_uint(zl[c]),
+                                                                    false, false);
+                    const float v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+                    if (half == 0) zr[(i & 1) * (WAVES * TT) + wave * TT + 32 * c + j] = v;
+                }
+                AVR_PROBE_BEGIN(dma);
+                if (tau + 1 < te) {
+                    // this wave's pieces of tile tau+1 have landed.  Younger in
+                    // vmcnt: the ring's later tiles and this wave's partial
+                    // stores since tile tau+1 was issued (a wave stores after
+                    // the barrier of iteration m when wave == m % WAVES), so no
+                    // store in flight is waited for
+                    int st = 0;
+                    for (int m = max(0, i + 2 - NB); m < i; ++m) st += (wave == m % WAVES);
+                    wait_vm(min(NB - 2, te - 2 - tau) * DPW + st);
+                }
+                if (i == 0) {
+                    // the next item's delay (its ray has landed): older than
+                    // the tiles issued from the next iteration on
+                    load_dly(nx);
+                    dly_issued = true;
+                }
+                if (tau == te - 1) {  // before the last partial store: nothing young to wait for
+                    touch(nx);
+                    touched = true;
+                }
+                AVR_PROBE_END(dma, 4);
+                AVR_PROBE_BEGIN(bar);
+                __builtin_amdgcn_s_waitcnt(0xC07F);  // every LDS access of tile tau (and the partials) done
+                __builtin_amdgcn_s_barrier();
+                AVR_PROBE_END(bar, 5);
+                if (wave == (i % WAVES) && lane < TT) {  // the wave partials of tile tau, in wave order
+                    const float* zz = zr + (i & 1) * (WAVES * TT) + lane;
+                    float v = zz[0];
+#pragma unroll
+                    for (int w = 1; w < WAVES; ++w) v += zz[TT * w];
+                    const int t = TT * tau + lane;
+                    if (t < T) zc[t] = v;
                 }
             }
+            // the next item's prologue rewrites the ring and the LDS metadata:
+            // every wave has passed the last tile's barrier, after which only
+            // the partials zr are read (rewritten after two more barriers)
         }
-        return z;
-    };
-    for (int tau = tb; tau < te; ++tau) {
-        const int i = tau - tb;
-        AVR_PROBE_BEGIN(comp);
-        if (tau + NB - 1 < te) issue(tau + NB - 1, (i + NB - 1) % NB);  // the slot tile tau-1 left
-        float zl[NC];
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            // group c holds a live ray of the wave from the wave's first live t
-            // on (cnt is nondecreasing in t), and nothing at or past lim
-            const int t0 = TT * tau + 32 * c;
-            zl[c] = (t0 + 31 >= dstart[wave] && t0 < lim) ? group(i % NB, tau, c) : 0.0f;
-        }
-        AVR_PROBE_END(comp, 6);
-        // lower + upper lane half (rows 4 half + ...), the same association in every lane
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-            const auto r =
-                __builtin_amdgcn_permlane32_swap(__float_as_uint(zl[c]), __float_as_uint(zl[c]), false, false);
-            const float v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-            if (half == 0) zr[(i & 1) * (WAVES * TT) + wave * TT + 32 * c + j] = v;
-        }
-        AVR_PROBE_BEGIN(dma);
-        if (tau + 1 < te) {
-            // this wave's pieces of tile tau+1 have landed.  Younger in vmcnt:
-            // the ring's later tiles and this wave's partial stores since tile
-            // tau+1 was issued (a wave stores after the barrier of iteration m
-            // when wave == m % WAVES), so no store in flight is waited for
-            int st = 0;
-            for (int m = max(0, i + 2 - NB); m < i; ++m) st += (wave == m % WAVES);
-            wait_vm(min(NB - 2, te - 2 - tau) * DPW + st);
-        }
-        AVR_PROBE_END(dma, 4);
-        AVR_PROBE_BEGIN(bar);
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // every LDS access of tile tau (and the partials) done
-        __builtin_amdgcn_s_barrier();
-        AVR_PROBE_END(bar, 5);
-        if (wave == (i % WAVES) && lane < TT) {  // the wave partials of tile tau, in wave order
-            const float* zz = zr + (i & 1) * (WAVES * TT) + lane;
-            float v = zz[0];
-#pragma unroll
-            for (int w = 1; w < WAVES; ++w) v += zz[TT * w];
-            const int t = TT * tau + lane;
-            if (t < T) zc[t] = v;
-        }
+        if (!dly_issued) load_dly(nx);
+        if (!touched) touch(nx);
+        if (tid == 0) qnext[iter & 1] = item_of(3 * gq + claim);
+        if (p0 >= nk || lim <= 0) __syncthreads();  // every item has a barrier between the qnext accesses
+        AVR_PROBE_FLUSH((int64_t)item * WAVES + wave);
+        item = nxt;
+        nxt = qnext[(iter + 1) & 1];
+        cur = nx;
     }
-    AVR_PROBE_FLUSH(blockIdx.x * WAVES + wave);
 }
 
 // W [T][K] -> Wf: for t-tile tau and k-step ks, the 64 lanes' 16-byte B
@@ -343,6 +440,8 @@ __global__ __launch_bounds__(256) void head_pack_exact_kernel(int T, int K, int 
         Wf[i] = v;
     }
 }
+
+constexpr int kExactQueueInts = 256;  // 8 work-queue counters, one 128-byte line each
 
 int exact_ksm(int K) { return K <= 128 ? 8 : (K <= 256 ? 16 : 32); }
 
@@ -380,6 +479,20 @@ void allow_lds(Kern k, size_t lds) {
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
 }
 
+// CUs of the current device (cached per device)
+int device_cus() {
+    static int cus[64] = {};
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev < 0 || dev >= 64) return 256;
+    if (!cus[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+
 }  // namespace
 
 extern "C" int avr_head_exact_layout(const avr_render_params* p, int32_t B, int32_t K, int32_t dtype,
@@ -408,8 +521,10 @@ extern "C" int avr_head_pack_w_exact(const avr_render_params* p, int32_t K, cons
 
 extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* Wf,
                                   int32_t dtype, const int32_t* perm, const float* ws, const int32_t* cnt,
-                                  int32_t n_split, float* zpart, void* stream) {
-    AVR_REQUIRE(p && B >= 1 && h && Wf && perm && ws && cnt && zpart, "avr_head_fwd_exact: bad args");
+                                  const int32_t* delay, int32_t n_split, float* zpart, int32_t* queue,
+                                  void* stream) {
+    AVR_REQUIRE(p && B >= 1 && h && Wf && perm && ws && cnt && delay && zpart && queue,
+                "avr_head_fwd_exact: bad args");
     if (int e = exact_check(p, K, dtype)) return e;
     AVR_REQUIRE(reinterpret_cast<uintptr_t>(h) % 16 == 0 && reinterpret_cast<uintptr_t>(Wf) % 16 == 0,
                 "avr_head_fwd_exact: h and Wf must be 16-byte aligned");
@@ -427,19 +542,31 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
         auto go = [&](auto kern, int ksm, int waves, int rays, int nb, int nc, const void* hv) {
             const size_t lds = xs_lds_bytes(ksm, T, waves, rays, nb, nc);
             allow_lds(kern, lds);
-            hipLaunchKernelGGL(kern, dim3((unsigned)items), dim3(64 * waves), lds, st, *p, (int)B, R, (int)K,
-                               (const E*)hv, (const frag8*)Wf, perm, ws, cnt, zpart);
+            // persistent workgroups: as many as fit on the chip at once (a
+            // multiple of 8: one work queue per XCD), at most one per 8 items
+            int per_cu = 1;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * waves, lds) != hipSuccess ||
+                per_cu < 1)
+                per_cu = 1;
+            const int64_t gq = std::min<int64_t>((int64_t)device_cus() * per_cu / 8, (items + 7) / 8);
+            const int grid = 8 * (int)std::max<int64_t>(gq, 1);
+            (void)hipMemsetAsync(queue, 0, kExactQueueInts * sizeof(int32_t), st);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), lds, st, *p, (int)B, R, (int)K, (const E*)hv,
+                               (const frag8*)Wf, perm, ws, cnt, delay, zpart, (int*)queue, (int)items);
         };
+        const bool rowdma = K == 512;
         if (small) {
-            if (KSM == 8) go(head_exact_kernel<E, 8, 4, 128, 2, 1>, 8, 4, 128, 2, 1, h);
-            else if (KSM == 16) go(head_exact_kernel<E, 16, 4, 128, 2, 1>, 16, 4, 128, 2, 1, h);
-            else go(head_exact_kernel<E, 32, 4, 128, 2, 1>, 32, 4, 128, 2, 1, h);
-        } else if (tt64 && KSM == 32) {
-            go(head_exact_kernel<E, 32, 8, 256, 2, 2>, 32, 8, 256, 2, 2, h);
+            if (KSM == 8) go(head_exact_kernel<E, 8, 4, 128, 2, 1, false>, 8, 4, 128, 2, 1, h);
+            else if (KSM == 16) go(head_exact_kernel<E, 16, 4, 128, 2, 1, false>, 16, 4, 128, 2, 1, h);
+            else if (rowdma) go(head_exact_kernel<E, 32, 4, 128, 2, 1, true>, 32, 4, 128, 2, 1, h);
+            else go(head_exact_kernel<E, 32, 4, 128, 2, 1, false>, 32, 4, 128, 2, 1, h);
+        } else if (tt64 && rowdma) {
+            go(head_exact_kernel<E, 32, 8, 256, 2, 2, true>, 32, 8, 256, 2, 2, h);
         } else {
-            if (KSM == 8) go(head_exact_kernel<E, 8, 8, 256, 4, 1>, 8, 8, 256, 4, 1, h);
-            else if (KSM == 16) go(head_exact_kernel<E, 16, 8, 256, 4, 1>, 16, 8, 256, 4, 1, h);
-            else go(head_exact_kernel<E, 32, 8, 256, 4, 1>, 32, 8, 256, 4, 1, h);
+            if (KSM == 8) go(head_exact_kernel<E, 8, 8, 256, 4, 1, false>, 8, 8, 256, 4, 1, h);
+            else if (KSM == 16) go(head_exact_kernel<E, 16, 8, 256, 4, 1, false>, 16, 8, 256, 4, 1, h);
+            else if (rowdma) go(head_exact_kernel<E, 32, 8, 256, 4, 1, true>, 32, 8, 256, 4, 1, h);
+            else go(head_exact_kernel<E, 32, 8, 256, 4, 1, false>, 32, 8, 256, 4, 1, h);
         }
     };
     if (dtype == AVR_DTYPE_F16)

@@ -31,8 +31,17 @@ __device__ __forceinline__ void stat_dma16(const void* g, uint32_t lds) {
 // 16-byte chunks rotated by jr slots (the DMA source of lane i is chunk
 // (i + jr) mod 64), so the 8 rows one fragment read touches fall on
 // distinct banks.
+// The lane index through an empty asm: a value the compiler cannot hoist out
+// of an enclosing loop, so the per-lane offsets below are formed where they
+// are used instead of held in registers across a persistent kernel's loop.
+__device__ __forceinline__ int stat_lane() {
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
+    return lane;
+}
+
 __device__ __forceinline__ void stat_issue_round(const uint16_t* row, char* stage, int k) {
-    const int lane = threadIdx.x & 63;
+    const int lane = stat_lane();
     const uint32_t st = (uint32_t)(uintptr_t)stage + (k & 1) * 8192;
     const uint64_t rowp = (uint64_t)(uintptr_t)row;
 #pragma unroll
@@ -53,7 +62,7 @@ __device__ __forceinline__ void stat_issue_round(const uint16_t* row, char* stag
 // while round k's fragments are read.  Leaves no DMA in flight and every
 // LDS read done.  K = 512.
 __device__ __forceinline__ void stat_finish_rows512(frag8_t (&a)[32], const uint16_t* row, char* stage) {
-    const int lane = threadIdx.x & 63;
+    const int lane = stat_lane();
     const int j = lane & 31, half = lane >> 5, jr = j & 7;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {

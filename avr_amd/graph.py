@@ -151,11 +151,14 @@ class GraphedRender:
         torch.rand(g.jit_n, out=g.jit_h)
         B = g.B
         if g.host_pose:
-            p = g.pose_np  # numpy view of the pinned buffer: no dispatcher per copy
-            p[:3 * B] = rays_o.detach().reshape(-1).numpy()
-            p[3 * B:6 * B] = position_tx.detach().reshape(-1).numpy()
-            if g.has_dtx:
-                p[6 * B:] = direction_tx.detach().reshape(-1).numpy()
+            poses = (rays_o, position_tx, direction_tx) if g.has_dtx else (rays_o, position_tx)
+            nb = 12 * B
+            for k, t in enumerate(poses):
+                if t.dtype is torch.float32 and t.is_contiguous():
+                    # one memmove into the pinned buffer: no dispatcher call
+                    ctypes.memmove(g.buf._h + k * nb, t.data_ptr(), nb)
+                else:
+                    g.pose_np[3 * B * k:3 * B * (k + 1)] = t.detach().reshape(-1).float().numpy()
         elif g.dtx is not None:
             torch._foreach_copy_([g.ro, g.tx, g.dtx], [rays_o, position_tx, direction_tx])
         else:

@@ -365,9 +365,10 @@ class FusedHeadCore(torch.autograd.Function):
             _lib.call("avr_head_exact_layout", pref, B, K, code, ctypes.byref(ns), ctypes.byref(wbytes))
             n_split = ns.value
             part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
+            queue = torch.empty(256, dtype=torch.int32, device=dev)  # work-queue counters (zeroed by the call)
             Wf = _packed_exact_weight(w_master, W, cache, pref, (p.T, K, code), wbytes.value, st)
             _lib.call("avr_head_fwd_exact", pref, B, K, _ptr(h), _ptr(Wf), code, _ptr(perm), _ptr(ws), _ptr(cnt),
-                      n_split, _ptr(part), st)
+                      _ptr(delay), n_split, _ptr(part), _ptr(queue), st)
         else:
             ns = ctypes.c_int32(0)
             _lib.call("avr_head_splits", pref, B, K, code, ctypes.byref(ns))

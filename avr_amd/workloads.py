@@ -125,6 +125,7 @@ MESHRIR_MODEL = dict(  # config_files/avr_meshrir.yml:44-89
     sigma_encoder_network=_mlp(3, 128), sigma_decoder_network=_mlp(3, 128),
     signal_network=dict(_mlp(3, 512), otype="CutlassMLP"),
 )
+SIMU_MODEL = dict(MESHRIR_MODEL, dir_encoding_sig=_grid(18), signal_output_dim=1600)  # avr_simu.yml model block
 RAF_MODEL = dict(  # config_files/avr_raf_furnished.yml:37-100
     signal_output_dim=1600, leaky_relu=0.03,
     pos_encoding_sigma=_grid(18), pos_encoding_sig=_grid(18), dir_encoding_sig=_grid(18),

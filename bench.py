@@ -120,6 +120,10 @@ def parse_args(argv=None):
     ap.add_argument("--workload", default=None, help="default: the mode's workload")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--network", action="store_true",
+                    help="ray-shard mode: render through the reference network (AVRModel, avr_simu.yml "
+                         "model block, random init, --mlp-dtype MLPs, fused rounding-exact head) instead of "
+                         "the stub's resident outputs")
     ap.add_argument("--no-network", action="store_true",
                     help="pose mode: skip the config-2 inference through the reference network")
     ap.add_argument("--poses", type=int, default=16,
@@ -560,14 +564,24 @@ def bench_ray_shard(args, w, world, rank, dev):
     dt = torch.float16 if w.signal_dtype == "float16" else torch.float32
     r0, r1 = shard_range(R, rank, world)
     Rl = r1 - r0
-    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    attn = (torch.rand(B, Rl * S, 1, device=dev, generator=gen) * 2).to(dt)
-    signal = (torch.randn(B, Rl * S, T, device=dev, generator=gen) * 0.1).to(dt)
+    if args.network:
+        # the reference network of config 5 (avr_simu.yml), the same random
+        # weights on every rank; each rank evaluates it on its own rays only
+        from avr_amd.model import AVRModel
+        from avr_amd.workloads import SIMU_MODEL
+        mlp_dtype = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[args.mlp_dtype]
+        torch.manual_seed(0)
+        net = AVRModel(dict(SIMU_MODEL, signal_output_dim=T), mlp_dtype=mlp_dtype).to(dev)
+    else:
+        gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+        attn = (torch.rand(B, Rl * S, 1, device=dev, generator=gen) * 2).to(dt)
+        signal = (torch.randn(B, Rl * S, T, device=dev, generator=gen) * 0.1).to(dt)
+        net = StubNet(attn, signal)
     # every rank renders the same poses (one pose, its rays split)
     pg = torch.Generator(device=dev).manual_seed(4321)
     P = args.poses
     rays_o, tx, dtx = _poses(w, P, dev, pg)
-    renderer = AVRRender(StubNet(attn, signal), **w.render)
+    renderer = AVRRender(net, **w.render).to(dev)
     timer = KernelTimer(args.steps)
     renderer.kernel_timer = timer
     sharded = RayShardedRender(renderer)
@@ -594,14 +608,19 @@ def bench_ray_shard(args, w, world, rank, dev):
     elapsed, t_issue = timed(lambda: run(args.steps), world, dev)
     value = whole_job_rate(w.ray_samples, 1, args.steps, elapsed)  # one pose per step, all ranks
     res = _base_result(args, w, world, value, elapsed, "f32" if dt == torch.float32 else "f16-storage/f32-math")
-    rf = roofline(w, timer, dt)
+    # with the network the fused head replaces the ray reduction (no events)
+    rf = roofline(w, timer, dt) if not args.network else None
+    if args.network:
+        res["dtype"] = args.mlp_dtype + " MLP / f32 render"
+        res["data"] = "synthetic poses; AVRModel (avr_simu.yml model block), random init, evaluated per ray shard"
     res.update({
         "scaling": "strong",
         "ir_render_ms_per_pose": elapsed * 1e3 / args.steps,
         "host_issue_ms_per_step": t_issue * 1e3 / args.steps,
         "config": {"workload": w.name, "mode": "ray-shard", "rays": R, "rays_per_rank": Rl, "samples": S,
                    "T": T, "freq_bins": w.F, "poses_per_step": B,
-                   "parallelism": f"rays x{world}, one RCCL all-reduce of the [B,F,2] spectrum per pose"},
+                   "parallelism": f"rays x{world}, one RCCL all-reduce of the [B,F,2] spectrum per pose",
+                   "network": "AVRModel (avr_simu.yml)" if args.network else "stub (outputs resident in HBM)"},
         "roofline": rf,
     })
     return res

@@ -432,14 +432,17 @@ int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, const void* h
  * of two <= 16, for avr_dft_phase_fwd) and the size of the packed weight;
  * avr_head_pack_w_exact packs W [T][K] into Wf (MFMA B-fragment order, once
  * per weight update); avr_head_fwd_exact writes zpart [n_split][B][S][T],
- * zero for t >= T-1-shift_s.  perm / ws / cnt from avr_head_sort. */
+ * zero for t >= T-1-shift_s.  perm / ws / cnt from avr_head_sort, delay
+ * [B][R][S] the integer delays avr_head_sort was given; queue: 256 int32 of
+ * device scratch (the kernel's work-queue counters, zeroed on the stream by
+ * the call), not shared with a concurrent call. */
 int avr_head_exact_layout(const avr_render_params* p, int32_t B, int32_t K, int32_t dtype,
                           int32_t* n_split, int64_t* wpack_bytes);
 int avr_head_pack_w_exact(const avr_render_params* p, int32_t K, const void* W, int32_t dtype, void* Wf,
                           void* stream);
 int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* Wf,
                        int32_t dtype, const int32_t* perm, const float* ws, const int32_t* cnt,
-                       int32_t n_split, float* zpart, void* stream);
+                       const int32_t* delay, int32_t n_split, float* zpart, int32_t* queue, void* stream);
 /* Backward: gz [B][S][T] (avr_dft_phase_bwd) -> grad_h [B][R][S][K] (dtype),
  * grad_w [B][R][S] fp32 (to avr_weights_bwd) and grad_W [T][K] fp32.
  * `workspace` holds avr_head_bwd_workspace() bytes of fp32 partials. */

@@ -35,3 +35,5 @@ AVR_LINEAR_SHAPE_PROBE=0 timeout -k 10 200 python tools/probe_phases.py linear >
 grep '^{' $OUT/phases_lin0.log | tail -1
 timeout -k 10 400 python tools/ddp_buckets.py --steps 3 > $OUT/ddp_buckets.log 2>&1 || { tail -20 $OUT/ddp_buckets.log; exit 1; }
 tail -2 $OUT/ddp_buckets.log
+timeout -k 10 200 python tools/lat_probe.py > $OUT/lat_probe.log 2>&1 || { tail -20 $OUT/lat_probe.log; exit 1; }
+tail -1 $OUT/lat_probe.log
