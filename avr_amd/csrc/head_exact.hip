@@ -450,7 +450,7 @@ int exact_ksm(int K) { return K <= 128 ? 8 : (K <= 256 ? 16 : 32); }
 // 256 rays, one workgroup per CU, otherwise.  AVR_EXACT_RAYS_PROBE=256 forces
 // the latter (probe runs).
 int exact_rays(int R, int T) {
-    const char* e = getenv("AVR_EXACT_RAYS_PROBE");
+    const char* e = AVR_PROBE_ENV("AVR_EXACT_RAYS_PROBE");
     if (e && atoi(e) == 256) return 256;
     return (R <= 16 * 128 && T <= 1024) ? 128 : 256;
 }
@@ -463,6 +463,16 @@ int exact_check(const avr_render_params* p, int32_t K, int32_t dtype) {
     AVR_REQUIRE(R >= 1 && R <= 16 * 256 && p->T >= 2 && p->T <= 4096 && p->n_samples >= 1,
                 "avr_head_fwd_exact: shape out of range (<= 4096 rays per shard, T <= 4096)");
     return 0;
+}
+
+// LDS of the launch avr_head_fwd_exact makes for (R, T, K): the W ring, the
+// column's cnt, the item's weights and the wave partials (<= 160 KiB)
+size_t exact_lds(int R, int T, int K) {
+    const int KSM = exact_ksm(K);
+    if (exact_rays(R, T) == 128) return xs_lds_bytes(KSM, T, 4, 128, 2, 1);
+    const char* tte = AVR_PROBE_ENV("AVR_EXACT_TT_PROBE");
+    if (tte && atoi(tte) == 64 && K == 512) return xs_lds_bytes(KSM, T, 8, 256, 2, 2);
+    return xs_lds_bytes(KSM, T, 8, 256, 4, 1);
 }
 
 int exact_splits(int R, int T) {
@@ -499,6 +509,8 @@ extern "C" int avr_head_exact_layout(const avr_render_params* p, int32_t B, int3
                                      int32_t* n_split, int64_t* wpack_bytes) {
     AVR_REQUIRE(B >= 1 && n_split && wpack_bytes, "avr_head_exact_layout: bad args");
     if (int e = exact_check(p, K, dtype)) return e;
+    if (exact_lds(n_rays(*p), p->T, K) > 160 * 1024)
+        return fail(AVR_E_CONFIG, "exact head: LDS image above 160 KiB for this shape");
     *n_split = exact_splits(n_rays(*p), p->T);
     // whole 64-t tile pairs (a 64-t tile reads two consecutive 32-t tiles), zero past T
     *wpack_bytes = (int64_t)((p->T + 63) / 64) * 2 * xs_tile_bytes(exact_ksm(K));
@@ -530,12 +542,14 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
                 "avr_head_fwd_exact: h and Wf must be 16-byte aligned");
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
     AVR_REQUIRE(n_split == exact_splits(R, T), "avr_head_fwd_exact: n_split must be avr_head_exact_layout's");
+    if (exact_lds(R, T, K) > 160 * 1024)
+        return fail(AVR_E_CONFIG, "exact head: LDS image above 160 KiB for this shape");
     const int64_t items = (int64_t)n_split * B * S;
     AVR_REQUIRE(items < (1ll << 31), "avr_head_fwd_exact: too many columns");
     const int KSM = exact_ksm(K);
     hipStream_t st = as_stream(stream);
     const bool small = exact_rays(R, T) == 128;
-    const char* tte = getenv("AVR_EXACT_TT_PROBE");
+    const char* tte = AVR_PROBE_ENV("AVR_EXACT_TT_PROBE");
     const bool tt64 = !small && tte && atoi(tte) == 64;
     auto run = [&](auto e_tag) {
         using E = decltype(e_tag);

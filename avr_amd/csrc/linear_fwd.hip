@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256) void linear_pack_w_kernel(const uint16_t* __re
 // two workgroups per CU (one's prologue under the other's MFMAs); 1 = 256
 // rows, 64-column tiles, one workgroup per CU; 2 = 256 rows, 32-column tiles
 int lin_shape(int N) {
-    const char* e = getenv("AVR_LINEAR_SHAPE_PROBE");
+    const char* e = AVR_PROBE_ENV("AVR_LINEAR_SHAPE_PROBE");
     const int v = e ? atoi(e) : 0;
     if (v == 1 && N % 64 == 0) return 1;
     return v == 2 ? 2 : 0;

@@ -13,6 +13,9 @@
 #pragma once
 
 #ifdef AVR_PHASE_PROBES
+// shape-selection switches of the probe tools (AVR_*_PROBE variables); the
+// shipped library reads no such variable (tests/test_lib_abi.py)
+#define AVR_PROBE_ENV(name) getenv(name)
 #define AVR_PROBE_TU(setter)                                                                  \
     namespace {                                                                              \
     __device__ unsigned long long* avr_probe_buf = nullptr;                                   \
@@ -38,6 +41,7 @@
         }                                                                      \
     } while (0)
 #else
+#define AVR_PROBE_ENV(name) ((const char*)nullptr)
 #define AVR_PROBE_TU(setter)
 #define AVR_PROBE_DECL
 #define AVR_PROBE_MARK(k)

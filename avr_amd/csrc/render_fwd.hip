@@ -241,13 +241,8 @@ template <typename Ta>
 __global__ __launch_bounds__(256) void weights_fwd_kernel(
     avr_render_params p, int B, const Ta* __restrict__ attn, const float* __restrict__ rays_o,
     const float* __restrict__ pos_tx, const float* __restrict__ dirs,
-    const float* __restrict__ d_vals, float* __restrict__ w_out, int32_t* __restrict__ delay,
-    int32_t* __restrict__ zero, int nzero) {
+    const float* __restrict__ d_vals, float* __restrict__ w_out, int32_t* __restrict__ delay) {
     extern __shared__ float lds_alpha[];
-    // the render core's DFT tickets, zeroed here: this launch precedes the DFT
-    // on the stream, so the tickets are zero when the DFT's workgroups count
-    if (zero && blockIdx.x == 0)
-        for (int i = threadIdx.x; i < nzero; i += 256) zero[i] = 0;
     const int R = n_rays(p), S = p.n_samples;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t ray = (int64_t)blockIdx.x * 4 + wave;  // flattened (b, r)
@@ -493,10 +488,9 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
     avr_render_params pp, const float* __restrict__ part, const float* __restrict__ pl,
     const int32_t* __restrict__ shift, const float2* __restrict__ phase,
     const float2* __restrict__ twg, float2* __restrict__ spart, int B, int S, int T, int KS,
-    int kchunk, int xcd_order, int* __restrict__ tickets, float2* __restrict__ out) {
+    int kchunk, int xcd_order) {
     extern __shared__ float2 tw[];           // [T]
     __shared__ float As[32][kKc + 1];
-    __shared__ int last_arriver;
     const int F = T / 2 + 1;
     const int P = ((S + 31) / 32) * KS;
     // XCD-aware order: every workgroup of one s-tile (its k-slices x F-blocks)
@@ -623,75 +617,6 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
     im += __shfl_xor(im, 32, 64);
     if (half == 0 && f < F) {
         spart[((int64_t)b * P + stile * KS + ks) * F + f] = make_float2(re, im);
-    }
-    if (!tickets) return;
-    // ---- finalize in this launch: the workgroup that completes an F-block
-    // (the last of its nst x KS (s-tile, k-slice) workgroups to arrive, by an
-    // agent-scope ticket; the tickets are zeroed by the render core's weights
-    // launch ahead of this one) sums the block's P partials.  Publish: stores
-    // done, barrier, one release fence, ticket; the last arriver acquires and
-    // reads the partials with plain loads.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        int* tk = tickets + (int64_t)b * nfb + fblk;
-        const int old = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int is_last = old == nst * KS - 1;
-        if (is_last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        last_arriver = is_last;
-    }
-    __syncthreads();
-    if (!last_arriver) return;
-    // out[b, f] for the block's 128 bins in spectrum_finalize_kernel's order
-    // (16 groups of partials p = g + 16 u + 64 q, then the groups in order),
-    // so the spectrum is bit-identical to the separate finalize launch.  Two
-    // threads per bin, each summing 8 groups with all their loads in flight;
-    // the upper 8 group sums meet the lower ones through LDS (As is free).
-    const int bin = threadIdx.x & 127, gh = threadIdx.x >> 7;  // groups 8 gh .. 8 gh + 7
-    const int fo = fblk * 128 + bin;
-    const float2* src = spart + (int64_t)b * P * F + min(fo, F - 1);
-    float2 gs[8];
-#pragma unroll
-    for (int g = 0; g < 8; ++g) gs[g] = make_float2(0.f, 0.f);
-    for (int q0 = 0; q0 < P; q0 += 64) {
-        float2 v[8][4];
-#pragma unroll
-        for (int g = 0; g < 8; ++g)
-#pragma unroll
-            for (int u = 0; u < 4; ++u) v[g][u] = src[(int64_t)min(q0 + 8 * gh + g + 16 * u, P - 1) * F];
-#pragma unroll
-        for (int g = 0; g < 8; ++g)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (q0 + 8 * gh + g + 16 * u < P) {
-                    gs[g].x += v[g][u].x;
-                    gs[g].y += v[g][u].y;
-                }
-    }
-    float2* up = reinterpret_cast<float2*>(&As[0][0]);  // [8][128] float2 = 8 KiB <= sizeof(As)
-    static_assert(sizeof(As) >= 8 * 128 * sizeof(float2), "As holds the upper group sums");
-    if (gh == 1)
-#pragma unroll
-        for (int g = 0; g < 8; ++g) up[g * 128 + bin] = gs[g];
-    __syncthreads();
-    if (gh == 0 && fo < F) {
-        float2 r = gs[0];
-#pragma unroll
-        for (int g = 1; g < 8; ++g) {
-            r.x += gs[g].x;
-            r.y += gs[g].y;
-        }
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            r.x += up[g * 128 + bin].x;
-            r.y += up[g * 128 + bin].y;
-        }
-        out[(int64_t)b * F + fo] = r;
     }
 }
 
@@ -1081,10 +1006,10 @@ extern "C" int avr_sample_rays_staged(const avr_render_params* p, int32_t B, con
     return check_launch("avr_sample_rays_staged");
 }
 
-namespace {
-int launch_weights_fwd(const avr_render_params* p, int32_t B, const void* attn, int32_t attn_dtype,
-                       const float* rays_o, const float* pos_tx, const float* dirs, const float* d_vals, float* w,
-                       int32_t* delay, int32_t* zero, int nzero, void* stream) {
+extern "C" int avr_weights_fwd(const avr_render_params* p, int32_t B, const void* attn,
+                               int32_t attn_dtype, const float* rays_o, const float* pos_tx,
+                               const float* dirs, const float* d_vals, float* w, int32_t* delay,
+                               void* stream) {
     if (int e = validate(p)) return e;
     AVR_REQUIRE(B >= 1 && attn && rays_o && pos_tx && dirs && d_vals && w && delay,
                 "avr_weights_fwd: bad args");
@@ -1101,26 +1026,19 @@ int launch_weights_fwd(const avr_render_params* p, int32_t B, const void* attn, 
     }
     if (attn_dtype == AVR_DTYPE_F32)
         hipLaunchKernelGGL(weights_fwd_kernel<float>, grid, dim3(256), lds, as_stream(stream), *p,
-                           (int)B, (const float*)attn, rays_o, pos_tx, dirs, d_vals, w, delay, zero, nzero);
+                           (int)B, (const float*)attn, rays_o, pos_tx, dirs, d_vals, w, delay);
     else if (attn_dtype == AVR_DTYPE_F16)
         hipLaunchKernelGGL(weights_fwd_kernel<__half>, grid, dim3(256), lds, as_stream(stream),
-                           *p, (int)B, (const __half*)attn, rays_o, pos_tx, dirs, d_vals, w, delay, zero, nzero);
+                           *p, (int)B, (const __half*)attn, rays_o, pos_tx, dirs, d_vals, w, delay);
     else if (attn_dtype == AVR_DTYPE_BF16)
         hipLaunchKernelGGL(weights_fwd_kernel<__hip_bfloat16>, grid, dim3(256), lds,
                            as_stream(stream), *p, (int)B, (const __hip_bfloat16*)attn, rays_o,
-                           pos_tx, dirs, d_vals, w, delay, zero, nzero);
+                           pos_tx, dirs, d_vals, w, delay);
     else
         return fail(AVR_E_ARG, "avr_weights_fwd: unknown attn dtype");
     return check_launch("avr_weights_fwd");
 }
-}  // namespace
 
-extern "C" int avr_weights_fwd(const avr_render_params* p, int32_t B, const void* attn,
-                               int32_t attn_dtype, const float* rays_o, const float* pos_tx,
-                               const float* dirs, const float* d_vals, float* w, int32_t* delay,
-                               void* stream) {
-    return launch_weights_fwd(p, B, attn, attn_dtype, rays_o, pos_tx, dirs, d_vals, w, delay, nullptr, 0, stream);
-}
 
 namespace {
 // Streaming variant of the reduction: 4 rows in flight per lane with
@@ -1262,15 +1180,12 @@ extern "C" int avr_ray_reduce_fwd(const avr_render_params* p, int32_t B, const v
     return fail(AVR_E_ARG, "avr_ray_reduce_fwd: unknown signal dtype");
 }
 
-namespace {
-// avr_dft_phase_fwd, optionally with the finalize folded in: with `tickets`
-// (B x ceil(F/128) int32, zero on entry, left zero) the last workgroup of
-// each F-block writes out [B][F][2] as avr_spectrum_finalize would.
-int launch_dft_phase_fwd(const avr_render_params* p, int32_t B, const float* part, int32_t n_split,
-                         const float* pl_table, const int32_t* shift, const float* phase, const float* twiddle,
-                         int32_t k_split, float* spart, int32_t* tickets, float* out, void* stream) {
+extern "C" int avr_dft_phase_fwd(const avr_render_params* p, int32_t B, const float* part,
+                                 int32_t n_split, const float* pl_table, const int32_t* shift,
+                                 const float* phase, const float* twiddle, int32_t k_split,
+                                 float* spart, void* stream) {
     if (int e = validate(p)) return e;
-    AVR_REQUIRE(B >= 1 && part && pl_table && shift && phase && twiddle && spart && (!tickets || out),
+    AVR_REQUIRE(B >= 1 && part && pl_table && shift && phase && twiddle && spart,
                 "avr_dft_phase_fwd: null pointer");
     const int S = p->n_samples, T = p->T, F = T / 2 + 1;
     const int nkc = (T + kKc - 1) / kKc;
@@ -1291,8 +1206,7 @@ int launch_dft_phase_fwd(const avr_render_params* p, int32_t B, const float* par
         hipLaunchKernelGGL(kern, grid, dim3(kDftThreads), lds, as_stream(stream), *p, part, pl_table,
                            shift, reinterpret_cast<const float2*>(phase),
                            reinterpret_cast<const float2*>(twiddle),
-                           reinterpret_cast<float2*>(spart), (int)B, S, T, (int)k_split, kchunk, xcd_order, tickets,
-                           reinterpret_cast<float2*>(out));
+                           reinterpret_cast<float2*>(spart), (int)B, S, T, (int)k_split, kchunk, xcd_order);
     };
     switch (n_split) {
         case 1: go(dft_phase_fwd_kernel<1>); break;
@@ -1303,15 +1217,6 @@ int launch_dft_phase_fwd(const avr_render_params* p, int32_t B, const float* par
         default: return fail(AVR_E_ARG, "avr_dft_phase_fwd: n_split must be 1, 2, 4, 8 or 16");
     }
     return check_launch("avr_dft_phase_fwd");
-}
-}  // namespace
-
-extern "C" int avr_dft_phase_fwd(const avr_render_params* p, int32_t B, const float* part,
-                                 int32_t n_split, const float* pl_table, const int32_t* shift,
-                                 const float* phase, const float* twiddle, int32_t k_split,
-                                 float* spart, void* stream) {
-    return launch_dft_phase_fwd(p, B, part, n_split, pl_table, shift, phase, twiddle, k_split, spart, nullptr,
-                                nullptr, stream);
 }
 
 extern "C" int avr_spectrum_finalize(int32_t B, int32_t P, int32_t F, const float* spart,
@@ -1384,8 +1289,8 @@ extern "C" int avr_irfft_bwd(int32_t B, int32_t F, const float* grad_ir, const f
 // allocation and argument marshalling).
 namespace {
 struct CoreLayout {
-    int64_t w, delay, part, spart, tickets, bytes;
-    int32_t n_split, k_split, P, ntickets;
+    int64_t w, delay, part, spart, bytes;
+    int32_t n_split, k_split, P;
 };
 
 CoreLayout core_layout(const avr_render_params* p, int B, int sig_dtype) {
@@ -1416,9 +1321,6 @@ CoreLayout core_layout(const avr_render_params* p, int B, int sig_dtype) {
     o += al((int64_t)ns * B * S * T * 4);
     L.spart = o;
     o += al((int64_t)B * L.P * F * 8);
-    L.tickets = o;  // the DFT's finalize tickets (inside the spart region of the ABI layout)
-    L.ntickets = (int32_t)(B * ((F + 127) / 128));
-    o += al((int64_t)L.ntickets * 4);
     L.bytes = o;
     return L;
 }
@@ -1455,19 +1357,20 @@ extern "C" int avr_render_core_fwd(const avr_render_params* p, int32_t B, const 
     int32_t* delay = reinterpret_cast<int32_t*>(ws + L.delay);
     float* part = reinterpret_cast<float*>(ws + L.part);
     float* spart = reinterpret_cast<float*>(ws + L.spart);
-    int32_t* tickets = reinterpret_cast<int32_t*>(ws + L.tickets);
-    if (int e = launch_weights_fwd(p, B, attn, attn_dtype, rays_o, pos_tx, dirs, tab->d_vals, w, delay, tickets,
-                                   L.ntickets, stream))
+    if (int e = avr_weights_fwd(p, B, attn, attn_dtype, rays_o, pos_tx, dirs, tab->d_vals, w, delay, stream))
         return e;
     hipStream_t s = as_stream(stream);
     if (ev_begin) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_begin), s);
     if (int e = avr_ray_reduce_fwd(p, B, signal, sig_dtype, w, delay, L.n_split, part, stream))
         return e;
     if (ev_end) (void)hipEventRecord(reinterpret_cast<hipEvent_t>(ev_end), s);
-    // DFT + phase with the finalize folded in (its last workgroup per F-block)
-    if (int e = launch_dft_phase_fwd(p, B, part, L.n_split, tab->pl_table, tab->shift, tab->phase, tab->twiddle,
-                                     L.k_split, spart, tickets, out, stream))
+    // DFT + phase, then the fixed-order sum of its partials.  The finalize
+    // folded into the DFT's last workgroup per F-block (round 4) was slower in
+    // both the serial and the pipelined renders
+    if (int e = avr_dft_phase_fwd(p, B, part, L.n_split, tab->pl_table, tab->shift, tab->phase, tab->twiddle,
+                                  L.k_split, spart, stream))
         return e;
+    if (int e = avr_spectrum_finalize(B, L.P, p->T / 2 + 1, spart, out, stream)) return e;
     if (ir) {
         AVR_REQUIRE(tab->ir_twiddle, "avr_render_core_fwd: ir requested without ir_twiddle");
         return avr_irfft(B, p->T / 2 + 1, out, tab->ir_twiddle, ir, stream);

@@ -7,6 +7,7 @@ model.py uses), HIP-event timing and agreement.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -17,6 +18,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from avr_amd import _lib  # noqa: E402
+
+# the shape switch (AVR_LINEAR_SHAPE_PROBE) is read only by the probe build
+# (`make -C avr_amd/csrc probe`); the shipped library always runs shape 0
+PROBE = ctypes.CDLL(os.path.join(ROOT, "avr_amd", "csrc", "build", "libavr_probe.so"))
 
 
 def main():
@@ -40,10 +45,14 @@ def main():
     y = torch.empty(M, N, dtype=dt, device=dev)
     st = torch.cuda.current_stream(dev).cuda_stream
     wf = torch.empty_like(w)
+    _lib.load()
+    PROBE.avr_linear_relu_fwd.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
+                                          ctypes.c_void_p]
     _lib.call("avr_linear_pack_w", N, K, w.data_ptr(), code, wf.data_ptr(), st)
 
     def ours():
-        _lib.call("avr_linear_relu_fwd", M, N, K, x.data_ptr(), wf.data_ptr(), code, 1, y.data_ptr(), st)
+        assert PROBE.avr_linear_relu_fwd(M, N, K, x.data_ptr(), wf.data_ptr(), code, 1, y.data_ptr(), st) == 0
         return y
 
     def blas():
