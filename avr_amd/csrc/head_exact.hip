@@ -104,7 +104,7 @@ __device__ __forceinline__ void wait_vm(int n) {
     }
 }
 
-// largest T of the 8-wave and the 4-wave items (exact_rays)
+// largest T of the 8-wave and the 4-wave items (exact_shape)
 constexpr int kExactMaxT[2] = {4096, 1024};
 
 // threadIdx.x through an empty asm: in a persistent kernel's item loop, the
@@ -211,6 +211,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
     };
 
     Meta cur, nx;
+    int claim = 0;
     int item = item_of(ql), nxt = item_of(gq + ql);
     load_meta(item, cur);
     load_dly(cur);
@@ -220,16 +221,18 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
         AVR_PROBE_DECL;
         const int tid = opaque_tid();
         const int lane = tid & 63, half = lane >> 5, j = lane & 31;
-        const int64_t col = (int64_t)item % ncol;
-        const int blk = (int)((int64_t)item / ncol);
-        const int s = (int)(col % S), b = (int)(col / S);
+        const int col = item % (int)ncol;  // items < 2^31 (checked by the host)
+        const int blk = item / (int)ncol;
+        const int s = col % S, b = col / S;
         const int lim = tail_limit(pp, s);
         float* zc = zpart + ((int64_t)blk * ncol + col) * T;
         const int p0 = blk * RAYS;
         const int pw = p0 + RPW * wave;
         const int nk = __builtin_amdgcn_readfirstlane(cur.nk);
-        // a claim two items ahead (kept in thread 0's register until this item ends)
-        int claim = 0;
+        // a claim two items ahead (thread 0's register; defined only by the
+        // atomic, so no re-initialisation at the loop top waits for the last
+        // one: a write-after-write behind a returning atomic costs a full
+        // vmcnt(0) there)
         if (tid == 0) {
             // the counter's offset through an empty asm: not provably uniform,
             // so the compiler's wave-aggregating atomic rewrite (which waits for
@@ -238,10 +241,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             asm volatile("" : "+v"(zero));
             claim = __hip_atomic_fetch_add(qctr + zero, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        // the next item's metadata: in flight under this item (older than its DMA)
-        load_meta(nxt, nx);
-        bool dly_issued = false, touched = false;
+        bool dly_issued = false, touched = false, published = false;
         if (p0 >= nk || lim <= 0) {
+            load_meta(nxt, nx);
             for (int t = tid; t < T; t += NT) zc[t] = 0.0f;
             load_dly(nx);
             dly_issued = true;
@@ -249,7 +251,12 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             // ---- prologue: the wave's rows by LDS-DMA through the (idle) ring
             const E* hrow = h + (((int64_t)b * R + cur.ray) * S + s) * K;
             frag8 a[NQ][KSM];
-            if constexpr (dma_rows) {
+            if (AVR_PROBE_SKIP(4)) {
+#pragma unroll
+                for (int ks = 0; ks < KSM; ++ks) a[0][ks] = frag8{(uint32_t)ks, 0u, 0u, 0u};
+#pragma unroll
+                for (int ks = 0; ks < KSM; ++ks) asm volatile("" : "+v"(a[0][ks]));
+            } else if constexpr (dma_rows) {
                 // every fragment defined before the lane-masked round writes:
                 // an undefined start would let the compiler carry the previous
                 // item's fragments into this item's prologue (128 more VGPRs)
@@ -280,13 +287,16 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             }
             if (tid < RAYS) wl[tid] = p0 + tid < nk ? cur.wsv : 0.0f;
             if (lane == 0) dstart[wave] = pw < nk ? cur.dly : 1 << 30;
-            __syncthreads();  // staging area free: the ring may fill; cl, wl, dstart written
+            // staging area free (the ring may fill); cl, wl, dstart written.  A
+            // bare barrier: nothing in flight on the vector-memory counter is
+            // waited for (the claim's atomic)
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_s_barrier();
             AVR_PROBE_MARK(10);
             const int tb = dstart[0] / TT;       // first tile with a live ray of the item
             const int te = (lim + TT - 1) / TT;  // tiles holding t < lim
-            for (int t = tid; t < T; t += NT)
-                if (t < TT * tb || t >= TT * te) zc[t] = 0.0f;
             auto issue = [&](int tau, int slot) {  // W tile tau into ring slot `slot`: this wave's DPW pieces
+                if (AVR_PROBE_SKIP(1)) return;
                 const char* src =
                     reinterpret_cast<const char*>(Wf) + (int64_t)tau * TILE + wave * DPW * 1024 + 16 * lane;
                 const uint32_t dst = ring_lds + slot * TILE + wave * DPW * 1024;
@@ -295,33 +305,55 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             };
             for (int i = 0; i < NB - 1; ++i)
                 if (tb + i < te) issue(tb + i, i);
-            AVR_VMCNT(0);
-            __syncthreads();
+            // the next item's metadata: in flight under this item, younger than
+            // the first tiles, so only the tiles are waited for here
+            load_meta(nxt, nx);
+            AVR_VMCNT(CLN + 3);  // the first tiles and the (older) claim have landed
+            if (tid == 0) {
+                // published now, not at the item's end: no returning atomic is
+                // in flight at the loop's back edge (the compiler would wait for
+                // every store of the item there).  Slot iter & 1 was last read
+                // before this item's first barrier
+                qnext[iter & 1] = item_of(3 * gq + claim);
+                published = true;
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_s_barrier();
             AVR_PROBE_MARK(2);
+#ifdef AVR_PHASE_PROBES
+            probe_w[12] = te - tb;                                   // tiles of the item
+            probe_w[13] = (uint64_t)(dstart[wave] < (1 << 30) ? (lim - dstart[wave] + 31) / 32 : 0);  // wave's live tiles
+            probe_w[14] = blockIdx.x;
+#endif
 
             // the wave's 32 rays against 32-t column group c of the tile in
             // ring slot `slot`: one MFMA chain over K (A from registers, B read
             // from the ring D k-steps ahead), then the epilogue (rounded,
             // masked by value: p < cnt[t], weighted, summed per lane in row order)
             const float* wq = wl + RPW * wave + 4 * half;
-            auto group = [&](int slot, int tau, int c) {
+            // The next W tile's DMA pieces (dtile >= 0) are issued inside the
+            // chain, one every KSM / DPW MFMAs: issued back to back before it,
+            // each stalls the wave ~100 cycles behind the previous one
+            // (tools/probe_phases.py), while between MFMAs the stall overlaps
+            // the matrix pipe.
+            auto group = [&](int slot, int tau, int c, int dtile, int dslot) {
                 const char* bsrc = ring + slot * TILE + c * xs_tile_bytes(KSM) + 16 * lane;
                 constexpr int D = KSM < 8 ? KSM : 8;  // B fragments read ahead
+                constexpr int DSTEP = KSM / DPW;      // MFMAs per DMA piece
                 frag8 bw[D];
 #pragma unroll
                 for (int u = 0; u < D; ++u) bw[u] = *reinterpret_cast<const frag8*>(bsrc + u * 1024);
                 f32x16 acc = f32x16{};
+                const char* dsrc = reinterpret_cast<const char*>(Wf) + (int64_t)dtile * TILE + wave * DPW * 1024 + 16 * lane;
+                const uint32_t ddst = ring_lds + dslot * TILE + wave * DPW * 1024;
 #pragma unroll
                 for (int ks = 0; ks < KSM; ++ks) {
                     acc = mfma16<E>(a[0][ks], bw[ks % D], acc);
                     if (ks + D < KSM) bw[ks % D] = *reinterpret_cast<const frag8*>(bsrc + (ks + D) * 1024);
+                    if (ks % DSTEP == 0 && dtile >= 0 && !AVR_PROBE_SKIP(1))
+                        dma_row16(dsrc + (ks / DSTEP) * 1024, ddst + (ks / DSTEP) * 1024);
                 }
-                __builtin_amdgcn_sched_group_barrier(0x100, D, 0);
-#pragma unroll
-                for (int ks = 0; ks < KSM; ++ks) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    if (ks + D < KSM) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                }
+                if (AVR_PROBE_SKIP(2)) return acc[0] + acc[15];
                 // register r of acc is row (r & 3) + 8 (r >> 2) + 4 half of the
                 // wave's rays, column t = TT tau + 32 c + j
                 const int t0 = TT * tau + 32 * c;
@@ -355,15 +387,24 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             for (int tau = tb; tau < te; ++tau) {
                 const int i = tau - tb;
                 AVR_PROBE_BEGIN(comp);
-                if (tau + NB - 1 < te) issue(tau + NB - 1, (i + NB - 1) % NB);  // the slot tile tau-1 left
+                // tile tau + NB - 1 into the slot tile tau - 1 left: inside the
+                // first live group's chain, else here
+                int dtile = tau + NB - 1 < te ? tau + NB - 1 : -1;
+                const int dslot = (i + NB - 1) % NB;
                 float zl[NC];
 #pragma unroll
                 for (int c = 0; c < NC; ++c) {
                     // group c holds a live ray of the wave from the wave's first
                     // live t on (cnt is nondecreasing in t), nothing at or past lim
                     const int t0 = TT * tau + 32 * c;
-                    zl[c] = (t0 + 31 >= dstart[wave] && t0 < lim) ? group(i % NB, tau, c) : 0.0f;
+                    if (t0 + 31 >= dstart[wave] && t0 < lim) {
+                        zl[c] = group(i % NB, tau, c, dtile, dslot);
+                        dtile = -1;
+                    } else {
+                        zl[c] = 0.0f;
+                    }
                 }
+                if (dtile >= 0) issue(dtile, dslot);
                 AVR_PROBE_END(comp, 6);
                 // lower + upper lane half (rows 4 half + ...), the same association in every lane
 #pragma unroll
@@ -384,9 +425,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                     for (int m = max(0, i + 2 - NB); m < i; ++m) st += (wave == m % WAVES);
                     wait_vm(min(NB - 2, te - 2 - tau) * DPW + st);
                 }
-                if (i == 0) {
-                    // the next item's delay (its ray has landed): older than
-                    // the tiles issued from the next iteration on
+                if (i == min(1, te - 1 - tb)) {
+                    // the next item's delay (its ray has landed by now): older
+                    // than the tiles issued from the next iteration on
                     load_dly(nx);
                     dly_issued = true;
                 }
@@ -408,13 +449,17 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                     if (t < T) zc[t] = v;
                 }
             }
+            // zero outside the item's tiles (after the tiles: no wait above
+            // includes these stores)
+            for (int t = tid; t < T; t += NT)
+                if (t < TT * tb || t >= TT * te) zc[t] = 0.0f;
             // the next item's prologue rewrites the ring and the LDS metadata:
             // every wave has passed the last tile's barrier, after which only
             // the partials zr are read (rewritten after two more barriers)
         }
         if (!dly_issued) load_dly(nx);
         if (!touched) touch(nx);
-        if (tid == 0) qnext[iter & 1] = item_of(3 * gq + claim);
+        if (tid == 0 && !published) qnext[iter & 1] = item_of(3 * gq + claim);
         if (p0 >= nk || lim <= 0) __syncthreads();  // every item has a barrier between the qnext accesses
         AVR_PROBE_FLUSH((int64_t)item * WAVES + wave);
         item = nxt;
@@ -445,14 +490,26 @@ constexpr int kExactQueueInts = 256;  // 8 work-queue counters, one 128-byte lin
 
 int exact_ksm(int K) { return K <= 128 ? 8 : (K <= 256 ? 16 : 32); }
 
-// Work-item shape: 128 rays and two workgroups per CU where the DFT's slab
-// count allows (<= 2048 rays) and two ~70 KB LDS images fit (T <= 1024);
-// 256 rays, one workgroup per CU, otherwise.  AVR_EXACT_RAYS_PROBE=256 forces
-// the latter (probe runs).
-int exact_rays(int R, int T) {
-    const char* e = AVR_PROBE_ENV("AVR_EXACT_RAYS_PROBE");
-    if (e && atoi(e) == 256) return 256;
-    return (R <= 16 * 128 && T <= 1024) ? 128 : 256;
+// Work-item shape.  K = 512 (the reference networks' width, rows by
+// LDS-DMA): 256 rays, one workgroup of eight waves per CU, 64-t tiles (two
+// MFMA chains per wave between barriers), 239 vs 248 us for the 128-ray form
+// per config-2 fp16 render (tools/ab_shapes.py, round 4).  Otherwise 128
+// rays and two workgroups per CU where the DFT's slab count allows (<= 2048
+// rays) and two ~70 KB LDS images fit (T <= 1024); 256 rays with 32-t tiles
+// beyond.  AVR_EXACT_RAYS_PROBE / AVR_EXACT_TT_PROBE override it in the probe
+// builds (csrc/probe.h).
+struct ExactShape {
+    int rays;
+    bool tt64;
+};
+
+ExactShape exact_shape(int R, int T, int K) {
+    ExactShape sh{(R <= 16 * 128 && T <= 1024) ? 128 : 256, false};
+    if (K == 512) sh = {256, true};
+    if (const char* e = AVR_PROBE_ENV("AVR_EXACT_RAYS_PROBE")) sh.rays = atoi(e) == 256 ? 256 : 128;
+    if (const char* e = AVR_PROBE_ENV("AVR_EXACT_TT_PROBE")) sh.tt64 = atoi(e) == 64;
+    if (sh.rays == 128 || K != 512) sh.tt64 = false;
+    return sh;
 }
 
 int exact_check(const avr_render_params* p, int32_t K, int32_t dtype) {
@@ -469,14 +526,14 @@ int exact_check(const avr_render_params* p, int32_t K, int32_t dtype) {
 // column's cnt, the item's weights and the wave partials (<= 160 KiB)
 size_t exact_lds(int R, int T, int K) {
     const int KSM = exact_ksm(K);
-    if (exact_rays(R, T) == 128) return xs_lds_bytes(KSM, T, 4, 128, 2, 1);
-    const char* tte = AVR_PROBE_ENV("AVR_EXACT_TT_PROBE");
-    if (tte && atoi(tte) == 64 && K == 512) return xs_lds_bytes(KSM, T, 8, 256, 2, 2);
+    const ExactShape sh = exact_shape(R, T, K);
+    if (sh.rays == 128) return xs_lds_bytes(KSM, T, 4, 128, 2, 1);
+    if (sh.tt64) return xs_lds_bytes(KSM, T, 8, 256, 2, 2);
     return xs_lds_bytes(KSM, T, 8, 256, 4, 1);
 }
 
-int exact_splits(int R, int T) {
-    const int rays = exact_rays(R, T);
+int exact_splits(int R, int T, int K) {
+    const int rays = exact_shape(R, T, K).rays;
     const int nb = (R + rays - 1) / rays;
     int n = 1;
     while (n < nb) n *= 2;
@@ -511,7 +568,7 @@ extern "C" int avr_head_exact_layout(const avr_render_params* p, int32_t B, int3
     if (int e = exact_check(p, K, dtype)) return e;
     if (exact_lds(n_rays(*p), p->T, K) > 160 * 1024)
         return fail(AVR_E_CONFIG, "exact head: LDS image above 160 KiB for this shape");
-    *n_split = exact_splits(n_rays(*p), p->T);
+    *n_split = exact_splits(n_rays(*p), p->T, K);
     // whole 64-t tile pairs (a 64-t tile reads two consecutive 32-t tiles), zero past T
     *wpack_bytes = (int64_t)((p->T + 63) / 64) * 2 * xs_tile_bytes(exact_ksm(K));
     return 0;
@@ -541,16 +598,15 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
     AVR_REQUIRE(reinterpret_cast<uintptr_t>(h) % 16 == 0 && reinterpret_cast<uintptr_t>(Wf) % 16 == 0,
                 "avr_head_fwd_exact: h and Wf must be 16-byte aligned");
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
-    AVR_REQUIRE(n_split == exact_splits(R, T), "avr_head_fwd_exact: n_split must be avr_head_exact_layout's");
+    AVR_REQUIRE(n_split == exact_splits(R, T, K), "avr_head_fwd_exact: n_split must be avr_head_exact_layout's");
     if (exact_lds(R, T, K) > 160 * 1024)
         return fail(AVR_E_CONFIG, "exact head: LDS image above 160 KiB for this shape");
     const int64_t items = (int64_t)n_split * B * S;
     AVR_REQUIRE(items < (1ll << 31), "avr_head_fwd_exact: too many columns");
     const int KSM = exact_ksm(K);
     hipStream_t st = as_stream(stream);
-    const bool small = exact_rays(R, T) == 128;
-    const char* tte = AVR_PROBE_ENV("AVR_EXACT_TT_PROBE");
-    const bool tt64 = !small && tte && atoi(tte) == 64;
+    const ExactShape shape = exact_shape(R, T, K);
+    const bool small = shape.rays == 128, tt64 = shape.tt64;
     auto run = [&](auto e_tag) {
         using E = decltype(e_tag);
         auto go = [&](auto kern, int ksm, int waves, int rays, int nb, int nc, const void* hv) {

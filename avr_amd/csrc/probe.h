@@ -12,17 +12,30 @@
 //   [8..15] s_memtime marks the kernel names (AVR_PROBE_MARK(8..15))
 #pragma once
 
-#ifdef AVR_PHASE_PROBES
-// shape-selection switches of the probe tools (AVR_*_PROBE variables); the
+// shape-selection switches of the probe tools (AVR_*_PROBE variables), read
+// only by the probe and shape-probe builds (`make probe`, `make shapes`); the
 // shipped library reads no such variable (tests/test_lib_abi.py)
+#if defined(AVR_PHASE_PROBES) || defined(AVR_SHAPE_PROBES)
 #define AVR_PROBE_ENV(name) getenv(name)
+#else
+#define AVR_PROBE_ENV(name) ((const char*)nullptr)
+#endif
+
+#ifdef AVR_PHASE_PROBES
 #define AVR_PROBE_TU(setter)                                                                  \
     namespace {                                                                              \
     __device__ unsigned long long* avr_probe_buf = nullptr;                                   \
+    __device__ int avr_probe_skip = 0;                                                        \
     }                                                                                        \
     extern "C" int setter(void* p) {                                                         \
         return hipMemcpyToSymbol(HIP_SYMBOL(avr_probe_buf), &p, sizeof(p)) == hipSuccess ? 0 : 1; \
+    }                                                                                        \
+    extern "C" int setter##_skip(int v) {                                                    \
+        return hipMemcpyToSymbol(HIP_SYMBOL(avr_probe_skip), &v, sizeof(v)) == hipSuccess ? 0 : 1; \
     }
+// phase-skip experiments (results WRONG; probe build only): a kernel skips
+// the phases whose bits the tool sets, to price them
+#define AVR_PROBE_SKIP(bit) (avr_probe_skip & (bit))
 #define AVR_PROBE_DECL                                                  \
     unsigned long long probe_w[16] = {};                                \
     probe_w[0] = __builtin_amdgcn_s_memrealtime();                      \
@@ -41,7 +54,7 @@
         }                                                                      \
     } while (0)
 #else
-#define AVR_PROBE_ENV(name) ((const char*)nullptr)
+#define AVR_PROBE_SKIP(bit) false
 #define AVR_PROBE_TU(setter)
 #define AVR_PROBE_DECL
 #define AVR_PROBE_MARK(k)

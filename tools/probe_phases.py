@@ -56,8 +56,17 @@ def summarize(buf, what):
     print(json.dumps(res), flush=True)
 
 
+def dump_items(buf, path):
+    """Raw per-(item, wave) records of the exact head for offline analysis."""
+    w = buf.view(-1, 16).cpu().numpy()
+    np.save(path, w[w[:, 1] > 0])
+
+
 def main():
     what = sys.argv[1] if len(sys.argv) > 1 else "exact"
+    # phase-skip bitmasks to run (probe build only; results wrong): 1 = no W
+    # DMA, 2 = no epilogue, 4 = no row loads (csrc/head_exact.hip)
+    skips = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0]
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(19)
     buf = torch.zeros(1 << 22, dtype=torch.int64, device=dev)
@@ -90,11 +99,16 @@ def main():
             _lib.call = call
             import avr_amd.renderer as rr
             rr._lib.call = call
-            for _ in range(3):
-                buf.zero_()
-                r.render_from_hidden(attn, h, W, torch.float16, geom)
-                torch.cuda.synchronize()
-                summarize(buf, "exact_head")
+            for sk in skips:
+                assert PROBE.avr_probe_set_exact_skip(sk) == 0
+                for _ in range(2):
+                    buf.zero_()
+                    r.render_from_hidden(attn, h, W, torch.float16, geom)
+                    torch.cuda.synchronize()
+                    summarize(buf, f"exact_head skip={sk}")
+                    if os.environ.get("AVR_PROBE_DUMP"):
+                        dump_items(buf, os.path.join(os.environ["AVR_PROBE_DUMP"], f"exact_skip{sk}.npy"))
+            assert PROBE.avr_probe_set_exact_skip(0) == 0
     else:
         assert PROBE.avr_probe_set_linear(ctypes.c_void_p(buf.data_ptr())) == 0
         M, N, K = 262144, 512, 512
