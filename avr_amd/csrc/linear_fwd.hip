@@ -127,7 +127,15 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(2, 2
 
     for (int tau = 0; tau < nt; ++tau) {
         AVR_PROBE_BEGIN(comp);
-        if (tau + NB - 1 < nt) issue(tau + NB - 1, (tau + NB - 1) % NB);  // the slot tile tau-1 left
+        // W tile tau + NB - 1 into the slot tile tau - 1 left, its DMA pieces
+        // issued inside the MFMA chain (one every DSTEP k-steps): issued back
+        // to back each stalls the wave behind the previous one, between MFMAs
+        // the stall overlaps the matrix pipe (csrc/head_exact.hip, round 4)
+        const bool dnext = tau + NB - 1 < nt;
+        const char* dsrc =
+            reinterpret_cast<const char*>(Wf) + (int64_t)(tau + NB - 1) * TILEB + wave * DPW * 1024 + 16 * lane;
+        const uint32_t ddst = ring_lds + ((tau + NB - 1) % NB) * TILEB + wave * DPW * 1024;
+        constexpr int DSTEP = kLKS / DPW;
         const char* bsrc = lds_l + (tau % NB) * TILEB + 16 * lane;
         constexpr int D = 8 / NC;  // k-steps of B fragments read ahead
         frag8 bw[D][NC];
@@ -145,15 +153,7 @@ __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(2, 2
                 acc[c] = lmfma<E>(bw[ks % D][c], a[ks], acc[c]);
                 if (ks + D < kLKS) bw[ks % D][c] = *reinterpret_cast<const frag8*>(bsrc + c * kLTile + (ks + D) * 1024);
             }
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, D * NC, 0);
-#pragma unroll
-        for (int ks = 0; ks < kLKS; ++ks) {
-#pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                if (ks + D < kLKS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            }
+            if (ks % DSTEP == 0 && dnext) ldma16(dsrc + (ks / DSTEP) * 1024, ddst + (ks / DSTEP) * 1024);
         }
         // epilogue: register r of acc[c] is column CT tau + 32 c + (r & 3) +
         // 8 (r >> 2) + 4 half of row rl.  Group pair (2p, 2p + 1) = columns

@@ -163,6 +163,39 @@ def _linear_relu_hip(x, w, w_master=None, cache=False):
     return y
 
 
+# hipBLASLt's solution for the width-512 layers at config-2 inference, picked
+# by PyTorch TunableOp over every hipBLASLt / rocBLAS candidate on MI355X
+# (tools/tune_gemms.sh; bit-identical output, 0.12 vs 0.16-0.21 ms per layer).
+# The file holds only these shapes; every other GEMM keeps the default
+# heuristic.  Not used when the process set up TunableOp itself, off with
+# AVR_TUNABLEOP=0.
+_TUNED_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_gfx950.csv")
+_TUNED = [False]
+
+
+def _enable_tuned_gemms(device):
+    """Load the shipped TunableOp results once, read-only (no tuning, nothing
+    recorded); the file's validators (library versions, gfx950) make
+    TunableOp ignore it anywhere else."""
+    if _TUNED[0]:
+        return
+    _TUNED[0] = True
+    if os.environ.get("AVR_TUNABLEOP", "1") == "0" or not os.path.exists(_TUNED_FILE):
+        return
+    import tempfile
+
+    import torch.cuda.tunable as tun
+
+    if tun.is_enabled() or "gfx950" not in torch.cuda.get_device_properties(device).gcnArchName:
+        return
+    tun.tuning_enable(False)
+    tun.record_untuned_enable(False)
+    # results written at exit go to a scratch file, never over the shipped one
+    tun.set_filename(os.path.join(tempfile.gettempdir(), f"avr_tunableop_{os.getpid()}.csv"))
+    tun.enable(True)
+    tun.read_file(_TUNED_FILE)
+
+
 class _LinearReLU(torch.autograd.Function):
     """y = relu(x W^T) with the ReLU in the GEMM epilogue: hipBLASLt's
     `_addmm_activation` with a zero bias (one kernel instead of GEMM + an
@@ -178,6 +211,7 @@ class _LinearReLU(torch.autograd.Function):
         y = _linear_relu_hip(x, w, w_master, cache) if x.is_cuda else None
         if y is None:
             if x.is_cuda:
+                _enable_tuned_gemms(x.device)
                 y = torch._addmm_activation(_zero_bias(w.size(0), dtype, x.device), x, w.t(),
                                             use_gelu=False)
             else:

@@ -384,7 +384,7 @@ def network_inference(w, dev, steps=20, warmup=3):
     ms = (time.perf_counter() - t0) * 1e3 / steps
     return {
         "network": "AVRModel (avr_meshrir.yml model block, random init), fp16 MLPs (tcnn precision)",
-        "path": "level-major hash grids + fused sigma networks + hipBLASLt 512x512 layers + fused signal head "
+        "path": "level-major hash grids + fused sigma networks + hipBLASLt 512x512 layers (TunableOp-selected solution, avr_amd/tunableop_gfx950.csv) + fused signal head "
                 "+ render + irfft",
         "ms_per_pose": ms,
         "ray_samples_per_s": w.ray_samples / (ms * 1e-3),

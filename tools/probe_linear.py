@@ -19,9 +19,10 @@ sys.path.insert(0, ROOT)
 
 from avr_amd import _lib  # noqa: E402
 
-# the shape switch (AVR_LINEAR_SHAPE_PROBE) is read only by the probe build
-# (`make -C avr_amd/csrc probe`); the shipped library always runs shape 0
-PROBE = ctypes.CDLL(os.path.join(ROOT, "avr_amd", "csrc", "build", "libavr_probe.so"))
+# the shape switch (AVR_LINEAR_SHAPE_PROBE) is read only by the shape-probe
+# build (`make -C avr_amd/csrc shapes`, no phase clocks); the shipped library
+# always runs shape 0
+PROBE = ctypes.CDLL(os.path.join(ROOT, "avr_amd", "csrc", "build", "libavr_shapes.so"))
 
 
 def main():
