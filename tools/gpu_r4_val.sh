@@ -26,7 +26,7 @@ for i in 1 2; do
 done
 step prof 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-network --no-cpu-baseline
 step prof1 400 rocprofv3 --kernel-trace --stats -d $OUT/prof1 -o run --output-format csv -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-network --no-cpu-baseline --streams 1
-tail -1 $OUT/prof1.log > $OUT/prof1.json
+grep "^{" $OUT/prof1.log | tail -1 > $OUT/prof1.json
 step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --no-network --steps 20 --warmup 3 --streams 1
 step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --no-network --steps 20 --warmup 3 --streams 1
 step profinfer 400 rocprofv3 --kernel-trace --stats -d $OUT/profinfer -o run --output-format csv -- python tools/bench_infer.py --mlp-dtype fp16 --variants fused --steps 10 --warmup 3
