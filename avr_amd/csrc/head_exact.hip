@@ -132,7 +132,7 @@ template <typename E, int KSM, int WAVES, int RAYS, int NB, int NC, bool ROWDMA>
 __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
     avr_render_params pp, int B, int R, int K, const E* __restrict__ h, const frag8* __restrict__ Wf,
     const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
-    const int32_t* __restrict__ delay, float* __restrict__ zpart, int* __restrict__ queue, int nitems) {
+    const int32_t* __restrict__ delay, float* __restrict__ zpart, int* __restrict__ queue, int nitems, int prio) {
     constexpr int NT = 64 * WAVES, TILE = NC * xs_tile_bytes(KSM);  // a tile: TT = 32 NC values of t
     constexpr int TT = 32 * NC;
     constexpr int RPW = RAYS / WAVES;    // rays per wave
@@ -152,6 +152,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
 
     const int64_t ncol = (int64_t)B * S;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // static priority for the second-dispatched half of the waves (the
+    // arbitration loser of every segment; MI355X_MICROARCH.md, two waves per SIMD)
+    if (prio && wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
     const int ksn = K / 16;
     constexpr bool dma_rows = ROWDMA;  // K == 512: whole 1 KiB rows by LDS-DMA
     const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
@@ -607,6 +610,11 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
     hipStream_t st = as_stream(stream);
     const ExactShape shape = exact_shape(R, T, K);
     const bool small = shape.rays == 128, tt64 = shape.tt64;
+    // s_setprio 1 for waves 4-7 of the 8-wave items: 234.0 vs 239.8 us per
+    // config-2 fp16 fused render (tools/ab_shapes.py, 5 interleaved rounds);
+    // the 4-wave items (two workgroups per CU) lose with it (252 vs 244)
+    int prio = small ? 0 : 1;
+    if (const char* pe = AVR_PROBE_ENV("AVR_EXACT_PRIO_PROBE")) prio = atoi(pe);
     auto run = [&](auto e_tag) {
         using E = decltype(e_tag);
         auto go = [&](auto kern, int ksm, int waves, int rays, int nb, int nc, const void* hv) {
@@ -622,7 +630,7 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
             const int grid = 8 * (int)std::max<int64_t>(gq, 1);
             (void)hipMemsetAsync(queue, 0, kExactQueueInts * sizeof(int32_t), st);
             hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), lds, st, *p, (int)B, R, (int)K, (const E*)hv,
-                               (const frag8*)Wf, perm, ws, cnt, delay, zpart, (int*)queue, (int)items);
+                               (const frag8*)Wf, perm, ws, cnt, delay, zpart, (int*)queue, (int)items, prio);
         };
         const bool rowdma = K == 512;
         if (small) {

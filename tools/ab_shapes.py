@@ -21,6 +21,13 @@ from avr_amd.workloads import WORKLOADS  # noqa: E402
 
 
 def set_shape(sh):
+    # "256/64p": static priority for the second half of the waves, "256/64n":
+    # none (AVR_EXACT_PRIO_PROBE; the library's default is on for 8-wave items)
+    if sh[-1] in "pn":
+        os.environ["AVR_EXACT_PRIO_PROBE"] = "1" if sh[-1] == "p" else "0"
+        sh = sh[:-1]
+    else:
+        os.environ.pop("AVR_EXACT_PRIO_PROBE", None)
     rays, _, tt = sh.partition("/")
     os.environ["AVR_EXACT_RAYS_PROBE"] = rays
     os.environ["AVR_EXACT_TT_PROBE"] = tt or "32"
