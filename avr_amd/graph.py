@@ -79,6 +79,7 @@ class GraphedRender:
         self.warmup = warmup
         self.ring = max(1, int(ring))
         self._graphs = {}  # key -> [instances], next index
+        self._dev_cache = {}  # current device index -> torch.device
 
     def _capture(self, dev, rays_o, position_tx, direction_tx, warmup):
         r = self.renderer
@@ -131,7 +132,12 @@ class GraphedRender:
         replayed; the tensors are the instance's static outputs.  Host
         (CPU) pose tensors take the staged path, device ones one copy."""
         r = self.renderer
-        dev = r._device(rays_o)
+        # the device without r._device's availability check and torch.device
+        # construction on every call (~1 us of the serial pose); a host pose
+        # renders on the current device, as the eager path does
+        dev = rays_o.device if rays_o.is_cuda else self._dev_cache.get(torch.cuda.current_device())
+        if dev is None:
+            dev = self._dev_cache.setdefault(torch.cuda.current_device(), r._device(rays_o))
         key = (int(position_tx.size(0)), direction_tx is None, rays_o.is_cuda, dev,
                tuple(p.data_ptr() for p in r.parameters()))
         slot = self._graphs.get(key)
@@ -164,7 +170,9 @@ class GraphedRender:
         else:
             torch._foreach_copy_([g.ro, g.tx], [rays_o, position_tx])
         if g.exec is not None:
-            _lib.call("avr_graph_launch", g.exec, torch._C._cuda_getCurrentRawStream(dev.index))
+            lib = _lib.load()
+            if lib.avr_graph_launch(g.exec, torch._C._cuda_getCurrentRawStream(dev.index)) != 0:
+                raise RuntimeError(f"avr_graph_launch failed: {lib.avr_last_error().decode(errors='replace')}")
         else:
             g.graph.replay()
         g.done = g.done or torch.cuda.Event()
