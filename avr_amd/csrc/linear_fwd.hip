@@ -42,10 +42,7 @@ typedef uint32_t frag8 __attribute__((ext_vector_type(4)));
 
 constexpr int kLK = 512;             // K
 constexpr int kLKS = kLK / 16;       // k-steps
-constexpr int kLRows = 256;          // rows of x per work item
-constexpr int kLRing = 4;            // W tiles in the LDS ring (3 in flight)
 constexpr int kLTile = kLKS * 1024;  // one 32-column W tile in fragment order
-constexpr size_t kLLds = (size_t)kLRing * kLTile;
 
 template <typename E>
 __device__ __forceinline__ f32x16 lmfma(frag8 a, frag8 b, f32x16 c) {

@@ -683,6 +683,13 @@ extern "C" int avr_sigma_fwd(const avr_sigma_desc* d, const void* wpack, void* b
     const bool two = d->variant == AVR_SIGMA_RAF;
     AVR_REQUIRE(src_ok(d->input[0]) && (!two || src_ok(d->input[1])), "avr_sigma_fwd: bad input source");
     AVR_REQUIRE(d->n_extra >= 0 && d->n_extra <= AVR_SIGMA_MAX_EXTRA, "avr_sigma_fwd: bad n_extra");
+#if defined(AVR_PHASE_PROBES) || defined(AVR_SHAPE_PROBES)
+    AVR_REQUIRE(d->tile_cfg >= 0 && d->tile_cfg <= 20, "avr_sigma_fwd: bad tile_cfg");
+#else
+    // 0..8 are tilings with correct results; the timing experiments (16..20)
+    // exist only in the probe builds
+    AVR_REQUIRE(d->tile_cfg >= 0 && d->tile_cfg <= 8, "avr_sigma_fwd: bad tile_cfg");
+#endif
     const int out_w = two ? 256 : (d->variant == AVR_SIGMA_MESHRIR_H1 ? 512 : 128);
     AVR_REQUIRE(ldb % 8 == 0 && reinterpret_cast<uintptr_t>(base) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(wpack) % 16 == 0,
@@ -730,8 +737,9 @@ int dispatch(const avr_sigma_desc* d, Args& a, bool h1, bool two, hipStream_t st
         if (d->tile_cfg == 6) return launch_meshrir_h1<E, 1, 4, 2, 32>(a, st);  // LDS-DMA weight staging
         if (d->tile_cfg == 7) return launch_meshrir_h1<E, 1, 4, 2, 96>(a, st);  // + h1 DMAs after the epilogue
         if (d->tile_cfg == 5) return launch_meshrir_h1<E, 2, 4, 2>(a, st);
-        // timing experiments (results are garbage): no barrier / no weight
-        // staging / no h1 stores (bf16 builds only)
+#if defined(AVR_PHASE_PROBES) || defined(AVR_SHAPE_PROBES)
+        // timing experiments (results are garbage; probe builds only): no
+        // barrier / no weight staging / no h1 stores (bf16 only)
         if constexpr (std::is_same<E, __bf16>::value) {
             if (d->tile_cfg == 16) return launch_meshrir_h1<E, 1, 4, 2, 1>(a, st);
             if (d->tile_cfg == 17) return launch_meshrir_h1<E, 1, 4, 2, 2>(a, st);
@@ -739,6 +747,7 @@ int dispatch(const avr_sigma_desc* d, Args& a, bool h1, bool two, hipStream_t st
             if (d->tile_cfg == 19) return launch_meshrir_h1<E, 1, 4, 2, 7>(a, st);
             if (d->tile_cfg == 20) return launch_meshrir_h1<E, 1, 4, 2, 8>(a, st);  // no bias loads
         }
+#endif
         if (d->tile_cfg == 8) return launch_meshrir_h1<E, 1, 4, 2>(a, st);  // register-staged weights
         return launch_meshrir_h1<E, 1, 4, 2, 96>(a, st);  // LDS-DMA staging, h1 DMAs after the epilogue
     }
@@ -751,13 +760,15 @@ int dispatch(const avr_sigma_desc* d, Args& a, bool h1, bool two, hipStream_t st
     if (cfg == 1) return launch_meshrir<E, 1, 8, 1>(a, st);
     if (cfg == 2) return launch_meshrir<E, 1, 4, 2>(a, st);
     if (cfg == 3) return launch_meshrir<E, 2, 4, 1>(a, st);
-    if constexpr (std::is_same<E, __bf16>::value) {
+#if defined(AVR_PHASE_PROBES) || defined(AVR_SHAPE_PROBES)
+    if constexpr (std::is_same<E, __bf16>::value) {  // timing experiments, garbage results
         if (cfg == 16) return launch_meshrir<E, 1, 8, 1, 1>(a, st);
         if (cfg == 17) return launch_meshrir<E, 1, 8, 1, 2>(a, st);
         if (cfg == 18) return launch_meshrir<E, 1, 8, 1, 3>(a, st);
         if (cfg == 19) return launch_meshrir<E, 1, 8, 1, 4>(a, st);
         if (cfg == 20) return launch_meshrir<E, 1, 8, 1, 7>(a, st);
     }
+#endif
     return launch_meshrir<E, 2, 4, 2>(a, st);
 }
 }  // namespace

@@ -352,7 +352,7 @@ typedef struct {
 
 typedef struct {
     int32_t variant;  /* AVR_SIGMA_* */
-    int32_t tile_cfg; /* 0 = default tiling (tuning knob) */
+    int32_t tile_cfg; /* 0 = default tiling (tuning knob, 0..8; anything else is AVR_E_ARG) */
     int64_t n_samples;
     float leaky_slope;
     avr_feat_src input[2];

@@ -192,3 +192,17 @@ def test_network_fused_h1_matches_per_layer(monkeypatch, dtype):
     torch.cuda.synchronize()
     _close(a1, a0, "attn")
     _close(h1, h0, "signal hidden")
+
+
+@pytest.mark.gpu
+def test_sigma_timing_experiments_not_in_shipped_library():
+    """tile_cfg 16..20 (garbage-result timing experiments) exist only in the
+    probe builds; the shipped library rejects them instead of computing."""
+    N, S = 256, 64
+    ws = _weights(sigma.MESHRIR_H1, 5)
+    inputs, _ = _sources(sigma.MESHRIR, N, S, N, 6)
+    bias = torch.zeros(N // S, 512, device=DEV)
+    packed = sigma.pack_layers(sigma.MESHRIR_H1, ws, torch.bfloat16)
+    for cfg in (16, 20, 9, -1):
+        with pytest.raises(RuntimeError, match="tile_cfg"):
+            sigma.sigma_fwd(sigma.MESHRIR_H1, packed, N, inputs, [], 512, 0.01, tile_cfg=cfg, bias=bias, bias_div=S)

@@ -14,7 +14,12 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from avr_amd import sigma  # noqa: E402
+from avr_amd import _lib, sigma  # noqa: E402
+
+# tile configs >= 16 (timing experiments, garbage results) exist only in the
+# shapes build: make -C avr_amd/csrc shapes
+_lib.LIB_PATH = os.environ.get("AVR_AB_LIB") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "avr_amd", "csrc", "build", "libavr_shapes.so")
 
 
 def main():
