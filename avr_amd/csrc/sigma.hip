@@ -38,6 +38,7 @@
 // carried as raw dwords; E only decides the conversions and the MFMA
 // (v_mfma_f32_32x32x16_bf16 / _f16).
 #include "common.h"
+#include "probe.h"
 
 using namespace avr;
 
@@ -730,6 +731,7 @@ int dispatch(const avr_sigma_desc* d, Args& a, bool h1, bool two, hipStream_t st
         // 0: 4 waves, streaming h1 stores (120 us at config 2); 1: 8 waves;
         // 2, 3: the same with plain stores (130 us)
         a.nt_store = d->tile_cfg < 2;
+        if (const char* f = AVR_PROBE_ENV("AVR_SIGMA_NT_PROBE")) a.nt_store = f[0] == '1';  // shapes build only
         if (d->tile_cfg == 1 || d->tile_cfg == 3) return launch_meshrir_h1<E, 1, 8, 1>(a, st);
         // 4, 5: 64 samples per wave (each weight fragment feeds two MFMAs),
         // 1 or 2 waves per SIMD (experiments)
