@@ -119,7 +119,6 @@ _SIGS = {
     "avr_spectrum_finalize": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _vp, _vp, _vp]),
     "avr_irfft": (ctypes.c_int, [_c_i32, _c_i32, _vp, _vp, _vp, _vp]),
     "avr_irfft_bwd": (ctypes.c_int, [_c_i32, _c_i32, _vp, _vp, _vp, _vp]),
-    "avr_spectrum_ir": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _vp, _vp, _vp, _vp, _vp]),
     "avr_dft_phase_bwd": (ctypes.c_int, [_vp, _c_i32] + [_vp] * 7),
     "avr_ray_reduce_bwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32] + [_vp] * 6),
     "avr_weights_bwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32, _vp, _vp, _vp, _vp]),

@@ -721,108 +721,6 @@ __global__ __launch_bounds__(256) void irfft_kernel(int F, int B1, const float2*
     }
 }
 
-// finalize + irfft in one launch (the IR render's tail: one boundary less
-// per pose).  Every block first forms the whole spectrum X[f] = sum_p
-// spart[b][p][f] in exactly spectrum_finalize_kernel's order (16 groups of
-// partials p = g + 16u + 64q, then the 16 group sums added in group order),
-// so `out` is bit-identical to avr_spectrum_finalize's; block 0 writes it.
-// The 16 x F group sums sit in LDS (F <= kSpecIrMaxF).  Then the block's 32
-// IR samples are formed as irfft_kernel does, with 32 bin slices instead of
-// 8 (1024 threads; the slices are added in slice order).
-constexpr int kSpecIrThreads = 1024;
-constexpr int kSpecIrMaxF = 1025;  // 16 x F float2 group sums + X + twiddles in LDS
-
-__global__ __launch_bounds__(kSpecIrThreads) void spectrum_ir_kernel(int B, int P, int F,
-                                                                     const float2* __restrict__ spart,
-                                                                     const float2* __restrict__ twg,
-                                                                     float2* __restrict__ out,
-                                                                     float* __restrict__ ir) {
-    extern __shared__ float2 lds_si[];
-    const int n = 2 * (F - 1);
-    float2* grp = lds_si;             // [16][F]
-    float2* X = lds_si + 16 * F;      // [F]
-    float2* tw = X + F;               // [n]
-    __shared__ float red[32][33];
-    const int b = blockIdx.y;
-    const int g = threadIdx.x >> 6, jl = threadIdx.x & 63;
-    const float2* src = spart + (int64_t)b * P * F;
-    // group sums: this thread's bins f = jl + 64 m, partials p = g + 16 u + 64 q
-    for (int f0 = 0; f0 < F; f0 += 64 * 4) {
-        float2 acc[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) acc[m] = make_float2(0.f, 0.f);
-        for (int q0 = 0; q0 < P; q0 += 64) {
-            float2 v[4][4];
-#pragma unroll
-            for (int m = 0; m < 4; ++m) {
-                const int f = min(f0 + 64 * m + jl, F - 1);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) v[m][u] = src[(int64_t)min(q0 + g + 16 * u, P - 1) * F + f];
-            }
-#pragma unroll
-            for (int m = 0; m < 4; ++m)
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-                    if (q0 + g + 16 * u < P) {
-                        acc[m].x += v[m][u].x;
-                        acc[m].y += v[m][u].y;
-                    }
-        }
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const int f = f0 + 64 * m + jl;
-            if (f < F) grp[g * F + f] = acc[m];
-        }
-    }
-    stage_table<kSpecIrThreads>(tw, twg, n);
-    __syncthreads();
-    for (int f = threadIdx.x; f < F; f += kSpecIrThreads) {
-        float2 r = grp[f];
-        for (int k = 1; k < 16; ++k) {
-            r.x += grp[k * F + f].x;
-            r.y += grp[k * F + f].y;
-        }
-        X[f] = r;
-        if (blockIdx.x == 0) out[(int64_t)b * F + f] = r;
-    }
-    __syncthreads();
-    // irfft of X: 32 IR samples x 32 bin slices
-    const int tl = threadIdx.x & 31, slice = threadIdx.x >> 5;
-    const int t = blockIdx.x * 32 + tl;
-    const int tm = (t < n) ? t : 0;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    int idx[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) idx[c] = (int)(((int64_t)(1 + slice + 32 * c) * tm) % n);
-    const int step4 = (int)((128LL * tm) % n);
-    int k = 1 + slice;
-    for (; k + 96 < F - 1; k += 128) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const float2 w = tw[idx[c]];
-            const float2 x = X[k + 32 * c];
-            acc[c] += x.x * w.x - x.y * w.y;
-            idx[c] += step4;
-            if (idx[c] >= n) idx[c] -= n;
-        }
-    }
-    for (; k < F - 1; k += 32) {
-        const int id = (int)(((int64_t)k * tm) % n);
-        const float2 w = tw[id];
-        const float2 x = X[k];
-        acc[0] += x.x * w.x - x.y * w.y;
-    }
-    red[slice][tl] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    __syncthreads();
-    if (slice == 0 && t < n) {
-        float sum = 0.0f;
-#pragma unroll
-        for (int q = 0; q < 32; ++q) sum += red[q][tl];
-        const float nyq = (t & 1) ? -X[F - 1].x : X[F - 1].x;
-        ir[(int64_t)b * n + t] = ((X[0].x + nyq) + 2.0f * sum) / (float)n;
-    }
-}
-
 // Adjoint irfft (torch's c2r backward): for bin k with weight c_k (1 at DC
 // and Nyquist, 2 inside),
 //   grad[k] = c_k / n * ( sum_t g[t] cos(2 pi k t/n), -sum_t g[t] sin(2 pi k t/n) )
@@ -1247,24 +1145,6 @@ int launch_irfft(int B, int F, const float* spec, const float* spec2, const floa
 extern "C" int avr_irfft(int32_t B, int32_t F, const float* spec, const float* tw, float* ir,
                          void* stream) {
     return avr::launch_irfft(B, F, spec, nullptr, tw, ir, nullptr, stream);
-}
-
-extern "C" int avr_spectrum_ir(int32_t B, int32_t P, int32_t F, const float* spart, const float* tw, float* out,
-                               float* ir, void* stream) {
-    AVR_REQUIRE(B >= 1 && P >= 1 && F >= 2 && spart && tw && out && ir, "avr_spectrum_ir: bad args");
-    if (F > kSpecIrMaxF) {  // long IRs: the two launches
-        if (int e = avr_spectrum_finalize(B, P, F, spart, out, stream)) return e;
-        return avr_irfft(B, F, out, tw, ir, stream);
-    }
-    const int n = 2 * (F - 1);
-    const size_t lds = (size_t)(17 * F + n) * sizeof(float2);
-    if (lds > 65536)
-        (void)hipFuncSetAttribute((const void*)spectrum_ir_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-    hipLaunchKernelGGL(spectrum_ir_kernel, dim3((unsigned)((n + 31) / 32), (unsigned)B), dim3(kSpecIrThreads), lds,
-                       as_stream(stream), (int)B, (int)P, (int)F, reinterpret_cast<const float2*>(spart),
-                       reinterpret_cast<const float2*>(tw), reinterpret_cast<float2*>(out), ir);
-    return check_launch("avr_spectrum_ir");
 }
 
 extern "C" int avr_irfft_bwd(int32_t B, int32_t F, const float* grad_ir, const float* tw,

@@ -160,11 +160,17 @@ class GraphedRender:
             poses = (rays_o, position_tx, direction_tx) if g.has_dtx else (rays_o, position_tx)
             nb = 12 * B
             for k, t in enumerate(poses):
-                if t.dtype is torch.float32 and t.is_contiguous():
+                if (t.dtype is torch.float32 and t.device.type == "cpu" and t.numel() == 3 * B
+                        and t.is_contiguous()):
                     # one memmove into the pinned buffer: no dispatcher call
                     ctypes.memmove(g.buf._h + k * nb, t.data_ptr(), nb)
                 else:
-                    g.pose_np[3 * B * k:3 * B * (k + 1)] = t.detach().reshape(-1).float().numpy()
+                    # another dtype or layout, or a device tensor beside host
+                    # rays_o (the eager path accepts mixed devices)
+                    v = t.detach().reshape(-1).float().cpu()
+                    if v.numel() != 3 * B:
+                        raise ValueError(f"GraphedRender: pose tensor {tuple(t.shape)} is not [{B}, 3]")
+                    g.pose_np[3 * B * k:3 * B * (k + 1)] = v.numpy()
         elif g.dtx is not None:
             torch._foreach_copy_([g.ro, g.tx, g.dtx], [rays_o, position_tx, direction_tx])
         else:

@@ -166,34 +166,85 @@ def _linear_relu_hip(x, w, w_master=None, cache=False):
 # hipBLASLt's solution for the width-512 layers at config-2 inference, picked
 # by PyTorch TunableOp over every hipBLASLt / rocBLAS candidate on MI355X
 # (tools/tune_gemms.sh; bit-identical output, 0.12 vs 0.16-0.21 ms per layer).
-# The file holds only these shapes; every other GEMM keeps the default
-# heuristic.  Not used when the process set up TunableOp itself, off with
-# AVR_TUNABLEOP=0.
+# TunableOp is process-global state, so it is switched on only for the
+# duration of one of the file's own GEMM shapes (`_tuned_window`) and left as
+# the caller had it afterwards: every other GEMM of the process keeps the
+# default heuristic, nothing is tuned or recorded, and no results file is
+# written at exit (TunableOp writes one only while it is enabled).  Not used
+# when the process runs TunableOp itself, off with AVR_TUNABLEOP=0.
 _TUNED_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_gfx950.csv")
-_TUNED = [False]
+_TUNED = [None]  # None: not loaded yet; then True (entries loaded) or False
+
+
+def _tuned_shapes(path=_TUNED_FILE):
+    """(torch dtype, M, N, K) of the `_addmm_activation` entries in the file:
+    `GemmAndBiasTunableOp_<dtype>_TN,tn_<N>_<M>_<K>_...` for y[M,N] = x[M,K] W^T."""
+    names = {"Half": torch.float16, "BFloat16": torch.bfloat16}
+    out = set()
+    if not os.path.exists(path):
+        return out
+    for line in open(path):
+        f = line.strip().split(",")
+        if len(f) < 3 or not f[0].startswith("GemmAndBiasTunableOp_") or not f[1].startswith("tn_"):
+            continue
+        dt = names.get(f[0][len("GemmAndBiasTunableOp_"):].rsplit("_", 1)[0])
+        n, m, k = (int(v) for v in f[1].split("_")[1:4])
+        if dt is not None:
+            out.add((dt, m, n, k))
+    return out
+
+
+_TUNED_SHAPES = _tuned_shapes()
+
+
+class _tuned_window:
+    """TunableOp on (tuning and untuned-recording off) inside the block; the
+    caller's enable / tuning / recording state restored on exit, whatever
+    the block raised.  The results file name is never touched."""
+
+    def __enter__(self):
+        import torch.cuda.tunable as tun
+
+        self.prev = (tun.is_enabled(), tun.tuning_is_enabled(), tun.record_untuned_is_enabled())
+        tun.tuning_enable(False)
+        tun.record_untuned_enable(False)
+        tun.enable(True)
+        return self
+
+    def __exit__(self, *exc):
+        import torch.cuda.tunable as tun
+
+        tun.enable(self.prev[0])
+        tun.tuning_enable(self.prev[1])
+        tun.record_untuned_enable(self.prev[2])
+        return False
 
 
 def _enable_tuned_gemms(device):
-    """Load the shipped TunableOp results once, read-only (no tuning, nothing
-    recorded); the file's validators (library versions, gfx950) make
-    TunableOp ignore it anywhere else."""
-    if _TUNED[0]:
-        return
-    _TUNED[0] = True
-    if os.environ.get("AVR_TUNABLEOP", "1") == "0" or not os.path.exists(_TUNED_FILE):
-        return
-    import tempfile
-
+    """Load the shipped TunableOp results once, read-only; True when they
+    loaded (the file's validators — library versions, gfx950 — make
+    TunableOp reject it anywhere else, and then it is not used)."""
+    if _TUNED[0] is not None:
+        return _TUNED[0]
+    _TUNED[0] = False
+    if os.environ.get("AVR_TUNABLEOP", "1") == "0" or not _TUNED_SHAPES:
+        return False
     import torch.cuda.tunable as tun
 
     if tun.is_enabled() or "gfx950" not in torch.cuda.get_device_properties(device).gcnArchName:
-        return
-    tun.tuning_enable(False)
-    tun.record_untuned_enable(False)
-    # results written at exit go to a scratch file, never over the shipped one
-    tun.set_filename(os.path.join(tempfile.gettempdir(), f"avr_tunableop_{os.getpid()}.csv"))
-    tun.enable(True)
-    tun.read_file(_TUNED_FILE)
+        return False
+    with _tuned_window():
+        ok = bool(tun.read_file(_TUNED_FILE))
+        loaded = {r[1] for r in tun.get_results()} if ok else set()
+    _TUNED[0] = ok and any(f"tn_{n}_{m}_{k}_" in s for _, m, n, k in _TUNED_SHAPES for s in loaded)
+    return _TUNED[0]
+
+
+def _tuned_gemm(x, w):
+    """True when relu(x W^T) is one of the shipped tuned shapes and the
+    results loaded: the caller then runs the GEMM inside `_tuned_window`."""
+    return ((x.dtype, x.size(0), w.size(0), x.size(1)) in _TUNED_SHAPES and x.is_cuda
+            and _enable_tuned_gemms(x.device))
 
 
 class _LinearReLU(torch.autograd.Function):
@@ -211,9 +262,12 @@ class _LinearReLU(torch.autograd.Function):
         y = _linear_relu_hip(x, w, w_master, cache) if x.is_cuda else None
         if y is None:
             if x.is_cuda:
-                _enable_tuned_gemms(x.device)
-                y = torch._addmm_activation(_zero_bias(w.size(0), dtype, x.device), x, w.t(),
-                                            use_gelu=False)
+                bias = _zero_bias(w.size(0), dtype, x.device)
+                if _tuned_gemm(x, w):
+                    with _tuned_window():
+                        y = torch._addmm_activation(bias, x, w.t(), use_gelu=False)
+                else:
+                    y = torch._addmm_activation(bias, x, w.t(), use_gelu=False)
             else:
                 y = torch.relu(x @ w.t())
         ctx.save_for_backward(x, w, y)

@@ -350,6 +350,36 @@ def cpu_baseline(w, budget_s=15.0, mode="pose"):
     }
 
 
+def cpu_leg_threads():
+    """Host threads for the CPU leg: the process's own setting, raised to the
+    box's per-GPU CPU share (16) when a launcher left it at 1 (torchrun sets
+    OMP_NUM_THREADS=1 when the environment has none); AVR_CPU_THREADS
+    overrides."""
+    want = int(os.environ.get("AVR_CPU_THREADS", "0"))
+    return want if want > 0 else max(torch.get_num_threads(), min(16, os.cpu_count() or 1))
+
+
+def attach_cpu_baseline(result, args, w, world, rank):
+    """The CPU leg in the same run at every world size (BASELINE.json
+    north_star: renderer_cpu.py timed beside the 1/2/4/8-GPU numbers): rank 0
+    times the oracle after the timed region and the other ranks wait for it
+    at a barrier, so no rank's GPU work overlaps it."""
+    if rank == 0 and not args.no_cpu_baseline:
+        prev = torch.get_num_threads()
+        torch.set_num_threads(cpu_leg_threads())
+        try:
+            result["cpu_baseline"] = cpu_baseline(w, args.cpu_budget, args.mode)
+        finally:
+            torch.set_num_threads(prev)
+        if world > 1:
+            result["cpu_baseline"]["note"] = (f"timed on rank 0's host after the {world}-rank timed region, "
+                                              "the other ranks idle at a barrier")
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
 def network_inference(w, dev, steps=20, warmup=3):
     """Config-2 inference through the reference's own network, not the stub:
     AVRModel with the avr_meshrir.yml `model:` block (random init), MLPs in
@@ -710,8 +740,7 @@ def main(argv=None):
     result = fn(args, w, world, rank, dev)
     if args.oversubscribe:
         result["oversubscribed"] = f"{world} ranks on cuda:0 over gloo (launcher rehearsal, not a scaling number)"
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(w, args.cpu_budget, args.mode)
+    attach_cpu_baseline(result, args, w, world, rank)
     if rank == 0 and world == 1 and args.mode == "pose" and w.name.startswith("c2_meshrir") \
             and not args.no_network:
         result["network_inference"] = network_inference(w, dev)

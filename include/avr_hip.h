@@ -184,13 +184,6 @@ int avr_spectrum_finalize(int32_t B, int32_t P, int32_t F, const float* spart, f
  * spec[B][F][2] -> ir[B][n], n = 2*(F-1), tw = avr_ir_twiddle(n). */
 int avr_irfft(int32_t B, int32_t F, const float* spec, const float* tw, float* ir,
               void* stream);
-/* avr_spectrum_finalize + avr_irfft in one launch (the render_ir tail):
- * out [B][F] complex (bit-identical to avr_spectrum_finalize's) and
- * ir [B][2(F-1)] from the DFT partials spart [B][P][F] and the irfft
- * twiddles tw (avr_ir_twiddle).  F > 1025 runs the two kernels. */
-int avr_spectrum_ir(int32_t B, int32_t P, int32_t F, const float* spart, const float* tw, float* out,
-                    float* ir, void* stream);
-
 /* Adjoint of avr_irfft (torch's irfft backward: 1/n, the interior bins
  * doubled, zero imaginary gradient at DC and Nyquist):
  * grad_ir[B][n] -> grad_spec[B][F][2].  Differentiates the IR the loss is

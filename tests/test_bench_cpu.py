@@ -119,3 +119,47 @@ def test_cpu_baseline_modes_on_a_small_workload():
         assert d["value"] > 0 and d["unit"] == "ray-samples/s" and d["kind"] == "port"
     shard = bench.cpu_baseline(WORKLOADS["c1_meshrir_plumbing"].replace(n_azi=48, n_ele=5), 0.05, "ray-shard")
     assert "32 rays (6x5+2)" in shard["sample"]
+
+
+def _cpu_leg_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from avr_amd.workloads import WORKLOADS
+
+        res = {}
+        for mode in ("pose", "ray-shard", "ddp-train"):
+            args = bench.parse_args(["--mode", mode, "--workload", "c1_meshrir_plumbing", "--cpu-budget", "0.05"])
+            r = {}
+            bench.attach_cpu_baseline(r, args, WORKLOADS[args.workload], world, rank)
+            res[mode] = r
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cpu_baseline_in_the_two_rank_line_gloo():
+    """World size 2: rank 0's result carries the CPU leg (cores stated) in
+    every mode, the other rank's does not, and both pass the barrier."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cpu_leg_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for mode in ("pose", "ray-shard", "ddp-train"):
+        cb = out[0][mode]["cpu_baseline"]
+        assert cb["value"] > 0 and cb["cores"] >= 1 and "rank 0" in cb["note"]
+        assert "cpu_baseline" not in out[1][mode]
+
+
+def test_cpu_leg_threads(monkeypatch):
+    monkeypatch.setenv("AVR_CPU_THREADS", "3")
+    assert bench.cpu_leg_threads() == 3
+    monkeypatch.delenv("AVR_CPU_THREADS")
+    assert bench.cpu_leg_threads() >= torch.get_num_threads()

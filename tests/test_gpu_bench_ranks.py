@@ -21,13 +21,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _bench(*args, timeout=400):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--oversubscribe",
-           "--steps", "3", "--warmup", "1", "--no-cpu-baseline", *args]
+           "--steps", "3", "--warmup", "1", "--cpu-budget", "0.2", *args]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, (p.returncode, p.stdout[-3000:], p.stderr[-3000:])
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-3000:]  # rank 0 only
-    return json.loads(lines[0])
+    d = json.loads(lines[0])
+    # the CPU leg is in the N-rank line too (north_star: "in the same run")
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["unit"] == "ray-samples/s" and "rank 0" in cb["note"]
+    return d
 
 
 def test_bench_two_ranks_ray_shard():

@@ -90,6 +90,37 @@ def test_graph_ring_pipelined_replays():
     assert not all(torch.equal(got[0], x) for x in got[1:])  # the jitter did change
 
 
+def test_graph_host_pose_mixed_devices_and_bad_shapes():
+    """Host rays_o with a DEVICE position_tx (or a float64 / strided one)
+    is staged by value, not by a host memmove from its pointer, and renders
+    as the eager path does; a pose of the wrong size raises instead of
+    reading past the tensor."""
+    w = WORKLOADS["c1_meshrir_plumbing"]
+    B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
+    g = torch.Generator(device=DEV).manual_seed(5)
+    attn = torch.rand(B, R * S, 1, device=DEV, generator=g) * 2
+    sig = torch.randn(B, R * S, T, device=DEV, generator=g) * 0.1
+    r = AVRRender(Stub(attn, sig), **w.render)
+    gr = GraphedRender(r, ring=1)
+    ro = torch.full((B, 3), 0.25)
+    txs = [torch.full((B, 3), -0.4, device=DEV),                  # device tensor beside host rays_o
+           torch.full((B, 3), 0.6, dtype=torch.float64),          # another dtype
+           torch.full((3, B), 0.2).t()]                           # non-contiguous
+    for k, tx in enumerate(txs):
+        with torch.no_grad():
+            torch.manual_seed(70 + k)
+            _, ir_g = gr.render_ir(ro, tx)
+            ir_g = ir_g.clone()
+            torch.manual_seed(70 + k)
+            _, ir_e = r.render_ir(ro.to(DEV), tx.to(DEV, torch.float32))
+        torch.cuda.synchronize()
+        assert torch.equal(ir_g, ir_e), k
+    with pytest.raises(ValueError):
+        gr.render_ir(ro, torch.zeros(B + 1, 3, device=DEV))
+    with pytest.raises(ValueError):
+        gr.render_ir(ro, torch.zeros(B, 2))
+
+
 @pytest.mark.parametrize("mlp_dtype", [torch.bfloat16, torch.float32])
 def test_graph_replay_sees_optimizer_step_avrmodel(mlp_dtype):
     """The package's own network captured (cast/packed-weight caches bypassed

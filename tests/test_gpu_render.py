@@ -437,30 +437,3 @@ def test_render_ir_differentiable():
     ir2 = torch.fft.irfft(out2[..., 0] + 1j * out2[..., 1], dim=-1)
     (ir2 * probe).sum().backward()
     assert rel_l2(gs.cpu(), sig.grad.cpu()) < 1e-4 and rel_l2(ga.cpu(), attn.grad.cpu()) < 1e-4
-
-
-@pytest.mark.parametrize("F,P,B", [(2, 1, 1), (65, 7, 2), (512, 56, 1), (801, 24, 3), (1025, 40, 1), (2048, 16, 1)])
-def test_spectrum_ir_matches_finalize_then_irfft(F, P, B):
-    """avr_spectrum_ir (finalize + irfft in one launch, the render_ir tail):
-    the spectrum bit-identical to avr_spectrum_finalize, the IR equal to
-    avr_irfft of it up to fp32 summation order (32 bin slices instead of 8);
-    F > 1025 runs the two kernels."""
-    from avr_amd import _lib
-    from avr_amd.renderer import _ir_twiddle
-
-    n = 2 * (F - 1)
-    g = torch.Generator(device=DEV).manual_seed(F)
-    spart = torch.randn(B, P, F, 2, device=DEV, generator=g)
-    tw = _ir_twiddle(n, DEV)
-    st = torch.cuda.current_stream(DEV).cuda_stream
-    out_a = torch.empty(B, F, 2, device=DEV)
-    ir_a = torch.empty(B, n, device=DEV)
-    _lib.call("avr_spectrum_finalize", B, P, F, spart.data_ptr(), out_a.data_ptr(), st)
-    _lib.call("avr_irfft", B, F, out_a.data_ptr(), tw.data_ptr(), ir_a.data_ptr(), st)
-    out_b = torch.empty_like(out_a)
-    ir_b = torch.empty_like(ir_a)
-    _lib.call("avr_spectrum_ir", B, P, F, spart.data_ptr(), tw.data_ptr(), out_b.data_ptr(), ir_b.data_ptr(), st)
-    torch.cuda.synchronize()
-    assert torch.equal(out_a, out_b)
-    scale = float(ir_a.abs().max())
-    assert float((ir_a - ir_b).abs().max()) <= 2e-6 * scale
