@@ -118,9 +118,20 @@ __device__ __forceinline__ int opaque_tid() {
 
 // bytes of one 32-t W tile in fragment order: KSM k-steps x 64 lanes x 16 B
 __host__ __device__ constexpr int xs_tile_bytes(int KSM) { return KSM * 1024; }
+// Stagger (MI355X_MICROARCH.md, two waves per SIMD, item 9): waves
+// WAVES/2 .. WAVES-1 defer the epilogue of each tile's last chain past the
+// tile's barrier, into the next tile, so that on every SIMD one wave's
+// epilogue VALU runs beside its partner's MFMA chain instead of both waves
+// rounding at once with the matrix pipe idle.  A tile's wave partials are then
+// complete one barrier later: three partial buffers instead of two.
+#ifndef AVR_EXACT_STAGGER
+#define AVR_EXACT_STAGGER 0
+#endif
+constexpr int kPartBufs = AVR_EXACT_STAGGER ? 3 : 2;
+
 __host__ __device__ constexpr size_t xs_lds_bytes(int KSM, int T, int waves, int rays, int nb, int nc) {
     return (size_t)nb * nc * xs_tile_bytes(KSM) + 4 * (size_t)((T + 3) / 4 * 4) + 4 * (size_t)rays +
-           4 * (size_t)(2 * waves * 32 * nc) + 4 * (size_t)waves + 8;
+           4 * (size_t)(kPartBufs * waves * 32 * nc) + 4 * (size_t)waves + 8;
 }
 
 // One work item: RAYS consecutive sorted rays of one column (b, s), WAVES
@@ -146,8 +157,8 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
     char* ring = lds_x;                                         // [NB][TILE]
     int* cl = reinterpret_cast<int*>(lds_x + NB * TILE);        // cnt of the column [Tp]
     float* wl = reinterpret_cast<float*>(cl + Tp);              // weights of the item's rays [RAYS]
-    float* zr = wl + RAYS;                                      // wave partials [2][WAVES][TT]
-    int* dstart = reinterpret_cast<int*>(zr + 2 * WAVES * TT);  // first live t per wave [WAVES]
+    float* zr = wl + RAYS;                                      // wave partials [kPartBufs][WAVES][TT]
+    int* dstart = reinterpret_cast<int*>(zr + kPartBufs * WAVES * TT);  // first live t per wave [WAVES]
     int* qnext = dstart + WAVES;                                // claimed items [2]
 
     const int64_t ncol = (int64_t)B * S;
@@ -339,7 +350,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             // each stalls the wave ~100 cycles behind the previous one
             // (tools/probe_phases.py), while between MFMAs the stall overlaps
             // the matrix pipe.
-            auto group = [&](int slot, int tau, int c, int dtile, int dslot) {
+            auto chain = [&](int slot, int c, int dtile, int dslot) {
                 const char* bsrc = ring + slot * TILE + c * xs_tile_bytes(KSM) + 16 * lane;
                 constexpr int D = KSM < 8 ? KSM : 8;  // B fragments read ahead
                 constexpr int DSTEP = KSM / DPW;      // MFMAs per DMA piece
@@ -356,6 +367,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                     if (ks % DSTEP == 0 && dtile >= 0 && !AVR_PROBE_SKIP(1))
                         dma_row16(dsrc + (ks / DSTEP) * 1024, ddst + (ks / DSTEP) * 1024);
                 }
+                return acc;
+            };
+            auto epi = [&](const f32x16& acc, int tau, int c) {
                 if (AVR_PROBE_SKIP(2)) return acc[0] + acc[15];
                 // register r of acc is row (r & 3) + 8 (r >> 2) + 4 half of the
                 // wave's rays, column t = TT tau + 32 c + j
@@ -387,9 +401,46 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                 }
                 return z;
             };
+            // a chain's per-lane sum, lower + upper lane half (rows 4 half +
+            // ...; the same association in every lane), into the partials of
+            // buffer `buf`
+            auto put = [&](float zlc, int buf, int c) {
+                const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zlc), __float_as_uint(zlc), false,
+                                                                false);
+                const float v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+                if (half == 0) zr[buf * (WAVES * TT) + wave * TT + 32 * c + j] = v;
+            };
+            // the wave partials of tile tau (buffer `buf`), in wave order
+            auto sum_tile = [&](int tau, int buf) {
+                if (lane < TT) {
+                    const float* zz = zr + buf * (WAVES * TT) + lane;
+                    float v = zz[0];
+#pragma unroll
+                    for (int w = 1; w < WAVES; ++w) v += zz[TT * w];
+                    const int t = TT * tau + lane;
+                    if (t < T) zc[t] = v;
+                }
+            };
+            // the wave that sums (and stores) a tile's partials right after the
+            // barrier of iteration m: tile m by wave m % WAVES, or with the
+            // stagger tile m - 1 by one of the non-deferring waves
+            auto summer = [&](int m) {
+                if constexpr (AVR_EXACT_STAGGER) return m >= 1 ? (m - 1) % (WAVES / 2) : -1;
+                else return m % WAVES;
+            };
+            constexpr bool kStag = AVR_EXACT_STAGGER;
+            const bool defer = kStag && wave >= WAVES / 2;
+            f32x16 dacc = f32x16{};
+            bool dlive = false;  // a deferred last chain is pending
             for (int tau = tb; tau < te; ++tau) {
                 const int i = tau - tb;
                 AVR_PROBE_BEGIN(comp);
+                if (kStag && defer) {
+                    // the previous tile's last chain: its epilogue now, beside
+                    // the partner wave's first chain of this tile
+                    if (i >= 1) put(dlive ? epi(dacc, tau - 1, NC - 1) : 0.0f, (i - 1) % kPartBufs, NC - 1);
+                    dlive = false;
+                }
                 // tile tau + NB - 1 into the slot tile tau - 1 left: inside the
                 // first live group's chain, else here
                 int dtile = tau + NB - 1 < te ? tau + NB - 1 : -1;
@@ -400,32 +451,32 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                     // group c holds a live ray of the wave from the wave's first
                     // live t on (cnt is nondecreasing in t), nothing at or past lim
                     const int t0 = TT * tau + 32 * c;
+                    zl[c] = 0.0f;
                     if (t0 + 31 >= dstart[wave] && t0 < lim) {
-                        zl[c] = group(i % NB, tau, c, dtile, dslot);
+                        const f32x16 acc = chain(i % NB, c, dtile, dslot);
                         dtile = -1;
-                    } else {
-                        zl[c] = 0.0f;
+                        if (kStag && defer && c == NC - 1) {
+                            dacc = acc;
+                            dlive = true;
+                        } else {
+                            zl[c] = epi(acc, tau, c);
+                        }
                     }
                 }
                 if (dtile >= 0) issue(dtile, dslot);
                 AVR_PROBE_END(comp, 6);
-                // lower + upper lane half (rows 4 half + ...), the same association in every lane
 #pragma unroll
-                for (int c = 0; c < NC; ++c) {
-                    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zl[c]), __float_as_uint(zl[c]),
-                                                                    false, false);
-                    const float v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-                    if (half == 0) zr[(i & 1) * (WAVES * TT) + wave * TT + 32 * c + j] = v;
-                }
+                for (int c = 0; c < NC; ++c)
+                    if (!(kStag && defer && c == NC - 1)) put(zl[c], i % kPartBufs, c);
                 AVR_PROBE_BEGIN(dma);
                 if (tau + 1 < te) {
                     // this wave's pieces of tile tau+1 have landed.  Younger in
                     // vmcnt: the ring's later tiles and this wave's partial
                     // stores since tile tau+1 was issued (a wave stores after
-                    // the barrier of iteration m when wave == m % WAVES), so no
+                    // the barrier of iteration m when wave == summer(m)), so no
                     // store in flight is waited for
                     int st = 0;
-                    for (int m = max(0, i + 2 - NB); m < i; ++m) st += (wave == m % WAVES);
+                    for (int m = max(0, i + 2 - NB); m < i; ++m) st += (wave == summer(m));
                     wait_vm(min(NB - 2, te - 2 - tau) * DPW + st);
                 }
                 if (i == min(1, te - 1 - tb)) {
@@ -443,14 +494,18 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                 __builtin_amdgcn_s_waitcnt(0xC07F);  // every LDS access of tile tau (and the partials) done
                 __builtin_amdgcn_s_barrier();
                 AVR_PROBE_END(bar, 5);
-                if (wave == (i % WAVES) && lane < TT) {  // the wave partials of tile tau, in wave order
-                    const float* zz = zr + (i & 1) * (WAVES * TT) + lane;
-                    float v = zz[0];
-#pragma unroll
-                    for (int w = 1; w < WAVES; ++w) v += zz[TT * w];
-                    const int t = TT * tau + lane;
-                    if (t < T) zc[t] = v;
+                if (wave == summer(i)) {
+                    if constexpr (kStag) sum_tile(tau - 1, (i - 1) % kPartBufs);
+                    else sum_tile(tau, i % kPartBufs);
                 }
+            }
+            if constexpr (kStag) {
+                // the last tile: its deferred chains, one more barrier, its sum
+                const int n = te - tb;
+                if (defer) put(dlive ? epi(dacc, te - 1, NC - 1) : 0.0f, (n - 1) % kPartBufs, NC - 1);
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_s_barrier();
+                if (wave == (n - 1) % (WAVES / 2)) sum_tile(te - 1, (n - 1) % kPartBufs);
             }
             // zero outside the item's tiles (after the tiles: no wait above
             // includes these stores)

@@ -1,6 +1,6 @@
 // Phase probes for timing experiments (tools/probe_phases.py).  Compiled
 // in only with -DAVR_PHASE_PROBES, which `make probe` sets for a separate
-// library (csrc/build/libavr_probe.so) that the tools load; the shipped
+// library (tools/_lib/libavr_probe.so) that the tools load; the shipped
 // libavr_hip.so has none of this.  A probed kernel records per wave, in a
 // buffer the tool hands over, sixteen 64-bit words:
 //   [0] s_memrealtime at the start (100 MHz, chip-wide)

@@ -199,13 +199,16 @@ _TUNED_SHAPES = _tuned_shapes()
 
 class _tuned_window:
     """TunableOp on (tuning and untuned-recording off) inside the block; the
-    caller's enable / tuning / recording state restored on exit, whatever
-    the block raised.  The results file name is never touched."""
+    caller's enable / tuning / recording state and results file name
+    restored on exit, whatever the block raised.  (TunableOp's first use
+    initialises its results manager, which sets the default file name; that
+    is put back too, so a process that never used TunableOp sees '' still.)"""
 
     def __enter__(self):
         import torch.cuda.tunable as tun
 
-        self.prev = (tun.is_enabled(), tun.tuning_is_enabled(), tun.record_untuned_is_enabled())
+        self.prev = (tun.is_enabled(), tun.tuning_is_enabled(), tun.record_untuned_is_enabled(),
+                     tun.get_filename())
         tun.tuning_enable(False)
         tun.record_untuned_enable(False)
         tun.enable(True)
@@ -217,6 +220,8 @@ class _tuned_window:
         tun.enable(self.prev[0])
         tun.tuning_enable(self.prev[1])
         tun.record_untuned_enable(self.prev[2])
+        if tun.get_filename() != self.prev[3]:
+            tun.set_filename(self.prev[3])
         return False
 
 

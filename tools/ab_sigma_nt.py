@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from avr_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.environ.get("AVR_AB_LIB") or os.path.join(ROOT, "avr_amd", "csrc", "build", "libavr_shapes.so")
+_lib.LIB_PATH = os.environ.get("AVR_AB_LIB") or os.path.join(ROOT, "tools", "_lib", "libavr_shapes.so")
 from avr_amd import sigma  # noqa: E402
 from avr_amd.model import _enable_tuned_gemms  # noqa: E402
 

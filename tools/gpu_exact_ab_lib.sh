@@ -10,7 +10,7 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 rc=$?; tail -1 $OUT/tests.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" $OUT/tests.log | head -30; exit $rc; }
 for i in 1 2 3; do
   for v in new old; do
-    lib=avr_amd/csrc/build/libavr_shapes.so; [ $v = old ] && lib=avr_amd/csrc/build/libavr_shapes_old.so
+    lib=tools/_lib/libavr_shapes.so; [ $v = old ] && lib=tools/_lib/libavr_shapes_old.so
     AVR_AB_LIB=$PWD/$lib timeout -k 10 200 python tools/ab_shapes.py --shapes 256/64 --rounds 3 > $OUT/$v.$i.log 2>&1 || { tail $OUT/$v.$i.log; exit 1; }
     echo "$v $i $(grep 'shape 256/64:' $OUT/$v.$i.log)"
   done

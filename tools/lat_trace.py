@@ -20,7 +20,7 @@ def run(eager):
     if "--shapes" in sys.argv:  # the shape-probe library (make -C avr_amd/csrc shapes): AVR_*_PROBE switches
         from avr_amd import _lib
 
-        _lib.LIB_PATH = os.path.join(ROOT, "avr_amd", "csrc", "build", "libavr_shapes.so")
+        _lib.LIB_PATH = os.path.join(ROOT, "tools", "_lib", "libavr_shapes.so")
     from avr_amd import AVRRender
     from avr_amd.graph import GraphedRender
     from avr_amd.workloads import WORKLOADS

@@ -22,7 +22,7 @@ from avr_amd import _lib  # noqa: E402
 # the shape switch (AVR_LINEAR_SHAPE_PROBE) is read only by the shape-probe
 # build (`make -C avr_amd/csrc shapes`, no phase clocks); the shipped library
 # always runs shape 0
-PROBE = ctypes.CDLL(os.path.join(ROOT, "avr_amd", "csrc", "build", "libavr_shapes.so"))
+PROBE = ctypes.CDLL(os.path.join(ROOT, "tools", "_lib", "libavr_shapes.so"))
 
 
 def main():

@@ -1,5 +1,5 @@
 """Phase clocks of the exact head / linear kernels from the probe build
-(csrc/build/libavr_probe.so, `make -C avr_amd/csrc probe`, csrc/probe.h).
+(tools/_lib/libavr_probe.so, `make -C avr_amd/csrc probe`, csrc/probe.h).
 
 The render runs through the shipped library; the one call under study is
 redirected to the probe library, whose kernel records per wave: start and
@@ -25,10 +25,12 @@ sys.path.insert(0, ROOT)
 from avr_amd import AVRRender, _lib  # noqa: E402
 from avr_amd.workloads import WORKLOADS  # noqa: E402
 
-PROBE = ctypes.CDLL(os.path.join(ROOT, "avr_amd", "csrc", "build", "libavr_probe.so"))
+# AVR_PROBE_LIB: another probe build (tools/build_var.sh NAME "-DAVR_PHASE_PROBES ...")
+PROBE = ctypes.CDLL(os.environ.get("AVR_PROBE_LIB") or os.path.join(ROOT, "tools", "_lib", "libavr_probe.so"))
 for name in ("avr_head_fwd_exact", "avr_linear_relu_fwd", "avr_linear_pack_w", "avr_last_error"):
-    fn = getattr(PROBE, name)
-    fn.restype, fn.argtypes = _lib._SIGS[name]
+    if hasattr(PROBE, name):
+        fn = getattr(PROBE, name)
+        fn.restype, fn.argtypes = _lib._SIGS[name]
 
 
 def summarize(buf, what):

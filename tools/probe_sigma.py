@@ -19,7 +19,7 @@ from avr_amd import _lib, sigma  # noqa: E402
 # tile configs >= 16 (timing experiments, garbage results) exist only in the
 # shapes build: make -C avr_amd/csrc shapes
 _lib.LIB_PATH = os.environ.get("AVR_AB_LIB") or os.path.join(
-    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "avr_amd", "csrc", "build", "libavr_shapes.so")
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "_lib", "libavr_shapes.so")
 
 
 def main():
