@@ -127,11 +127,29 @@ __host__ __device__ constexpr int xs_tile_bytes(int KSM) { return KSM * 1024; }
 #ifndef AVR_EXACT_STAGGER
 #define AVR_EXACT_STAGGER 0
 #endif
+#ifndef AVR_EXACT_DMA_WAVES
+#define AVR_EXACT_DMA_WAVES 0
+#endif
+#ifndef AVR_EXACT_DMA_SPREAD
+#define AVR_EXACT_DMA_SPREAD 0
+#endif
+// Slot flags instead of a workgroup barrier per tile (32-t tiles, a 4-slot
+// ring): per slot a FULL count (loader waves whose pieces landed), a DONE
+// count (waves through the tile; the last one to arrive sums the partials)
+// and a FREE count (the last arriver's release of the slot).  Waves drift
+// apart by up to one tile, so a wave's epilogue and DMA issue fall beside
+// its SIMD partner's MFMA chain.
+#ifndef AVR_EXACT_FLAGS
+#define AVR_EXACT_FLAGS 0
+#endif
+#ifndef AVR_EXACT_NC1  // the barrier form on 32-t tiles and a 4-slot ring (the flags form's shape)
+#define AVR_EXACT_NC1 0
+#endif
 constexpr int kPartBufs = AVR_EXACT_STAGGER ? 3 : 2;
 
 __host__ __device__ constexpr size_t xs_lds_bytes(int KSM, int T, int waves, int rays, int nb, int nc) {
     return (size_t)nb * nc * xs_tile_bytes(KSM) + 4 * (size_t)((T + 3) / 4 * 4) + 4 * (size_t)rays +
-           4 * (size_t)(kPartBufs * waves * 32 * nc) + 4 * (size_t)waves + 8;
+           4 * (size_t)(kPartBufs * waves * 32 * nc) + 4 * (size_t)waves + 8 + 64;
 }
 
 // One work item: RAYS consecutive sorted rays of one column (b, s), WAVES
@@ -148,8 +166,15 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
     constexpr int TT = 32 * NC;
     constexpr int RPW = RAYS / WAVES;    // rays per wave
     constexpr int NQ = RPW / 32;         // 32-ray A tiles per wave
-    constexpr int DPW = NC * KSM / WAVES;  // 1 KiB DMAs per wave and tile
-    static_assert((NC * KSM) % WAVES == 0 && NQ == 1 && DPW * NB <= 63 && NT >= RAYS, "shape");
+    // W-tile DMA pieces (1 KiB each): issued by every wave, or only by one
+    // half of the waves (AVR_EXACT_DMA_WAVES 1: waves 0 .. WAVES/2-1, 2: the
+    // other half), so that on every SIMD one wave's DMA issue stalls fall
+    // beside its partner's MFMAs; spread over all the tile's chains or all in
+    // its first live chain (AVR_EXACT_DMA_SPREAD)
+    constexpr int LW = AVR_EXACT_DMA_WAVES == 0 ? WAVES : WAVES / 2;  // loader waves
+    constexpr int DPW = NC * KSM / LW;                                // pieces per loader wave and tile
+    constexpr int PPC = AVR_EXACT_DMA_SPREAD ? DPW / NC : DPW;        // pieces per chain
+    static_assert((NC * KSM) % LW == 0 && NQ == 1 && DPW * NB <= 63 && NT >= RAYS && KSM % PPC == 0, "shape");
     AVR_PROBE_DECL;
     extern __shared__ __attribute__((aligned(16))) char lds_x[];
     const int T = pp.T, S = pp.n_samples;
@@ -160,9 +185,15 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
     float* zr = wl + RAYS;                                      // wave partials [kPartBufs][WAVES][TT]
     int* dstart = reinterpret_cast<int*>(zr + kPartBufs * WAVES * TT);  // first live t per wave [WAVES]
     int* qnext = dstart + WAVES;                                // claimed items [2]
+    int* fl_full = qnext + 2;                                   // slot flags [3][4] (AVR_EXACT_FLAGS)
+    int* fl_done = fl_full + 4;
+    int* fl_free = fl_full + 8;
+    constexpr bool kFlags = AVR_EXACT_FLAGS && NC == 1 && NB == 4;
 
     const int64_t ncol = (int64_t)B * S;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool loader = AVR_EXACT_DMA_WAVES == 0 || ((AVR_EXACT_DMA_WAVES == 1) == (wave < WAVES / 2));
+    const int lidx = AVR_EXACT_DMA_WAVES == 2 ? wave - WAVES / 2 : wave;  // loader index (if loader)
     // static priority for the second-dispatched half of the waves (the
     // arbitration loser of every segment; MI355X_MICROARCH.md, two waves per SIMD)
     if (prio && wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
@@ -301,6 +332,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             }
             if (tid < RAYS) wl[tid] = p0 + tid < nk ? cur.wsv : 0.0f;
             if (lane == 0) dstart[wave] = pw < nk ? cur.dly : 1 << 30;
+            if (kFlags && tid < 12) fl_full[tid] = tid < 3 ? LW : 0;  // tiles 0-2: landed in the prologue
             // staging area free (the ring may fill); cl, wl, dstart written.  A
             // bare barrier: nothing in flight on the vector-memory counter is
             // waited for (the claim's atomic)
@@ -309,14 +341,15 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             AVR_PROBE_MARK(10);
             const int tb = dstart[0] / TT;       // first tile with a live ray of the item
             const int te = (lim + TT - 1) / TT;  // tiles holding t < lim
-            auto issue = [&](int tau, int slot) {  // W tile tau into ring slot `slot`: this wave's DPW pieces
-                if (AVR_PROBE_SKIP(1)) return;
+            // W tile tau into ring slot `slot`: this loader wave's pieces p0 .. p1-1
+            auto issue_pieces = [&](int tau, int slot, int p0, int p1) {
+                if (AVR_PROBE_SKIP(1) || !loader) return;
                 const char* src =
-                    reinterpret_cast<const char*>(Wf) + (int64_t)tau * TILE + wave * DPW * 1024 + 16 * lane;
-                const uint32_t dst = ring_lds + slot * TILE + wave * DPW * 1024;
-#pragma unroll
-                for (int d = 0; d < DPW; ++d) dma_row16(src + d * 1024, dst + d * 1024);
+                    reinterpret_cast<const char*>(Wf) + (int64_t)tau * TILE + lidx * DPW * 1024 + 16 * lane;
+                const uint32_t dst = ring_lds + slot * TILE + lidx * DPW * 1024;
+                for (int d = p0; d < p1; ++d) dma_row16(src + d * 1024, dst + d * 1024);
             };
+            auto issue = [&](int tau, int slot) { issue_pieces(tau, slot, 0, DPW); };
             for (int i = 0; i < NB - 1; ++i)
                 if (tb + i < te) issue(tb + i, i);
             // the next item's metadata: in flight under this item, younger than
@@ -350,22 +383,25 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             // each stalls the wave ~100 cycles behind the previous one
             // (tools/probe_phases.py), while between MFMAs the stall overlaps
             // the matrix pipe.
-            auto chain = [&](int slot, int c, int dtile, int dslot) {
+            // pieces pbase .. pbase + PPC - 1 of tile dtile (if >= 0) issued
+            // inside the chain, one every KSM / PPC MFMAs
+            auto chain = [&](int slot, int c, int dtile, int dslot, int pbase) {
                 const char* bsrc = ring + slot * TILE + c * xs_tile_bytes(KSM) + 16 * lane;
                 constexpr int D = KSM < 8 ? KSM : 8;  // B fragments read ahead
-                constexpr int DSTEP = KSM / DPW;      // MFMAs per DMA piece
+                constexpr int DSTEP = KSM / PPC;      // MFMAs per DMA piece
                 frag8 bw[D];
 #pragma unroll
                 for (int u = 0; u < D; ++u) bw[u] = *reinterpret_cast<const frag8*>(bsrc + u * 1024);
                 f32x16 acc = f32x16{};
-                const char* dsrc = reinterpret_cast<const char*>(Wf) + (int64_t)dtile * TILE + wave * DPW * 1024 + 16 * lane;
-                const uint32_t ddst = ring_lds + dslot * TILE + wave * DPW * 1024;
+                const char* dsrc = reinterpret_cast<const char*>(Wf) + (int64_t)dtile * TILE +
+                                   (lidx * DPW + pbase) * 1024 + 16 * lane;
+                const uint32_t ddst = ring_lds + dslot * TILE + (lidx * DPW + pbase) * 1024;
+                const bool dma = dtile >= 0 && loader && !AVR_PROBE_SKIP(1);
 #pragma unroll
                 for (int ks = 0; ks < KSM; ++ks) {
                     acc = mfma16<E>(a[0][ks], bw[ks % D], acc);
                     if (ks + D < KSM) bw[ks % D] = *reinterpret_cast<const frag8*>(bsrc + (ks + D) * 1024);
-                    if (ks % DSTEP == 0 && dtile >= 0 && !AVR_PROBE_SKIP(1))
-                        dma_row16(dsrc + (ks / DSTEP) * 1024, ddst + (ks / DSTEP) * 1024);
+                    if (ks % DSTEP == 0 && dma) dma_row16(dsrc + (ks / DSTEP) * 1024, ddst + (ks / DSTEP) * 1024);
                 }
                 return acc;
             };
@@ -432,6 +468,91 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             const bool defer = kStag && wave >= WAVES / 2;
             f32x16 dacc = f32x16{};
             bool dlive = false;  // a deferred last chain is pending
+            if constexpr (kFlags) {
+                // LDS counter ops by lane 0 (one per wave); polls read the
+                // word in every lane (a broadcast) and spin with s_sleep
+                auto lds_add = [&](int* p, int v) {
+                    if (lane == 0) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                };
+                // (bounded: a protocol error ends the spin after ~30 ms with a
+                // wrong result rather than a hung launch)
+                auto poll_ge = [&](const int* p, int target) {
+                    for (int spin = 0; spin < (1 << 20); ++spin) {
+                        if (__builtin_amdgcn_readfirstlane(
+                                __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >= target)
+                            break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                };
+                // vector-memory operations this wave has issued (for counted
+                // vmcnt waits on one tile's pieces) and the count after the
+                // pieces of the tile in each slot
+                int nops = 0;
+                int mark[NB] = {0, 0, 0, 0};
+                for (int k = 0; k < NB - 1; ++k) mark[k] = 0;  // prologue tiles: landed
+                for (int tau = tb; tau < te; ++tau) {
+                    const int i = tau - tb;
+                    const int slot = i & 3, gen = i >> 2;
+                    AVR_PROBE_BEGIN(comp);
+                    // tile i + 3 goes into the slot tile i - 1 used: every wave
+                    // must be through tile i - 1 (its last arriver's release)
+                    const int dtile = tau + 3 < te ? tau + 3 : -1;
+                    const int dslot = (i + 3) & 3;
+                    if (dtile >= 0 && loader && i >= 1) poll_ge(fl_free + dslot, ((i - 1) >> 2) + 1);
+                    // tile i's pieces from every loader wave
+                    if (i >= 3) poll_ge(fl_full + slot, LW * (gen + 1));
+                    float zl = 0.0f;
+                    const int t0 = TT * tau;
+                    bool issued = false;
+                    if (t0 + 31 >= dstart[wave] && t0 < lim) {
+                        const f32x16 acc = chain(slot, 0, dtile, dslot, 0);
+                        issued = dtile >= 0;
+                        zl = epi(acc, tau, 0);
+                    }
+                    if (dtile >= 0 && !issued) issue_pieces(dtile, dslot, 0, DPW);
+                    if (dtile >= 0 && loader) {
+                        nops += DPW;
+                        mark[dslot] = nops;
+                    }
+                    AVR_PROBE_END(comp, 6);
+                    put(zl, slot, 0);
+                    AVR_PROBE_BEGIN(dma);
+                    // tile i + 2's pieces (issued during tile i - 1) landed:
+                    // published for the waves that reach it
+                    if (i >= 1 && tau + 2 < te && loader) {
+                        wait_vm(nops - mark[(i + 2) & 3]);
+                        lds_add(fl_full + ((i + 2) & 3), 1);
+                    }
+                    if (i == min(1, te - 1 - tb)) {
+                        load_dly(nx);
+                        ++nops;
+                        dly_issued = true;
+                    }
+                    AVR_PROBE_END(dma, 4);
+                    AVR_PROBE_BEGIN(bar);
+                    // through tile i: its B reads and the partial written
+                    __builtin_amdgcn_s_waitcnt(0xC07F);
+                    int old = 0;
+                    if (lane == 0)
+                        old = __hip_atomic_fetch_add(fl_done + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    old = __builtin_amdgcn_readfirstlane(old);
+                    AVR_PROBE_END(bar, 5);
+                    if (old == WAVES * gen + WAVES - 1) {
+                        // the last arrival: the partials in wave order, then the
+                        // slot is free for tile i + 4
+                        sum_tile(tau, slot);
+                        ++nops;
+                        __builtin_amdgcn_s_waitcnt(0xC07F);
+                        lds_add(fl_free + slot, 1);
+                    }
+                }
+                touch(nx);
+                touched = true;
+                // every wave through every tile (and every sum done) before the
+                // next item's prologue reuses the ring and resets the flags
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_s_barrier();
+            } else {
             for (int tau = tb; tau < te; ++tau) {
                 const int i = tau - tb;
                 AVR_PROBE_BEGIN(comp);
@@ -443,8 +564,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                 }
                 // tile tau + NB - 1 into the slot tile tau - 1 left: inside the
                 // first live group's chain, else here
-                int dtile = tau + NB - 1 < te ? tau + NB - 1 : -1;
+                const int dtile = tau + NB - 1 < te ? tau + NB - 1 : -1;
                 const int dslot = (i + NB - 1) % NB;
+                int pdone = 0;  // pieces of dtile issued (in chain order)
                 float zl[NC];
 #pragma unroll
                 for (int c = 0; c < NC; ++c) {
@@ -453,8 +575,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                     const int t0 = TT * tau + 32 * c;
                     zl[c] = 0.0f;
                     if (t0 + 31 >= dstart[wave] && t0 < lim) {
-                        const f32x16 acc = chain(i % NB, c, dtile, dslot);
-                        dtile = -1;
+                        const bool carry = pdone < DPW;
+                        const f32x16 acc = chain(i % NB, c, carry ? dtile : -1, dslot, pdone);
+                        if (carry) pdone += PPC;
                         if (kStag && defer && c == NC - 1) {
                             dacc = acc;
                             dlive = true;
@@ -463,13 +586,13 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                         }
                     }
                 }
-                if (dtile >= 0) issue(dtile, dslot);
+                if (dtile >= 0 && pdone < DPW) issue_pieces(dtile, dslot, pdone, DPW);
                 AVR_PROBE_END(comp, 6);
 #pragma unroll
                 for (int c = 0; c < NC; ++c)
                     if (!(kStag && defer && c == NC - 1)) put(zl[c], i % kPartBufs, c);
                 AVR_PROBE_BEGIN(dma);
-                if (tau + 1 < te) {
+                if (tau + 1 < te && loader) {
                     // this wave's pieces of tile tau+1 have landed.  Younger in
                     // vmcnt: the ring's later tiles and this wave's partial
                     // stores since tile tau+1 was issued (a wave stores after
@@ -499,7 +622,8 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                     else sum_tile(tau, i % kPartBufs);
                 }
             }
-            if constexpr (kStag) {
+            }
+            if constexpr (kStag && !kFlags) {
                 // the last tile: its deferred chains, one more barrier, its sum
                 const int n = te - tb;
                 if (defer) put(dlive ? epi(dacc, te - 1, NC - 1) : 0.0f, (n - 1) % kPartBufs, NC - 1);
@@ -586,6 +710,7 @@ size_t exact_lds(int R, int T, int K) {
     const int KSM = exact_ksm(K);
     const ExactShape sh = exact_shape(R, T, K);
     if (sh.rays == 128) return xs_lds_bytes(KSM, T, 4, 128, 2, 1);
+    if ((AVR_EXACT_FLAGS || AVR_EXACT_NC1) && K == 512) return xs_lds_bytes(KSM, T, 8, 256, 4, 1);
     if (sh.tt64) return xs_lds_bytes(KSM, T, 8, 256, 2, 2);
     return xs_lds_bytes(KSM, T, 8, 256, 4, 1);
 }
@@ -669,6 +794,9 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
     // config-2 fp16 fused render (tools/ab_shapes.py, 5 interleaved rounds);
     // the 4-wave items (two workgroups per CU) lose with it (252 vs 244)
     int prio = small ? 0 : 1;
+#ifdef AVR_EXACT_NOPRIO
+    prio = 0;
+#endif
     if (const char* pe = AVR_PROBE_ENV("AVR_EXACT_PRIO_PROBE")) prio = atoi(pe);
     auto run = [&](auto e_tag) {
         using E = decltype(e_tag);
@@ -693,6 +821,8 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
             else if (KSM == 16) go(head_exact_kernel<E, 16, 4, 128, 2, 1, false>, 16, 4, 128, 2, 1, h);
             else if (rowdma) go(head_exact_kernel<E, 32, 4, 128, 2, 1, true>, 32, 4, 128, 2, 1, h);
             else go(head_exact_kernel<E, 32, 4, 128, 2, 1, false>, 32, 4, 128, 2, 1, h);
+        } else if ((AVR_EXACT_FLAGS || AVR_EXACT_NC1) && rowdma) {
+            go(head_exact_kernel<E, 32, 8, 256, 4, 1, true>, 32, 8, 256, 4, 1, h);
         } else if (tt64 && rowdma) {
             go(head_exact_kernel<E, 32, 8, 256, 2, 2, true>, 32, 8, 256, 2, 2, h);
         } else {
