@@ -83,8 +83,18 @@ __device__ __forceinline__ float round16(float x) {
 // the builtin it inserts vmcnt(0) inside the MFMA chain); completion is
 // waited for explicitly with counted vmcnt.
 __device__ __forceinline__ void dma_row16(const void* g, uint32_t lds) {
+#if AVR_EXACT_XCHAIN_RFL
+    lds = __builtin_amdgcn_readfirstlane(lds);  // kept in an SGPR under pressure
+#endif
+#if AVR_EXACT_DMA_NOMEM
+    // no "memory" clobber: the B-fragment reads of other ring slots may be
+    // scheduled across the DMA (its slot's reuse is ordered by the barriers,
+    // which keep their place relative to this volatile statement)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(g));
+#else
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(g)
                  : "memory", "m0");
+#endif
 }
 
 // s_waitcnt vmcnt(n) (expcnt / lgkmcnt not waited on; gfx9 encoding)
@@ -142,10 +152,28 @@ __host__ __device__ constexpr int xs_tile_bytes(int KSM) { return KSM * 1024; }
 #ifndef AVR_EXACT_FLAGS
 #define AVR_EXACT_FLAGS 0
 #endif
+// B fragments read ahead in the MFMA chain; XCHAIN: the two chains of a
+// 64-t tile as one B-fragment stream (the second chain's first fragments are
+// read during the first chain's tail and land under its epilogue)
+#ifndef AVR_EXACT_D
+#define AVR_EXACT_D 8
+#endif
+#ifndef AVR_EXACT_XCHAIN
+#define AVR_EXACT_XCHAIN 0
+#endif
+// PREFETCH = k > 0: k tiles before an item's end, every wave touches each
+// 128-byte line of its next item's 32 rows (four dword loads per lane), so
+// that the next prologue's row loads find them in L2 / the Infinity Cache
+#ifndef AVR_EXACT_PREFETCH
+#define AVR_EXACT_PREFETCH 0
+#endif
 #ifndef AVR_EXACT_NC1  // the barrier form on 32-t tiles and a 4-slot ring (the flags form's shape)
 #define AVR_EXACT_NC1 0
 #endif
-constexpr int kPartBufs = AVR_EXACT_STAGGER ? 3 : 2;
+// partial buffers: one per tile in flight (flags: one per ring slot, the
+// partials of tile i live in zr[i % 4] until its last arriver sums them)
+constexpr int kPartBufs = AVR_EXACT_FLAGS ? 4 : (AVR_EXACT_STAGGER ? 3 : 2);
+// (placed after the flag switches below, which need four)
 
 __host__ __device__ constexpr size_t xs_lds_bytes(int KSM, int T, int waves, int rays, int nb, int nc) {
     return (size_t)nb * nc * xs_tile_bytes(KSM) + 4 * (size_t)((T + 3) / 4 * 4) + 4 * (size_t)rays +
@@ -387,7 +415,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             // inside the chain, one every KSM / PPC MFMAs
             auto chain = [&](int slot, int c, int dtile, int dslot, int pbase) {
                 const char* bsrc = ring + slot * TILE + c * xs_tile_bytes(KSM) + 16 * lane;
-                constexpr int D = KSM < 8 ? KSM : 8;  // B fragments read ahead
+                constexpr int D = KSM < AVR_EXACT_D ? KSM : AVR_EXACT_D;  // B fragments read ahead
                 constexpr int DSTEP = KSM / PPC;      // MFMAs per DMA piece
                 frag8 bw[D];
 #pragma unroll
@@ -437,6 +465,35 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                 }
                 return z;
             };
+            // both chains of a 64-t tile (NC == 2) as one B stream; chain 0
+            // carries the DMA pieces; returns chain 1's accumulator, chain 0's
+            // epilogue sum in z0
+            auto chain2 = [&](int slot, int dtile, int dslot, int tau, float& z0) {
+                const char* b0 = ring + slot * TILE + 16 * lane;
+                constexpr int D = AVR_EXACT_D;
+                constexpr int DSTEP = KSM / PPC;
+                frag8 bw[D];
+#pragma unroll
+                for (int u = 0; u < D; ++u) bw[u] = *reinterpret_cast<const frag8*>(b0 + u * 1024);
+                const char* dsrc = reinterpret_cast<const char*>(Wf) + (int64_t)dtile * TILE + (lidx * DPW) * 1024 + 16 * lane;
+                const uint32_t ddst = ring_lds + dslot * TILE + (lidx * DPW) * 1024;
+                const bool dma = dtile >= 0 && loader && !AVR_PROBE_SKIP(1);
+                f32x16 acc = f32x16{};
+#pragma unroll
+                for (int g = 0; g < KSM; ++g) {
+                    acc = mfma16<E>(a[0][g], bw[g % D], acc);
+                    bw[g % D] = *reinterpret_cast<const frag8*>(b0 + (g + D) * 1024);  // g + D < 2 KSM
+                    if (g % DSTEP == 0 && dma) dma_row16(dsrc + (g / DSTEP) * 1024, ddst + (g / DSTEP) * 1024);
+                }
+                z0 = epi(acc, tau, 0);
+                f32x16 acc1 = f32x16{};
+#pragma unroll
+                for (int g = KSM; g < 2 * KSM; ++g) {
+                    acc1 = mfma16<E>(a[0][g - KSM], bw[g % D], acc1);
+                    if (g + D < 2 * KSM) bw[g % D] = *reinterpret_cast<const frag8*>(b0 + (g + D) * 1024);
+                }
+                return acc1;
+            };
             // a chain's per-lane sum, lower + upper lane half (rows 4 half +
             // ...; the same association in every lane), into the partials of
             // buffer `buf`
@@ -460,12 +517,14 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             // the wave that sums (and stores) a tile's partials right after the
             // barrier of iteration m: tile m by wave m % WAVES, or with the
             // stagger tile m - 1 by one of the non-deferring waves
+            // (AVR_EXACT_STAGGER 1: waves WAVES/2.. defer; 2: waves 0 .. WAVES/2-1)
+            constexpr int kSumOff = AVR_EXACT_STAGGER == 2 ? WAVES / 2 : 0;
             auto summer = [&](int m) {
-                if constexpr (AVR_EXACT_STAGGER) return m >= 1 ? (m - 1) % (WAVES / 2) : -1;
+                if constexpr (AVR_EXACT_STAGGER) return m >= 1 ? kSumOff + (m - 1) % (WAVES / 2) : -1;
                 else return m % WAVES;
             };
             constexpr bool kStag = AVR_EXACT_STAGGER;
-            const bool defer = kStag && wave >= WAVES / 2;
+            const bool defer = kStag && ((wave >= WAVES / 2) == (AVR_EXACT_STAGGER == 1));
             f32x16 dacc = f32x16{};
             bool dlive = false;  // a deferred last chain is pending
             if constexpr (kFlags) {
@@ -553,6 +612,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                 __builtin_amdgcn_s_waitcnt(0xC07F);
                 __builtin_amdgcn_s_barrier();
             } else {
+            uint32_t pfs = 0;  // sink of the row prefetch
             for (int tau = tb; tau < te; ++tau) {
                 const int i = tau - tb;
                 AVR_PROBE_BEGIN(comp);
@@ -568,11 +628,22 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                 const int dslot = (i + NB - 1) % NB;
                 int pdone = 0;  // pieces of dtile issued (in chain order)
                 float zl[NC];
+                bool both = false;
+                if constexpr (AVR_EXACT_XCHAIN && NC == 2 && !AVR_EXACT_DMA_SPREAD && !kStag) {
+                    // both chains live: one B stream over the two
+                    both = __builtin_amdgcn_readfirstlane((int)(TT * tau + 31 >= dstart[wave] && TT * tau + 32 < lim));
+                    if (both) {
+                        const f32x16 acc1 = chain2(i % NB, dtile, dslot, tau, zl[0]);
+                        zl[1] = epi(acc1, tau, 1);
+                        pdone = DPW;
+                    }
+                }
 #pragma unroll
                 for (int c = 0; c < NC; ++c) {
                     // group c holds a live ray of the wave from the wave's first
                     // live t on (cnt is nondecreasing in t), nothing at or past lim
                     const int t0 = TT * tau + 32 * c;
+                    if (both) continue;
                     zl[c] = 0.0f;
                     if (t0 + 31 >= dstart[wave] && t0 < lim) {
                         const bool carry = pdone < DPW;
@@ -608,6 +679,15 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                     load_dly(nx);
                     dly_issued = true;
                 }
+                if constexpr (AVR_EXACT_PREFETCH > 0 && ROWDMA) {  // whole 1 KiB rows (K == 512) only
+                    if (i == max(1, te - tb - AVR_EXACT_PREFETCH) && nx.item < nitems) {
+                        const int colp = nx.item % (int)ncol;
+                        const uint32_t* hn = reinterpret_cast<const uint32_t*>(
+                            h + (((int64_t)(colp / S) * R + nx.ray) * S + colp % S) * K);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) pfs ^= hn[(2 * u + half) * 32];
+                    }
+                }
                 if (tau == te - 1) {  // before the last partial store: nothing young to wait for
                     touch(nx);
                     touched = true;
@@ -622,6 +702,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                     else sum_tile(tau, i % kPartBufs);
                 }
             }
+            if constexpr (AVR_EXACT_PREFETCH > 0) asm volatile("" ::"v"(pfs));
             }
             if constexpr (kStag && !kFlags) {
                 // the last tile: its deferred chains, one more barrier, its sum
@@ -629,7 +710,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                 if (defer) put(dlive ? epi(dacc, te - 1, NC - 1) : 0.0f, (n - 1) % kPartBufs, NC - 1);
                 __builtin_amdgcn_s_waitcnt(0xC07F);
                 __builtin_amdgcn_s_barrier();
-                if (wave == (n - 1) % (WAVES / 2)) sum_tile(te - 1, (n - 1) % kPartBufs);
+                if (wave == kSumOff + (n - 1) % (WAVES / 2)) sum_tile(te - 1, (n - 1) % kPartBufs);
             }
             // zero outside the item's tiles (after the tiles: no wait above
             // includes these stores)

@@ -14,8 +14,12 @@ step() {
 }
 for wl in ${WORKLOADS:-c2_meshrir_1024x256x512}; do
   step xab_$wl 400 python tools/xbench_exact.py "$LIBS" --workload $wl --rounds ${ROUNDS:-5} --iters ${ITERS:-10}
+  # LIBS2: a second set (new, riskier variants), run only after the first passed
+  if [ -n "${LIBS2:-}" ]; then
+    step xab2_$wl 400 python tools/xbench_exact.py "$LIBS2" --workload $wl --rounds ${ROUNDS:-5} --iters ${ITERS:-10}
+  fi
 done
 for p in ${PROBES:-}; do
-  AVR_PROBE_LIB=tools/_lib/libvar_$p.so step probe_$p 300 python tools/probe_phases.py exact
+  AVR_PROBE_LIB=tools/_lib/libvar_$p.so step probe_$p 300 python tools/probe_phases.py exact ${SKIPS:-0}
 done
 echo all-ok

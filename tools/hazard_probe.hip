@@ -101,6 +101,97 @@ PROBE_KERNEL(war_mov_2, SET_OLD "s_nop 7\n\t" MFMA NOPS_2 MOV_NEW DRAIN)
 PROBE_KERNEL(war_mov_4, SET_OLD "s_nop 7\n\t" MFMA NOPS_4 MOV_NEW DRAIN)
 PROBE_KERNEL(war_mov_8, SET_OLD "s_nop 7\n\t" MFMA NOPS_8 MOV_NEW DRAIN)
 
+// WAR with the matrix pipe busy: the MFMA that reads B issues behind another
+// MFMA (on its own accumulator, or on the same one: a dependent chain), then
+// N states, then the VALU rewrite of B.  Q = v[204:219], P = v[220:235]
+#define MFMA_P_OTHER "v_mfma_f32_32x32x16_f16 v[220:235], %[a], %[hv], 0\n\t"
+#define MFMA_Q_OTHER "v_mfma_f32_32x32x16_f16 v[204:219], %[a], %[hv], 0\n\t"
+#define MFMA_Q_DEP "v_mfma_f32_32x32x16_f16 v[204:219], %[a], v[200:203], v[204:219]\n\t"
+#define CLOB2 CLOB, "v220", "v221", "v222", "v223", "v224", "v225", "v226", "v227", "v228", "v229", "v230", \
+    "v231", "v232", "v233", "v234", "v235"
+#define PROBE_KERNEL2(NAME, BODY)                                                                 \
+    __global__ __launch_bounds__(512) void NAME(const uint32_t* in, float* out, int iters) {     \
+        const int lane = threadIdx.x & 63;                                                        \
+        const size_t w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;                      \
+        frag8 a, bo, lo, hi;                                                                      \
+        for (int q = 0; q < 4; ++q) {                                                             \
+            a[q] = in[lane * 4 + q];                                                              \
+            bo[q] = in[256 + lane * 4 + q];                                                       \
+            lo[q] = in[512 + lane * 4 + q];                                                       \
+            hi[q] = in[768 + lane * 4 + q];                                                       \
+        }                                                                                         \
+        int nbad = 0;                                                                             \
+        float first[16];                                                                          \
+        for (int it = 0; it < iters; ++it) {                                                      \
+            float d[16];                                                                          \
+            asm volatile(BODY COPY_OUT : OUTS : INS, [hv] "v"(hi) : CLOB2);                       \
+            if (it == 0)                                                                          \
+                for (int r = 0; r < 16; ++r) first[r] = d[r];                                     \
+            for (int r = 0; r < 16; ++r) nbad += d[r] != first[r];                                \
+        }                                                                                         \
+        for (int r = 0; r < 16; ++r) out[(w * 64 + lane) * 16 + r] = first[r];                   \
+        out[(size_t)gridDim.x * (blockDim.x / 64) * 64 * 16 + w * 64 + lane] = (float)nbad;      \
+    }
+// behind an independent MFMA: Q = A x B_old
+PROBE_KERNEL2(war_busy_indep_0, SET_OLD "s_nop 7\n\t" MFMA_P_OTHER MFMA NOPS_0 MOV_NEW DRAIN)
+PROBE_KERNEL2(war_busy_indep_2, SET_OLD "s_nop 7\n\t" MFMA_P_OTHER MFMA NOPS_2 MOV_NEW DRAIN)
+// dependent chain: Q = A x hi, then Q += A x B_old (must not see B_new)
+PROBE_KERNEL2(war_busy_dep_0, SET_OLD "s_nop 7\n\t" MFMA_Q_OTHER MFMA_Q_DEP NOPS_0 MOV_NEW DRAIN)
+PROBE_KERNEL2(war_busy_dep_1, SET_OLD "s_nop 7\n\t" MFMA_Q_OTHER MFMA_Q_DEP NOPS_1 MOV_NEW DRAIN)
+PROBE_KERNEL2(war_busy_dep_2, SET_OLD "s_nop 7\n\t" MFMA_Q_OTHER MFMA_Q_DEP NOPS_2 MOV_NEW DRAIN)
+PROBE_KERNEL2(war_busy_dep_4, SET_OLD "s_nop 7\n\t" MFMA_Q_OTHER MFMA_Q_DEP NOPS_4 MOV_NEW DRAIN)
+PROBE_KERNEL2(war_busy_dep_8, SET_OLD "s_nop 7\n\t" MFMA_Q_OTHER MFMA_Q_DEP NOPS_8 MOV_NEW DRAIN)
+// RAW behind an independent MFMA: Q = A x B_new
+PROBE_KERNEL2(raw_busy_0, SET_OLD "s_nop 7\n\t" MFMA_P_OTHER PERM_NEW NOPS_0 MFMA DRAIN)
+PROBE_KERNEL2(raw_busy_1, SET_OLD "s_nop 7\n\t" MFMA_P_OTHER PERM_NEW NOPS_1 MFMA DRAIN)
+
+// WAR on a DS read's ADDRESS register: ds_read_b64 from the address in v236,
+// N states, a VALU rewrite of v236 (another address).  The read must return
+// the OLD address's data.  BUSY: 8 ds_read_b128 queued ahead of it, so the
+// LDS unit is backed up when the victim read issues.
+#define DS_WAR(NAME, BUSY, NOPS)                                                                  \
+    __global__ __launch_bounds__(512) void NAME(float* out, int iters) {                          \
+        __shared__ uint2 tab[1024];                                                                \
+        for (int i = threadIdx.x; i < 1024; i += blockDim.x) tab[i] = make_uint2(7 * i + 1, 13 * i + 5); \
+        __syncthreads();                                                                           \
+        const int lane = threadIdx.x & 63;                                                         \
+        const size_t w = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;                       \
+        const uint32_t base = (uint32_t)(uintptr_t)tab;                                            \
+        const uint32_t a_old = base + 8 * ((lane * 5 + 3) & 511), a_new = base + 8 * (512 + lane);   \
+        int nbad = 0;                                                                              \
+        uint32_t first0 = 0, first1 = 0;                                                           \
+        for (int it = 0; it < iters; ++it) {                                                       \
+            uint32_t d0, d1;                                                                       \
+            asm volatile("v_mov_b32 v236, %[ao]\n\ts_nop 7\n\t" BUSY                             \
+                         "ds_read_b64 v[238:239], v236\n\t" NOPS                                 \
+                         "v_mov_b32 v236, %[an]\n\t"                                              \
+                         "s_waitcnt lgkmcnt(0)\n\ts_nop 3\n\t"                                   \
+                         "v_mov_b32 %[d0], v238\n\tv_mov_b32 %[d1], v239"                        \
+                         : [d0] "=&v"(d0), [d1] "=&v"(d1)                                          \
+                         : [ao] "v"(a_old), [an] "v"(a_new), [b] "v"(base + 16 * lane)            \
+                         : "v220", "v221", "v222", "v223", "v224", "v225", "v226", "v227", "v228", \
+                           "v229", "v230", "v231", "v232", "v233", "v234", "v235", "v236", "v237", \
+                           "v238", "v239", "memory");                                              \
+            if (it == 0) {                                                                         \
+                first0 = d0;                                                                       \
+                first1 = d1;                                                                       \
+            }                                                                                      \
+            nbad += (d0 != first0) || (d1 != first1);                                              \
+        }                                                                                          \
+        out[(w * 64 + lane) * 2 + 0] = __uint_as_float(first0);                                    \
+        out[(w * 64 + lane) * 2 + 1] = __uint_as_float(first1);                                    \
+        out[(size_t)gridDim.x * (blockDim.x / 64) * 64 * 2 + w * 64 + lane] = (float)nbad;        \
+    }
+#define DS_BUSY                                                                                   \
+    "ds_read_b128 v[220:223], %[b]\n\tds_read_b128 v[224:227], %[b] offset:1024\n\t"             \
+    "ds_read_b128 v[228:231], %[b] offset:2048\n\tds_read_b128 v[232:235], %[b] offset:3072\n\t" \
+    "ds_read_b128 v[220:223], %[b] offset:4096\n\tds_read_b128 v[224:227], %[b] offset:5120\n\t" \
+    "ds_read_b128 v[228:231], %[b] offset:6144\n\tds_read_b128 v[232:235], %[b] offset:7168\n\t"
+DS_WAR(ds_war_0, "", NOPS_0)
+DS_WAR(ds_war_busy_0, DS_BUSY, NOPS_0)
+DS_WAR(ds_war_busy_1, DS_BUSY, NOPS_1)
+DS_WAR(ds_war_busy_4, DS_BUSY, NOPS_4)
+
 // bf16 (the §13e2 DFT's instruction): checked against the nops-8 form and
 // the old-operand product, both measured (no host reference)
 PROBE_KERNEL(raw_bf_0, SET_OLD "s_nop 7\n\t" PERM_NEW NOPS_0 MFMA_BF DRAIN)
@@ -198,10 +289,16 @@ int main(int argc, char** argv) {
     std::vector<uint32_t> bnew(256), bold(in.begin() + 256, in.begin() + 512);
     for (int i = 0; i < 256; ++i) bnew[i] = (in[512 + i] & 0xFFFF) | (in[768 + i] << 16);
     std::vector<uint32_t> bmov(in.begin() + 512, in.begin() + 768);
-    std::vector<float> d_old(1024), d_new(1024), d_mov(1024);
+    std::vector<float> d_old(1024), d_new(1024), d_mov(1024), d_hi(1024), d_dep(1024), d_depnew(1024);
     ref(in.data(), bold.data(), d_old.data());
     ref(in.data(), bnew.data(), d_new.data());
     ref(in.data(), bmov.data(), d_mov.data());
+    std::vector<uint32_t> bhi(in.begin() + 768, in.begin() + 1024);
+    ref(in.data(), bhi.data(), d_hi.data());
+    for (int i = 0; i < 1024; ++i) {
+        d_dep[i] = d_hi[i] + d_old[i];     // the dependent chain on the old B
+        d_depnew[i] = d_hi[i] + d_mov[i];  // ... on the rewritten B (the hazard)
+    }
     uint32_t* din;
     float* dout;
     const size_t nout = (size_t)waves * 64 * 16 + (size_t)waves * 64;
@@ -212,8 +309,12 @@ int main(int argc, char** argv) {
     struct K {
         const char* name;
         kern_t k;
-        int war;
-    } ks[] = {{"raw_perm_nops0", raw_perm_0, 0},   {"raw_perm_nops1", raw_perm_1, 0},
+        int war;  // 0: want new (RAW), 1: want old (WAR), 2: dependent chain on the old B
+    } ks[] = {{"war_busy_indep_nops0", war_busy_indep_0, 1}, {"war_busy_indep_nops2", war_busy_indep_2, 1},
+              {"war_busy_dep_nops0", war_busy_dep_0, 2},     {"war_busy_dep_nops1", war_busy_dep_1, 2},
+              {"war_busy_dep_nops2", war_busy_dep_2, 2},     {"war_busy_dep_nops4", war_busy_dep_4, 2},
+              {"war_busy_dep_nops8", war_busy_dep_8, 2},     {"raw_busy_nops0", raw_busy_0, 0},
+              {"raw_busy_nops1", raw_busy_1, 0},{"raw_perm_nops0", raw_perm_0, 0},   {"raw_perm_nops1", raw_perm_1, 0},
               {"raw_perm_nops2", raw_perm_2, 0},   {"raw_perm_nops3", raw_perm_3, 0},
               {"raw_perm_nops4", raw_perm_4, 0},   {"raw_perm_nops8", raw_perm_8, 0},
               {"raw_perm_compiler", raw_perm_compiler, 0},
@@ -228,8 +329,8 @@ int main(int argc, char** argv) {
             return 1;
         }
         hipMemcpy(out.data(), dout, nout * 4, hipMemcpyDeviceToHost);
-        const float* want = k.war ? d_old.data() : d_new.data();
-        const float* other = k.war ? d_mov.data() : d_old.data();
+        const float* want = k.war == 2 ? d_dep.data() : k.war ? d_old.data() : d_new.data();
+        const float* other = k.war == 2 ? d_depnew.data() : k.war ? d_mov.data() : d_old.data();
         long ok = 0, wrong_other = 0, garbage = 0, unstable = 0;
         long bad_lane_hist[64] = {};
         for (int w = 0; w < waves; ++w)
@@ -259,6 +360,53 @@ int main(int argc, char** argv) {
             }
         printf("]}\n");
         fflush(stdout);
+    }
+    // DS address WAR
+    {
+        typedef void (*dk_t)(float*, int);
+        struct KD {
+            const char* name;
+            dk_t k;
+        } kd[] = {{"ds_addr_war_nops0", ds_war_0}, {"ds_addr_war_busy_nops0", ds_war_busy_0},
+                  {"ds_addr_war_busy_nops1", ds_war_busy_1}, {"ds_addr_war_busy_nops4", ds_war_busy_4}};
+        const size_t nd = (size_t)waves * 64 * 3;
+        std::vector<float> od(nd);
+        for (auto& k : kd) {
+            hipMemset(dout, 0, nd * 4);
+            hipLaunchKernelGGL(k.k, dim3(blocks), dim3(threads), 0, 0, dout, iters);
+            if (hipDeviceSynchronize() != hipSuccess) {
+                printf("{\"probe\": \"%s\", \"error\": \"launch failed\"}\n", k.name);
+                return 1;
+            }
+            hipMemcpy(od.data(), dout, nd * 4, hipMemcpyDeviceToHost);
+            long ok = 0, newaddr = 0, other = 0, unstable = 0;
+            long badl[64] = {};
+            for (size_t i = 0; i < (size_t)waves * 64; ++i) {
+                const int lane = (int)(i & 63);
+                const int io = (lane * 5 + 3) & 511, in_ = 512 + lane;
+                uint32_t d0, d1;
+                memcpy(&d0, &od[i * 2], 4);
+                memcpy(&d1, &od[i * 2 + 1], 4);
+                if (d0 == (uint32_t)(7 * io + 1) && d1 == (uint32_t)(13 * io + 5)) ++ok;
+                else {
+                    ++badl[lane];
+                    if (d0 == (uint32_t)(7 * in_ + 1) && d1 == (uint32_t)(13 * in_ + 5)) ++newaddr;
+                    else ++other;
+                }
+                unstable += od[(size_t)waves * 64 * 2 + i] != 0.0f;
+            }
+            printf("{\"probe\": \"%s\", \"lanes\": %ld, \"correct\": %ld, \"new_address\": %ld, \"neither\": %ld, "
+                   "\"lanes_varying_over_iterations\": %ld, \"bad_lanes\": [", k.name, (long)waves * 64, ok, newaddr,
+                   other, unstable);
+            bool fst = true;
+            for (int l = 0; l < 64; ++l)
+                if (badl[l]) {
+                    printf("%s%d", fst ? "" : ",", l);
+                    fst = false;
+                }
+            printf("]}\n");
+            fflush(stdout);
+        }
     }
     // bf16 forms against measured references
     auto run = [&](kern_t k, std::vector<float>& o) {
