@@ -124,42 +124,43 @@ def _zero_bias(n, dtype, device):
     return z
 
 
-# AVR_LINEAR=1 runs the width-512 hidden layers on csrc/linear_fwd.hip
-# (opt-in until it measures faster than hipBLASLt)
-_LINEAR_HIP = os.environ.get("AVR_LINEAR", "0") == "1"
+# Two consecutive width-512 hidden layers at inference in ONE launch
+# (csrc/mlp512.hip: the intermediate activation stays on chip, x read and y
+# written once).  AVR_MLP512X2=0 keeps the per-layer GEMMs.
+_MLP512X2 = os.environ.get("AVR_MLP512X2", "0") == "1"
 
 
-def _linear_relu_hip(x, w, w_master=None, cache=False):
-    """relu(x W^T) for the width-512 hidden layers on the HIP MFMA kernel
-    (csrc/linear_fwd.hip), or None when the shape is not its (16-bit, K = 512,
-    N a multiple of 32).  W is packed into MFMA-fragment order
-    (avr_linear_pack_w), cached on the master weight like its cast."""
-    if not (_LINEAR_HIP and x.is_cuda and x.dtype in (torch.float16, torch.bfloat16) and w.dtype == x.dtype
-            and x.dim() == 2 and x.size(1) == 512 and w.size(1) == 512 and w.size(0) % 32 == 0
-            and x.is_contiguous() and w.is_contiguous() and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0):
-        return None
+def _mlp512x2_ok(x, lin1, lin2, dtype):
+    return (_MLP512X2 and x.is_cuda and not torch.is_grad_enabled() and dtype in (torch.float16, torch.bfloat16)
+            and x.dim() == 2 and x.size(1) == 512 and tuple(lin1.weight.shape) == (512, 512)
+            and tuple(lin2.weight.shape) == (512, 512) and x.size(0) >= 1)
+
+
+def _mlp512x2(x, w1_master, w2_master, dtype):
+    """relu(relu(x W1^T) W2^T) for x [M, 512] on csrc/mlp512.hip.  The packed
+    weights are cached on W1's master weight, keyed by both weights' storage
+    and versions (bypassed while a HIP graph is captured, wcache.capturing)."""
     import ctypes
 
     from . import _lib
-    from .wcache import cache_lookup, cache_store, capturing
 
-    M, N = x.size(0), w.size(0)
-    y = torch.empty(M, N, dtype=x.dtype, device=x.device)
-    if M == 0:
-        return y
-    code = _lib.DTYPE_F16 if x.dtype == torch.float16 else _lib.DTYPE_BF16
+    x = x.to(dtype).contiguous()
+    code = _lib.DTYPE_F16 if dtype == torch.float16 else _lib.DTYPE_BF16
     st = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
-    owner = w_master if w_master is not None else w
-    key = (w.data_ptr(), owner._version, code)
-    use_cache = cache and not capturing()
-    wf = cache_lookup(owner, "_avr_linpack", key) if use_cache else None
+    key = (w1_master.data_ptr(), w1_master._version, w2_master.data_ptr(), w2_master._version, code)
+    use_cache = not capturing()
+    wf = cache_lookup(w1_master, "_avr_mlp512x2", key) if use_cache else None
     if wf is None:
-        wf = torch.empty_like(w)
-        _lib.call("avr_linear_pack_w", N, 512, ctypes.c_void_p(w.data_ptr()), code, ctypes.c_void_p(wf.data_ptr()), st)
+        w1 = cast_weight(w1_master, dtype, use_cache).contiguous()
+        w2 = cast_weight(w2_master, dtype, use_cache).contiguous()
+        wf = torch.empty(2, 512, 512, dtype=dtype, device=x.device)
+        _lib.call("avr_mlp512x2_pack_w", ctypes.c_void_p(w1.data_ptr()), ctypes.c_void_p(w2.data_ptr()), code,
+                  ctypes.c_void_p(wf.data_ptr()), st)
         if use_cache:
-            cache_store(owner, "_avr_linpack", key, wf)
-    _lib.call("avr_linear_relu_fwd", M, N, 512, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(wf.data_ptr()),
-              code, 1, ctypes.c_void_p(y.data_ptr()), st)
+            cache_store(w1_master, "_avr_mlp512x2", key, wf)
+    y = torch.empty_like(x)
+    _lib.call("avr_mlp512x2_fwd", x.size(0), ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(wf.data_ptr()), code,
+              ctypes.c_void_p(y.data_ptr()), st)
     return y
 
 
@@ -255,26 +256,22 @@ def _tuned_gemm(x, w):
 class _LinearReLU(torch.autograd.Function):
     """y = relu(x W^T) with the ReLU in the GEMM epilogue: hipBLASLt's
     `_addmm_activation` with a zero bias (one kernel instead of GEMM + an
-    elementwise pass over the [N, width] activation, bit-identical output),
-    or with AVR_LINEAR=1 the HIP MFMA kernel for the width-512 layers
-    (`_linear_relu_hip`, bit-identical to hipBLASLt on the probe).
+    elementwise pass over the [N, width] activation, bit-identical output).
     The backward is ReLU's own (threshold on the saved output), then the
     same data / weight gradients as `_Linear`."""
 
     @staticmethod
     def forward(ctx, x, w_master, dtype, cache=False):
         w = cast_weight(w_master, dtype, cache)
-        y = _linear_relu_hip(x, w, w_master, cache) if x.is_cuda else None
-        if y is None:
-            if x.is_cuda:
-                bias = _zero_bias(w.size(0), dtype, x.device)
-                if _tuned_gemm(x, w):
-                    with _tuned_window():
-                        y = torch._addmm_activation(bias, x, w.t(), use_gelu=False)
-                else:
+        if x.is_cuda:
+            bias = _zero_bias(w.size(0), dtype, x.device)
+            if _tuned_gemm(x, w):
+                with _tuned_window():
                     y = torch._addmm_activation(bias, x, w.t(), use_gelu=False)
             else:
-                y = torch.relu(x @ w.t())
+                y = torch._addmm_activation(bias, x, w.t(), use_gelu=False)
+        else:
+            y = torch.relu(x @ w.t())
         ctx.save_for_backward(x, w, y)
         return y
 
@@ -312,10 +309,18 @@ class MLP(nn.Module):
 
     def hidden_from(self, x, start):
         """Hidden layers start .. n-2 (each followed by ReLU) on x, the
-        rectified output of layer start-1."""
+        rectified output of layer start-1; at inference two 512 -> 512
+        layers at a time in one launch (`_mlp512x2`)."""
         x = x.to(self.dtype).contiguous()
-        for lin in self.layers[start:-1]:
-            x = _LinearReLU.apply(x, lin.weight, self.dtype, not torch.is_grad_enabled())
+        hid = list(self.layers[start:-1])
+        i = 0
+        while i < len(hid):
+            if i + 1 < len(hid) and _mlp512x2_ok(x, hid[i], hid[i + 1], self.dtype):
+                x = _mlp512x2(x, hid[i].weight, hid[i + 1].weight, self.dtype)
+                i += 2
+                continue
+            x = _LinearReLU.apply(x, hid[i].weight, self.dtype, not torch.is_grad_enabled())
+            i += 1
         return x
 
     def last(self, h):

@@ -299,15 +299,16 @@ int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const float* x, co
  * avr_runner.py:190).  Split-K over n: `workspace` holds splits*M*K fp32
  * partials (splits from avr_linear_wgrad_splits), summed deterministically. */
 int avr_linear_wgrad_splits(int64_t N, int32_t M, int32_t K, int32_t* splits);
-/* y = relu(x W^T) (relu != 0) or x W^T: x [M, K] and W [N, K] (nn.Linear
- * layout) 16-bit (dtype fp16 / bf16), y [M, N] of the same type, fp32
- * accumulation and one rounding.  K = 512, N a multiple of 32 (the signal
- * network's hidden layers, model.py:176-180).  avr_linear_pack_w packs W
- * into Wf (N*K 16-bit values, MFMA fragment order; once per weight update);
- * x, Wf and y 16-byte aligned (csrc/linear_fwd.hip). */
-int avr_linear_pack_w(int32_t N, int32_t K, const void* W, int32_t dtype, void* Wf, void* stream);
-int avr_linear_relu_fwd(int64_t M, int32_t N, int32_t K, const void* x, const void* Wf, int32_t dtype,
-                        int32_t relu, void* y, void* stream);
+/* Two consecutive width-512 hidden layers of the signal network in one
+ * launch (model.py:176-180, AVRModel's `_model_signal` layers 1 and 2 at
+ * inference): y = relu(relu(x W1^T) W2^T), x / y [M][512], W1 / W2 [512][512]
+ * (nn.Linear layout), all 16-bit (dtype fp16 / bf16); each layer fp32
+ * accumulation over k in order and one rounding, the intermediate activation
+ * kept on chip.  avr_mlp512x2_pack_w packs both weights into Wf (2 * 512 * 512
+ * 16-bit values; once per weight update); x, W1, W2, Wf, y 16-byte aligned
+ * (csrc/mlp512.hip). */
+int avr_mlp512x2_pack_w(const void* W1, const void* W2, int32_t dtype, void* Wf, void* stream);
+int avr_mlp512x2_fwd(int64_t M, const void* x, const void* Wf, int32_t dtype, void* y, void* stream);
 int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* grad_y, const void* x,
                      float* workspace, int32_t splits, float* grad_w, void* stream);
 
