@@ -749,6 +749,271 @@ __global__ __launch_bounds__(256) void head_pack_exact_kernel(int T, int K, int 
     }
 }
 
+// ---- AVR_EXACT_V2 (compile-time, off): one wave per SIMD and 64 rays per
+// wave as two 32-ray A tiles (256 registers), so that every B fragment read
+// from the ring feeds two MFMAs: half the ring reads per MFMA of the 8-wave
+// form, whose per-tile LDS traffic (eight waves reading the whole 64 KiB
+// tile, plus its DMA) is the suspected limiter.  With one
+// wave per SIMD nothing else fills the matrix pipe during an epilogue, so
+// each chain carries the previous chain's epilogue, one value per k-step,
+// between its MFMAs; a tile's partials are complete one barrier later
+// (three partial buffers).  K = 512 only (rows by LDS-DMA), 64-t tiles, a
+// two-tile ring, the next tile's DMA inside the tile's first chain.
+#ifndef AVR_EXACT_V2
+#define AVR_EXACT_V2 0
+#endif
+
+__host__ __device__ constexpr size_t xs2_lds_bytes(int T) {
+    return 2 * (size_t)65536 + 4 * (size_t)((T + 3) / 4 * 4) + 4 * 256 + 4 * 3 * 4 * 64 + 4 * 8 + 8;
+}
+
+template <typename E>
+__global__ __launch_bounds__(256, 1) void head_exact2_kernel(
+    avr_render_params pp, int B, int R, int K, const E* __restrict__ h, const frag8* __restrict__ Wf,
+    const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
+    const int32_t* __restrict__ delay, float* __restrict__ zpart, int* __restrict__ queue, int nitems) {
+    constexpr int KSM = 32, WAVES = 4, NT = 256, RAYS = 256, RPW = 64, TT = 64, TILE = 65536, NBUF = 3;
+    constexpr int DPW = 2 * KSM / WAVES;  // W pieces (1 KiB) per wave and tile
+    extern __shared__ __attribute__((aligned(16))) char lds_x[];
+    const int T = pp.T, S = pp.n_samples;
+    const int Tp = (T + 3) & ~3;
+    char* ring = lds_x;                                                // [2][TILE]
+    int* cl = reinterpret_cast<int*>(lds_x + 2 * TILE);                // cnt of the column [Tp]
+    float* wl = reinterpret_cast<float*>(cl + Tp);                     // weights of the item's rays [RAYS]
+    float* zr = wl + RAYS;                                             // wave partials [NBUF][WAVES][TT]
+    int* dstart = reinterpret_cast<int*>(zr + NBUF * WAVES * TT);      // first live t per A tile [WAVES][2]
+    int* qnext = dstart + 2 * WAVES;                                   // claimed items [2]
+
+    const int64_t ncol = (int64_t)B * S;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
+    const int qx = blockIdx.x & 7, gq = gridDim.x >> 3, ql = blockIdx.x >> 3;
+    int* qctr = queue + 32 * qx;
+    auto item_of = [&](int claim) { return qx + 8 * claim; };
+
+    constexpr int CLN = kExactMaxT[0] / NT;
+    struct Meta {
+        int item, nk, ray0, ray1, dly0, dly1;
+        int clv[CLN];
+        float wsv;
+    };
+    auto load_meta = [&](int item, Meta& m) {
+        const int tid = opaque_tid();
+        m.item = item;
+        const int it = min(item, nitems - 1);
+        const int64_t col = (int64_t)it % ncol;
+        const int blk = (int)((int64_t)it / ncol);
+        const int* cc = cnt + col * T;
+        m.nk = cc[T - 1 - (tid >> 12)];
+        const int pb = blk * RAYS + RPW * wave + (tid & 31);
+        m.ray0 = perm[col * R + min(pb, R - 1)];
+        m.ray1 = perm[col * R + min(pb + 32, R - 1)];
+#pragma unroll
+        for (int u = 0; u < CLN; ++u) m.clv[u] = cc[min(tid + NT * u, T - 1)];
+        m.wsv = ws[col * R + min(blk * RAYS + tid, R - 1)];
+    };
+    auto load_dly = [&](Meta& m) {
+        const int it = min(m.item, nitems - 1);
+        const int64_t col = (int64_t)it % ncol;
+        const int s = (int)(col % S), b = (int)(col / S);
+        m.dly0 = delay[((int64_t)b * R + m.ray0) * S + s];
+        m.dly1 = delay[((int64_t)b * R + m.ray1) * S + s];
+    };
+    auto touch = [&](Meta& m) {
+        asm volatile("" ::"v"(m.nk), "v"(m.ray0), "v"(m.ray1), "v"(m.dly0), "v"(m.dly1), "v"(m.wsv));
+#pragma unroll
+        for (int u = 0; u < CLN; ++u) asm volatile("" ::"v"(m.clv[u]));
+    };
+
+    Meta cur, nx;
+    int claim = 0;
+    int item = item_of(ql), nxt = item_of(gq + ql);
+    load_meta(item, cur);
+    load_dly(cur);
+    if (threadIdx.x == 0) qnext[1] = item_of(2 * gq + ql);
+    __syncthreads();
+    for (int iter = 0; item < nitems; ++iter) {
+        const int tid = opaque_tid();
+        const int lane = tid & 63, half = lane >> 5, j = lane & 31;
+        const int col = item % (int)ncol;
+        const int blk = item / (int)ncol;
+        const int s = col % S, b = col / S;
+        const int lim = tail_limit(pp, s);
+        float* zc = zpart + ((int64_t)blk * ncol + col) * T;
+        const int p0 = blk * RAYS;
+        const int pw = p0 + RPW * wave;
+        const int nk = __builtin_amdgcn_readfirstlane(cur.nk);
+        if (tid == 0) {
+            int zero = 0;
+            asm volatile("" : "+v"(zero));
+            claim = __hip_atomic_fetch_add(qctr + zero, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bool dly_issued = false, touched = false, published = false;
+        if (p0 >= nk || lim <= 0) {
+            load_meta(nxt, nx);
+            for (int t = tid; t < T; t += NT) zc[t] = 0.0f;
+            load_dly(nx);
+            dly_issued = true;
+        } else {
+            // ---- prologue: the wave's 64 rows, two A tiles, by LDS-DMA
+            frag8 a[2][KSM];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+#pragma unroll
+                for (int ks = 0; ks < KSM; ++ks) a[q][ks] = frag8{0u, 0u, 0u, 0u};
+                const E* hrow = h + (((int64_t)b * R + (q ? cur.ray1 : cur.ray0)) * S + s) * K;
+                stat_load_rows512(reinterpret_cast<frag8_t(&)[32]>(a[q]), reinterpret_cast<const uint16_t*>(hrow),
+                                  ring + wave * 16384);
+            }
+#pragma unroll
+            for (int u = 0; u < CLN; ++u) {
+                const int t = tid + NT * u;
+                if (t < T) cl[t] = cur.clv[u];
+            }
+            wl[tid] = p0 + tid < nk ? cur.wsv : 0.0f;
+            if (lane == 0) {
+                dstart[2 * wave] = pw < nk ? cur.dly0 : 1 << 30;
+                dstart[2 * wave + 1] = pw + 32 < nk ? cur.dly1 : 1 << 30;
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_s_barrier();
+            const int tb = dstart[0] / TT;
+            const int te = (lim + TT - 1) / TT;
+            const int d0 = __builtin_amdgcn_readfirstlane(dstart[2 * wave]);
+            const int d1 = __builtin_amdgcn_readfirstlane(dstart[2 * wave + 1]);
+            // tile tb into slot 0, this wave's pieces
+            if (tb < te) {
+                const char* src = reinterpret_cast<const char*>(Wf) + (int64_t)tb * TILE + wave * DPW * 1024 + 16 * lane;
+                const uint32_t dst = ring_lds + wave * DPW * 1024;
+                for (int d = 0; d < DPW; ++d) dma_row16(src + d * 1024, dst + d * 1024);
+            }
+            load_meta(nxt, nx);
+            AVR_VMCNT(CLN + 4);  // the first tile (and the older claim) landed; the metadata may fly
+            if (tid == 0) {
+                qnext[iter & 1] = item_of(3 * gq + claim);
+                published = true;
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_s_barrier();
+
+            const float* wq = wl + RPW * wave + 4 * half;
+            const int pos0 = pw + 4 * half;
+            // one chain: the wave's NM (0, 1 or 2) A tiles against 32-t group c
+            // of the tile in `slot` (B read once for both), the DMA pieces of
+            // tile dtile (if >= 0) one every two k-steps, and the epilogue of
+            // the previous chain's accumulators (q0, q1 at t0 = pt0; none if
+            // pt0 < 0), one value per k-step: returns its per-lane sum
+            auto chain = [&](auto NM, int slot, int c, int dtile, int dslot, const f32x16& q0, const f32x16& q1,
+                             int pt0, f32x16& n0, f32x16& n1) {
+                constexpr int nm = decltype(NM)::value;
+                constexpr int D = 4;
+                const char* bsrc = ring + slot * TILE + c * xs_tile_bytes(KSM) + 16 * lane;
+                const int pt = pt0 + j;
+                const int ct = (pt0 >= 0 && pt < lim) ? cl[min(pt, T - 1)] : 0;
+                const char* dsrc = reinterpret_cast<const char*>(Wf) + (int64_t)dtile * TILE + wave * DPW * 1024 +
+                                   16 * lane;
+                const uint32_t ddst = ring_lds + dslot * TILE + wave * DPW * 1024;
+                frag8 bw[D];
+                if constexpr (nm > 0) {
+#pragma unroll
+                    for (int u = 0; u < D; ++u) bw[u] = *reinterpret_cast<const frag8*>(bsrc + u * 1024);
+                }
+                n0 = f32x16{};
+                n1 = f32x16{};
+                float z = 0.0f;
+                float4 w4 = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int ks = 0; ks < KSM; ++ks) {
+                    if constexpr (nm > 0) n0 = mfma16<E>(a[0][ks], bw[ks % D], n0);
+                    if constexpr (nm > 1) n1 = mfma16<E>(a[1][ks], bw[ks % D], n1);
+                    if constexpr (nm > 0)
+                        if (ks + D < KSM) bw[ks % D] = *reinterpret_cast<const frag8*>(bsrc + (ks + D) * 1024);
+                    if (ks % 2 == 0 && dtile >= 0) dma_row16(dsrc + (ks / 2) * 1024, ddst + (ks / 2) * 1024);
+                    // value r of A tile rt: ray pos0 + 32 rt + 8 (r >> 2) + (r & 3)
+                    const int rt = ks >> 4, r = ks & 15, e = r & 3;
+                    if (e == 0) w4 = *reinterpret_cast<const float4*>(wq + 32 * rt + 8 * (r >> 2));
+                    const float wv = e == 0 ? w4.x : (e == 1 ? w4.y : (e == 2 ? w4.z : w4.w));
+                    const float v = round16<E>(rt ? q1[r] : q0[r]);
+                    z = fmaf(wv, (pos0 + 32 * rt + 8 * (r >> 2) + e < ct) ? v : 0.0f, z);
+                }
+                return z;
+            };
+            auto put = [&](float zlc, int buf, int c) {
+                const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zlc), __float_as_uint(zlc), false,
+                                                                false);
+                const float v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+                if (half == 0) zr[buf * (WAVES * TT) + wave * TT + 32 * c + j] = v;
+            };
+            auto sum_tile = [&](int tau, int buf) {
+                const float* zz = zr + buf * (WAVES * TT) + lane;
+                float v = zz[0];
+#pragma unroll
+                for (int w = 1; w < WAVES; ++w) v += zz[TT * w];
+                const int t = TT * tau + lane;
+                if (t < T) zc[t] = v;
+            };
+            f32x16 q0 = f32x16{}, q1 = f32x16{};
+            int qt = -1, qbuf = 0;  // the pending chain's t0 and partial buffer
+            for (int tau = tb; tau < te; ++tau) {
+                const int i = tau - tb;
+                const int dtile = tau + 1 < te ? tau + 1 : -1;
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int t0 = TT * tau + 32 * c;
+                    const bool live0 = t0 + 31 >= d0 && t0 < lim, live1 = t0 + 31 >= d1 && t0 < lim;
+                    const int dt = c == 0 ? dtile : -1;
+                    f32x16 n0, n1;
+                    float zp;
+                    if (live1)
+                        zp = chain(std::integral_constant<int, 2>{}, i & 1, c, dt, (i + 1) & 1, q0, q1, qt, n0, n1);
+                    else if (live0)
+                        zp = chain(std::integral_constant<int, 1>{}, i & 1, c, dt, (i + 1) & 1, q0, q1, qt, n0, n1);
+                    else
+                        zp = chain(std::integral_constant<int, 0>{}, i & 1, c, dt, (i + 1) & 1, q0, q1, qt, n0, n1);
+                    if (qt >= 0) put(zp, qbuf, c ^ 1);
+                    q0 = n0;
+                    q1 = n1;
+                    qt = t0;
+                    qbuf = i % NBUF;
+                }
+                if (dtile >= 0) AVR_VMCNT(0);  // this wave's pieces of the next tile landed
+                if (i == min(1, te - 1 - tb)) {
+                    load_dly(nx);
+                    dly_issued = true;
+                }
+                if (tau == te - 1) {
+                    touch(nx);
+                    touched = true;
+                }
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_s_barrier();
+                // tile i - 1's partials are complete (its second chain's
+                // epilogue ran in tile i's first chain)
+                if (i >= 1 && wave == (i - 1) % WAVES) sum_tile(tau - 1, (i - 1) % NBUF);
+            }
+            if (te > tb) {
+                // the last chain's epilogue, then the last tile's sum
+                const int n = te - tb;
+                f32x16 n0, n1;
+                const float zp = chain(std::integral_constant<int, 0>{}, 0, 0, -1, 0, q0, q1, qt, n0, n1);
+                put(zp, qbuf, 1);
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_s_barrier();
+                if (wave == (n - 1) % WAVES) sum_tile(te - 1, (n - 1) % NBUF);
+            }
+            for (int t = tid; t < T; t += NT)
+                if (t < TT * tb || t >= TT * te) zc[t] = 0.0f;
+        }
+        if (!dly_issued) load_dly(nx);
+        if (!touched) touch(nx);
+        if (tid == 0 && !published) qnext[iter & 1] = item_of(3 * gq + claim);
+        if (p0 >= nk || lim <= 0) __syncthreads();
+        item = nxt;
+        nxt = qnext[(iter + 1) & 1];
+        cur = nx;
+    }
+}
+
 constexpr int kExactQueueInts = 256;  // 8 work-queue counters, one 128-byte line each
 
 int exact_ksm(int K) { return K <= 128 ? 8 : (K <= 256 ? 16 : 32); }
@@ -791,7 +1056,8 @@ size_t exact_lds(int R, int T, int K) {
     const int KSM = exact_ksm(K);
     const ExactShape sh = exact_shape(R, T, K);
     if (sh.rays == 128) return xs_lds_bytes(KSM, T, 4, 128, 2, 1);
-    if ((AVR_EXACT_FLAGS || AVR_EXACT_NC1) && K == 512) return xs_lds_bytes(KSM, T, 8, 256, 4, 1);
+    if (AVR_EXACT_V2 != 0 && K == 512) return xs2_lds_bytes(T);
+    if ((AVR_EXACT_FLAGS != 0 || AVR_EXACT_NC1 != 0) && K == 512) return xs_lds_bytes(KSM, T, 8, 256, 4, 1);
     if (sh.tt64) return xs_lds_bytes(KSM, T, 8, 256, 2, 2);
     return xs_lds_bytes(KSM, T, 8, 256, 4, 1);
 }
@@ -902,7 +1168,18 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
             else if (KSM == 16) go(head_exact_kernel<E, 16, 4, 128, 2, 1, false>, 16, 4, 128, 2, 1, h);
             else if (rowdma) go(head_exact_kernel<E, 32, 4, 128, 2, 1, true>, 32, 4, 128, 2, 1, h);
             else go(head_exact_kernel<E, 32, 4, 128, 2, 1, false>, 32, 4, 128, 2, 1, h);
-        } else if ((AVR_EXACT_FLAGS || AVR_EXACT_NC1) && rowdma) {
+#if AVR_EXACT_V2
+        } else if (rowdma) {
+            auto kern = head_exact2_kernel<E>;
+            const size_t lds = xs2_lds_bytes(T);
+            allow_lds(kern, lds);
+            const int64_t gq = std::min<int64_t>((int64_t)device_cus() / 8, (items + 7) / 8);
+            const int grid = 8 * (int)std::max<int64_t>(gq, 1);
+            (void)hipMemsetAsync(queue, 0, kExactQueueInts * sizeof(int32_t), st);
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, *p, (int)B, R, (int)K, (const E*)h,
+                               (const frag8*)Wf, perm, ws, cnt, delay, zpart, (int*)queue, (int)items);
+#endif
+        } else if ((AVR_EXACT_FLAGS != 0 || AVR_EXACT_NC1 != 0) && rowdma) {
             go(head_exact_kernel<E, 32, 8, 256, 4, 1, true>, 32, 8, 256, 4, 1, h);
         } else if (tt64 && rowdma) {
             go(head_exact_kernel<E, 32, 8, 256, 2, 2, true>, 32, 8, 256, 2, 2, h);

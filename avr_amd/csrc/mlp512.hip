@@ -41,6 +41,37 @@ using namespace avr;
 
 namespace {
 
+// Compile-time variants (tools/xbench_mlp.py; the defaults are the product):
+// AVR_MLP_DMA 1: the W ring filled by LDS-DMA (global_load_lds_dwordx4) a
+// whole pair ahead instead of register staging; AVR_MLP_DBG (timing probes,
+// wrong results): bit 0 no W staging, bit 1 no barrier, bit 2 no y stores
+// (skipped at run time), bit 3 no layer-1 epilogue (raw accumulator bits).
+#ifndef AVR_MLP_DMA
+#define AVR_MLP_DMA 0
+#endif
+#ifndef AVR_MLP_DBG
+#define AVR_MLP_DBG 0
+#endif
+// AVR_MLP_TSTORE 1: y leaves through a per-wave LDS transpose as whole
+// 128-byte lines (else each store instruction writes 32 B into 32 rows)
+// AVR_MLP_SCHED 1: the pair's MFMA / ring-read order pinned by sched_group_barrier
+#ifndef AVR_MLP_SCHED
+#define AVR_MLP_SCHED 0
+#endif
+#ifndef AVR_MLP_TSTORE
+#define AVR_MLP_TSTORE 0
+#endif
+
+// s_waitcnt vmcnt(n) (gfx9 encoding; expcnt / lgkmcnt not waited on)
+#define AVR_MLP_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 0xF) | (0x7 << 4) | (0xF << 8) | (((N) >> 4) << 14))
+
+// lane i's 16 bytes at sbase + voff land at LDS byte lds + 16 i (scalar base,
+// 32-bit lane offset: one VGPR for every piece)
+__device__ __forceinline__ void mlp_dma16(const void* sbase, uint32_t voff, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds), "v"(voff), "s"(sbase)
+                 : "memory");
+}
+
 // workgroup barrier that waits for the LDS traffic only: the W staging
 // loads and y stores in flight are not waited for (the compiler waits for a
 // load where its registers are used); "memory" keeps LDS accesses on their side
@@ -107,6 +138,13 @@ __global__ __launch_bounds__(256, 1) void mlp512x2_kernel(int64_t M, const E* __
 #pragma unroll
         for (int i = 0; i < kMShare / 2; ++i) stg[i] = src[i * 64];
     };
+    // LDS-DMA form: this wave's 16 pieces of pair p into ring slot `slot`
+    auto dma_pair = [&](int p, int slot) {
+        const char* src = reinterpret_cast<const char*>(Wf) + (int64_t)p * kMPair + kMShare * wave * 1024;
+        const uint32_t dst = (uint32_t)(uintptr_t)(lds_m + slot * kMPair) + kMShare * wave * 1024;
+#pragma unroll
+        for (int i = 0; i < kMShare; ++i) mlp_dma16(src + i * 1024, 16 * lane, dst + i * 1024);
+    };
     auto write_half = [&](int slot, int h) {
         frag8* dst = reinterpret_cast<frag8*>(lds_m + slot * kMPair) + (kMShare * wave + 8 * h) * 64 + lane;
 #pragma unroll
@@ -126,21 +164,54 @@ __global__ __launch_bounds__(256, 1) void mlp512x2_kernel(int64_t M, const E* __
         const int64_t nrows = std::min<int64_t>(kMRows, M - r0);
         const __amdgpu_buffer_rsrc_t yres =
             __builtin_amdgcn_make_buffer_rsrc((void*)(y + r0 * kMK), (short)0, (int)(nrows * kMK * 2), 0x00020000);
-        const int rl = 32 * wave + j;
+        const bool st_on = !(AVR_MLP_DBG & 4) || M < 0;  // (DBG 4: stores skipped at run time)
+        if constexpr (AVR_MLP_TSTORE) {
+            // through this wave's 4 KiB of LDS, two tiles (64 columns) at a
+            // time: written as the fragments lie (row j, 16-byte chunk
+            // 4 (n & 1) + 2 pp + half, XOR-swizzled by row), read back as
+            // 8 rows x 128 contiguous bytes per instruction (whole lines)
+            char* tr = lds_m + 2 * kMPair + wave * 4096;
 #pragma unroll
-        for (int n = 0; n < kMN; ++n) {
-            frag8 f[2];
-            epilogue<E>(acc2[n], f);
+            for (int m = 0; m < kMN / 2; ++m) {
 #pragma unroll
-            for (int pp = 0; pp < 2; ++pp)
-                __builtin_amdgcn_raw_buffer_store_b128(f[pp], yres, (rl * kMK + 32 * n + 16 * pp + 8 * half) * 2, 0, 0);
+                for (int u = 0; u < 2; ++u) {
+                    frag8 f[2];
+                    epilogue<E>(acc2[2 * m + u], f);
+#pragma unroll
+                    for (int pp = 0; pp < 2; ++pp)
+                        *reinterpret_cast<frag8*>(tr + j * 128 + (((4 * u + 2 * pp + half) ^ (j & 7)) * 16)) = f[pp];
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int row = 8 * q + (lane >> 3), ch = lane & 7;
+                    const frag8 v = *reinterpret_cast<const frag8*>(tr + row * 128 + ((ch ^ (row & 7)) * 16));
+                    if (st_on)
+                        __builtin_amdgcn_raw_buffer_store_b128(v, yres, ((32 * wave + row) * kMK + 64 * m + 8 * ch) * 2,
+                                                               0, 0);
+                }
+            }
+        } else {
+            const int rl = 32 * wave + j;
+#pragma unroll
+            for (int n = 0; n < kMN; ++n) {
+                frag8 f[2];
+                epilogue<E>(acc2[n], f);
+#pragma unroll
+                for (int pp = 0; pp < 2; ++pp)
+                    if (st_on)
+                        __builtin_amdgcn_raw_buffer_store_b128(f[pp], yres,
+                                                               (rl * kMK + 32 * n + 16 * pp + 8 * half) * 2, 0, 0);
+            }
         }
     };
     // The 64 MFMAs of a pair, layer 1's tile and layer 2's slice alternating
     // (s even: layer-1 k-step s / 2, piece s / 2; s odd: layer-2 column
     // tile n = (s - 1) / 4, k-step (s - 1) / 2 % 2, piece 32 + (s - 1) / 2),
     // the W fragments read D ahead in that order.  `mid` runs at the middle.
-    constexpr int D = 6;  // (8 spills a few registers)
+#ifndef AVR_MLP_D
+#define AVR_MLP_D 6
+#endif
+    constexpr int D = AVR_MLP_D;  // (8 spills a few registers)
     auto piece = [](int st) { return (st & 1) ? kMKS + (st >> 1) : (st >> 1); };
     auto run_pair = [&](const frag8* ring, f32x16& acc1, bool t1, auto&& mid) {
         frag8 bw[D];
@@ -155,16 +226,28 @@ __global__ __launch_bounds__(256, 1) void mlp512x2_kernel(int64_t M, const E* __
                 acc2[i >> 1] = mma<E>(bw[st % D], bx[i & 1], acc2[i >> 1]);
             }
             if (st + D < 2 * kMKS) bw[st % D] = ring[piece(st + D) * 64];
+#if AVR_MLP_SCHED
+            // issue order pinned: this step's MFMA, then the read D steps
+            // ahead (left to itself the scheduler issues each read just
+            // before its MFMA, two or three reads of lead)
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if (st + D < 2 * kMKS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#endif
             if (st == kMKS - 1) mid();
         }
     };
 
     load_rows(blockIdx.x);
-    load_half(0, 0);
-    write_half(0, 0);
-    load_half(0, 1);
-    write_half(0, 1);
-    load_half(1, 0);
+    if constexpr (AVR_MLP_DMA) {
+        dma_pair(0, 0);
+        AVR_MLP_VMCNT(0);
+    } else {
+        load_half(0, 0);
+        write_half(0, 0);
+        load_half(0, 1);
+        write_half(0, 1);
+        load_half(1, 0);
+    }
     lds_barrier();
 #pragma unroll
     for (int n = 0; n < kMN; ++n) acc2[n] = f32x16{};
@@ -179,26 +262,59 @@ __global__ __launch_bounds__(256, 1) void mlp512x2_kernel(int64_t M, const E* __
             // pair q + 1: first half written now (loaded during pair q - 1),
             // second half loaded now and written mid-pair; pair q + 2's first
             // half loaded after that
-            write_half(slot1, 0);
-            load_half((c + 1) % kMN, 1);
+            if constexpr (AVR_MLP_DMA) {
+                // nothing of this wave's in flight on the vector-memory counter
+                // (the previous pair's pieces were waited for; the rows and y
+                // stores here): the compiler, which cannot count the DMA
+                // below, then waits for nothing inside the pair
+                AVR_MLP_VMCNT(0);
+                if (!(AVR_MLP_DBG & 1)) dma_pair((c + 1) % kMN, slot1);
+            } else if (!(AVR_MLP_DBG & 1)) {
+                write_half(slot1, 0);
+                load_half((c + 1) % kMN, 1);
+            }
             f32x16 acc1 = f32x16{};
             run_pair(ring, acc1, true, [&] {
-                write_half(slot1, 1);
-                load_half((c + 2) % kMN, 0);
+                if constexpr (!AVR_MLP_DMA && !(AVR_MLP_DBG & 1)) {
+                    write_half(slot1, 1);
+                    load_half((c + 2) % kMN, 0);
+                } else {
+                    asm volatile("" ::: "memory");  // (the two halves scheduled apart, as with staging)
+                }
             });
             if (c == 0 && prev >= 0) {
                 store_out(prev);
 #pragma unroll
                 for (int n = 0; n < kMN; ++n) acc2[n] = f32x16{};
             }
-            epilogue<E>(acc1, bx);
+            if constexpr (AVR_MLP_DBG & 8) {  // (timing probe: the raw accumulator bits)
+                bx[0] = frag8{__float_as_uint(acc1[0]), __float_as_uint(acc1[1]), __float_as_uint(acc1[2]),
+                              __float_as_uint(acc1[3])};
+                bx[1] = frag8{__float_as_uint(acc1[4]), __float_as_uint(acc1[5]), __float_as_uint(acc1[6]),
+                              __float_as_uint(acc1[7])};
+            } else {
+                epilogue<E>(acc1, bx);
+            }
             if (c == kMN - 1) {
                 // the last use of this item's rows was tile 15: the next item's
                 const int nxt = it + G;
+                // (not scheduled into the pair above: both items' rows live
+                // at once would not fit the register file)
+                __builtin_amdgcn_sched_barrier(0);
                 if (nxt < nitems) load_rows(nxt);
                 prev = it;
             }
-            lds_barrier();
+            if constexpr (AVR_MLP_DMA) {
+                // this wave's pieces of pair q + 1 landed: younger are the y
+                // stores of pair 0 and the next item's row loads of pair 15
+                const int young = (c == 0 && prev >= 0 && !(AVR_MLP_DBG & 4) ? 2 * kMN : 0) +
+                                  (c == kMN - 1 && it + G < nitems ? kMKS : 0);
+                if (young == 0) AVR_MLP_VMCNT(0);
+                else if (young == 2 * kMN) AVR_MLP_VMCNT(2 * kMN);
+                else if (young == kMKS) AVR_MLP_VMCNT(kMKS);
+                else AVR_MLP_VMCNT(2 * kMN + kMKS);
+            }
+            if (!(AVR_MLP_DBG & 2)) lds_barrier();
         }
     }
     // layer 2's slice 15 of the last item: the second half of pair 0
@@ -257,7 +373,7 @@ extern "C" int avr_mlp512x2_fwd(int64_t M, const void* x, const void* Wf, int32_
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int grid = (int)std::min<int64_t>(items, std::max(cus, 1));
-    const size_t lds = 2 * (size_t)kMPair;
+    const size_t lds = 2 * (size_t)kMPair + (AVR_MLP_TSTORE ? 4 * 4096 : 0);
     hipStream_t st = as_stream(stream);
     auto go = [&](auto e_tag) {
         using E = decltype(e_tag);

@@ -206,3 +206,32 @@ def test_sigma_timing_experiments_not_in_shipped_library():
     for cfg in (16, 20, 9, -1):
         with pytest.raises(RuntimeError, match="tile_cfg"):
             sigma.sigma_fwd(sigma.MESHRIR_H1, packed, N, inputs, [], 512, 0.01, tile_cfg=cfg, bias=bias, bias_div=S)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("variant", [sigma.MESHRIR, sigma.RAF, sigma.MESHRIR_H1])
+def test_sigma_repeat_bitwise(variant, dtype):
+    """Five launches of every shipped tiling on the same 262,144 samples give
+    the same bits: the compiled schedules rewrite MFMA B operands by VALU at 0
+    wait states behind a queued MFMA (tools/isa_mfma_audit.py),
+    the pattern of the round-4 bf16x3 DFT whose B-lane corruption showed as
+    run-to-run differences."""
+    N, S = 262144, 256
+    g = torch.Generator(device=DEV).manual_seed(9)
+    base_v = sigma.MESHRIR if variant == sigma.MESHRIR_H1 else variant
+    ws = _weights(variant, 3)
+    inputs, extras = _sources(base_v, N, S, N, 4)
+    slope = 0.03 if variant == sigma.RAF else 0.01
+    packed = sigma.pack_layers(variant, ws, dtype)
+    kw = {}
+    if variant == sigma.MESHRIR_H1:
+        extras, out_w = [], 512
+        kw = dict(bias=torch.randn(N // S, 512, device=DEV, generator=g) * 0.3, bias_div=S)
+    else:
+        out_w = 128 if variant == sigma.MESHRIR else 256
+    for cfg in range(9):
+        outs = [sigma.sigma_fwd(variant, packed, N, inputs, extras, out_w, slope, tile_cfg=cfg, **kw)
+                for _ in range(5)]
+        torch.cuda.synchronize()
+        for attn, base in outs[1:]:
+            assert torch.equal(attn, outs[0][0]) and torch.equal(base, outs[0][1]), f"cfg {cfg}"

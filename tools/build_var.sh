@@ -11,7 +11,7 @@ mkdir -p $ROOT/tools/_lib /tmp/avr_var_$NAME
 FLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -fno-gpu-rdc -Wall -Wno-unused-function -Wno-inline-asm -I$ROOT/include"
 OBJS=""
 for f in errors.cpp $SRCS; do
-  /opt/rocm/bin/hipcc $FLAGS $DEFS -c $ROOT/avr_amd/csrc/$f -o /tmp/avr_var_$NAME/$f.o
+  /opt/rocm/bin/hipcc $FLAGS ${EXTRA:-} $DEFS -c $ROOT/avr_amd/csrc/$f -o /tmp/avr_var_$NAME/$f.o
   OBJS="$OBJS /tmp/avr_var_$NAME/$f.o"
 done
 /opt/rocm/bin/hipcc $FLAGS -shared $OBJS -o $OUT

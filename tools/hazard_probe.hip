@@ -145,6 +145,22 @@ PROBE_KERNEL2(war_busy_dep_8, SET_OLD "s_nop 7\n\t" MFMA_Q_OTHER MFMA_Q_DEP NOPS
 PROBE_KERNEL2(raw_busy_0, SET_OLD "s_nop 7\n\t" MFMA_P_OTHER PERM_NEW NOPS_0 MFMA DRAIN)
 PROBE_KERNEL2(raw_busy_1, SET_OLD "s_nop 7\n\t" MFMA_P_OTHER PERM_NEW NOPS_1 MFMA DRAIN)
 
+// The bf16x3 DFT's compiled schedule: two accumulators
+// interleaved, so the MFMA that reads B waits behind the other accumulator's
+// MFMA AND for its own accumulator from two MFMAs back; the four B registers
+// are rewritten by v_perm_b32 right after it, then read (new) by the next
+// MFMA.  Q must hold hi + old (or 2 hi + old in the longer chain).
+#define MFMA_P_DEP_NEW "v_mfma_f32_32x32x16_f16 v[220:235], %[a], v[200:203], v[220:235]\n\t"
+#define MFMA_Q_DEP_HI "v_mfma_f32_32x32x16_f16 v[204:219], %[a], %[hv], v[204:219]\n\t"
+#define MFMA_P_DEP_HI "v_mfma_f32_32x32x16_f16 v[220:235], %[a], %[hv], v[220:235]\n\t"
+PROBE_KERNEL2(war_inter_perm_0, SET_OLD "s_nop 7\n\t" MFMA_Q_OTHER MFMA_P_OTHER MFMA_Q_DEP NOPS_0 PERM_NEW "s_nop 1\n\t" MFMA_P_DEP_NEW DRAIN)
+PROBE_KERNEL2(war_inter_perm_1, SET_OLD "s_nop 7\n\t" MFMA_Q_OTHER MFMA_P_OTHER MFMA_Q_DEP NOPS_1 PERM_NEW "s_nop 1\n\t" MFMA_P_DEP_NEW DRAIN)
+PROBE_KERNEL2(war_inter_perm_4, SET_OLD "s_nop 7\n\t" MFMA_Q_OTHER MFMA_P_OTHER MFMA_Q_DEP NOPS_4 PERM_NEW "s_nop 1\n\t" MFMA_P_DEP_NEW DRAIN)
+PROBE_KERNEL2(war_inter_chain_0, SET_OLD "s_nop 7\n\t" MFMA_Q_OTHER MFMA_P_OTHER MFMA_Q_DEP_HI MFMA_P_DEP_HI MFMA_Q_DEP NOPS_0 PERM_NEW "s_nop 1\n\t" MFMA_P_DEP_NEW DRAIN)
+// RAW into the stalled dependent MFMA at 1 and 2 states (hipcc pads 2)
+PROBE_KERNEL2(raw_inter_1, SET_OLD "s_nop 7\n\t" MFMA_Q_OTHER MFMA_P_OTHER PERM_NEW NOPS_1 MFMA_Q_DEP DRAIN)
+PROBE_KERNEL2(raw_inter_2, SET_OLD "s_nop 7\n\t" MFMA_Q_OTHER MFMA_P_OTHER PERM_NEW NOPS_2 MFMA_Q_DEP DRAIN)
+
 // WAR on a DS read's ADDRESS register: ds_read_b64 from the address in v236,
 // N states, a VALU rewrite of v236 (another address).  The read must return
 // the OLD address's data.  BUSY: 8 ds_read_b128 queued ahead of it, so the
@@ -290,6 +306,7 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 256; ++i) bnew[i] = (in[512 + i] & 0xFFFF) | (in[768 + i] << 16);
     std::vector<uint32_t> bmov(in.begin() + 512, in.begin() + 768);
     std::vector<float> d_old(1024), d_new(1024), d_mov(1024), d_hi(1024), d_dep(1024), d_depnew(1024);
+    std::vector<float> d_hinew(1024), d_2hiold(1024), d_2hinew(1024);
     ref(in.data(), bold.data(), d_old.data());
     ref(in.data(), bnew.data(), d_new.data());
     ref(in.data(), bmov.data(), d_mov.data());
@@ -298,6 +315,9 @@ int main(int argc, char** argv) {
     for (int i = 0; i < 1024; ++i) {
         d_dep[i] = d_hi[i] + d_old[i];     // the dependent chain on the old B
         d_depnew[i] = d_hi[i] + d_mov[i];  // ... on the rewritten B (the hazard)
+        d_hinew[i] = d_hi[i] + d_new[i];
+        d_2hiold[i] = d_hi[i] + d_hi[i] + d_old[i];
+        d_2hinew[i] = d_hi[i] + d_hi[i] + d_new[i];
     }
     uint32_t* din;
     float* dout;
@@ -309,8 +329,12 @@ int main(int argc, char** argv) {
     struct K {
         const char* name;
         kern_t k;
-        int war;  // 0: want new (RAW), 1: want old (WAR), 2: dependent chain on the old B
-    } ks[] = {{"war_busy_indep_nops0", war_busy_indep_0, 1}, {"war_busy_indep_nops2", war_busy_indep_2, 1},
+        int war;  // 0: want new (RAW), 1: want old (WAR), 2: dependent chain on the old B,
+                  // 3: hi + old (perm rewrite), 4: 2 hi + old, 5: hi + new (RAW into the chain)
+    } ks[] = {{"war_inter_perm_nops0", war_inter_perm_0, 3}, {"war_inter_perm_nops1", war_inter_perm_1, 3},
+              {"war_inter_perm_nops4", war_inter_perm_4, 3}, {"war_inter_chain_nops0", war_inter_chain_0, 4},
+              {"raw_inter_nops1", raw_inter_1, 5}, {"raw_inter_nops2", raw_inter_2, 5},
+              {"war_busy_indep_nops0", war_busy_indep_0, 1}, {"war_busy_indep_nops2", war_busy_indep_2, 1},
               {"war_busy_dep_nops0", war_busy_dep_0, 2},     {"war_busy_dep_nops1", war_busy_dep_1, 2},
               {"war_busy_dep_nops2", war_busy_dep_2, 2},     {"war_busy_dep_nops4", war_busy_dep_4, 2},
               {"war_busy_dep_nops8", war_busy_dep_8, 2},     {"raw_busy_nops0", raw_busy_0, 0},
@@ -329,8 +353,10 @@ int main(int argc, char** argv) {
             return 1;
         }
         hipMemcpy(out.data(), dout, nout * 4, hipMemcpyDeviceToHost);
-        const float* want = k.war == 2 ? d_dep.data() : k.war ? d_old.data() : d_new.data();
-        const float* other = k.war == 2 ? d_depnew.data() : k.war ? d_mov.data() : d_old.data();
+        const float* want = k.war == 5 ? d_hinew.data() : k.war == 4 ? d_2hiold.data() : k.war == 3 ? d_dep.data()
+                            : k.war == 2 ? d_dep.data() : k.war ? d_old.data() : d_new.data();
+        const float* other = k.war == 5 ? d_dep.data() : k.war == 4 ? d_2hinew.data() : k.war == 3 ? d_hinew.data()
+                             : k.war == 2 ? d_depnew.data() : k.war ? d_mov.data() : d_old.data();
         long ok = 0, wrong_other = 0, garbage = 0, unstable = 0;
         long bad_lane_hist[64] = {};
         for (int w = 0; w < waves; ++w)

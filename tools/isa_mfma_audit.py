@@ -108,14 +108,22 @@ def audit_asm(path, window):
             if not op.startswith("v_mfma") or len(ops) < 4:
                 continue
             srcab = regs(ops[1]) | regs(ops[2])
-            # WAR: later writers of SrcA/B
+            srcb = regs(ops[2])
+            # the MFMA issued right behind another one (the matrix pipe busy:
+            # it may wait to start while later instructions issue)
+            behind = i > 0 and block[i - 1][0].startswith("v_mfma")
+            # WAR: later writers of SrcA/B (SrcB separately: the bf16x3 DFT's
+            # stale bins were B-operand lanes, §14d)
             dist = 0
             for op2, ops2, line2 in block[i + 1:]:
                 if dist >= window:
                     break
                 w = writes(op2, ops2)
                 if w & srcab:
-                    key = (kernel, "WAR_after_mfma", klass(op2))
+                    kind = "WAR_after_mfma_B" if w & srcb else "WAR_after_mfma_A"
+                    if behind and kind.endswith("B"):
+                        kind += "_behind_mfma"
+                    key = (kernel, kind, klass(op2))
                     f = findings[key]
                     f["count"] += 1
                     if dist < f["min_states"]:
@@ -164,7 +172,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("sources", nargs="*")
     ap.add_argument("--window", type=int, default=8)
+    ap.add_argument("--asm", nargs="*", default=[], help="audit these assembly files instead")
     a = ap.parse_args()
+    for path in a.asm:
+        for (kern, kind, cls), f in sorted(audit_asm(path, a.window).items()):
+            print(json.dumps({"asm": os.path.basename(path), "kernel": kern[:60], "kind": kind, "writer": cls,
+                              "pairs": f["count"], "min_wait_states": f["min_states"], "example": f["example"]}))
+    if a.asm:
+        return
     srcs = a.sources or sorted(os.path.basename(p) for p in glob.glob(os.path.join(CSRC, "*.hip")))
     tmp = tempfile.mkdtemp(prefix="avr_isa_")
     for src in srcs:

@@ -109,7 +109,9 @@ def main():
         t = sorted(times[name])
         print(json.dumps({"lib": name, "workload": a.workload, "dtype": a.dtype, "median_us": t[len(t) // 2],
                           "min_us": t[0], "n": len(t), "bitwise_equal_to_" + libs[0][0]: bool(torch.equal(outs[name], ref)),
-                          "finite": bool(torch.isfinite(outs[name]).all())}), flush=True)
+                          "finite": bool(torch.isfinite(outs[name]).all()),
+                          "max_abs_diff": float((outs[name] - ref).abs().max()),
+                          "rel_l2_diff": float((outs[name] - ref).norm() / ref.norm())}), flush=True)
 
 
 if __name__ == "__main__":
