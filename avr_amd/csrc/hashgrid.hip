@@ -670,7 +670,7 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
                                                                          const int* __restrict__ part_start,
                                                                          const int* __restrict__ slice_base,
                                                                          const uint3* __restrict__ contrib,
-                                                                         float* __restrict__ gparams) {
+                                                                         float* __restrict__ gparams, int overwrite) {
     __shared__ float2 img_all[kReduceWaves][kPartEntries];
     __shared__ uint8_t tag_all[kReduceWaves][kPartEntries];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -687,15 +687,22 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
     const int p = lo;
     const int ns = slice_base[p + 1] - slice_base[p], sl = b - slice_base[p];
     const int n = totals[p];
-    if (n == 0) return;  // wave-uniform
-    const int i0 = part_start[p] + (int)((int64_t)n * sl / ns);
-    const int i1 = part_start[p] + (int)((int64_t)n * (sl + 1) / ns);
     int l = 0;
     while (plan.pbase[l + 1] <= p) ++l;
     const int64_t e0 = (int64_t)(p - plan.pbase[l]) * kPartEntries;
     // level sizes are multiples of 8 entries: ne is, and the partition's
     // 2*ne floats start 16-byte aligned
     const int ne = (int)min((int64_t)kPartEntries, lt.offset[l + 1] - lt.offset[l] - e0);
+    float* dstf = gparams + 2 * (lt.offset[l] + e0);
+    if (n == 0) {  // wave-uniform
+        if (overwrite) {  // (a partition without contributions has one slice)
+            float4* dst = reinterpret_cast<float4*>(dstf);
+            for (int i = lane; i < ne / 2; i += 64) dst[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        return;
+    }
+    const int i0 = part_start[p] + (int)((int64_t)n * sl / ns);
+    const int i1 = part_start[p] + (int)((int64_t)n * (sl + 1) / ns);
     for (int i = lane; i < ne; i += 64) img[i] = make_float2(0.f, 0.f);
     constexpr int U = 8;
     for (int i = i0; i < i1; i += 64 * U) {
@@ -750,12 +757,11 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
             }
         }
     }
-    float* dstf = gparams + 2 * (lt.offset[l] + e0);
     const float4* img4 = reinterpret_cast<const float4*>(img);
-    if (ns == 1) {  // the wave owns these entries: plain read-add-write
+    if (ns == 1) {  // the wave owns these entries: plain read-add-write (or write)
         float4* dst = reinterpret_cast<float4*>(dstf);
         for (int i = lane; i < ne / 2; i += 64) {
-            float4 a = dst[i];
+            float4 a = overwrite ? make_float4(0.f, 0.f, 0.f, 0.f) : dst[i];
             const float4 c = img4[i];
             a.x += c.x;
             a.y += c.y;
@@ -764,10 +770,26 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
             dst[i] = a;
         }
     } else {  // several slices: no-return atomics of the touched entries
+        // (overwrite: hg_bwd_zero_hot_kernel cleared these partitions first)
         const float* imgf = reinterpret_cast<const float*>(img);
         for (int i = lane; i < 2 * ne; i += 64)
             if (imgf[i] != 0.0f) atomicAdd(dstf + i, imgf[i]);
     }
+}
+
+// overwrite form: the partitions the reduce splits over several slices
+// (their slices add with atomics) are cleared first; one block per partition
+__global__ __launch_bounds__(256) void hg_bwd_zero_hot_kernel(LevelTable lt, BwdPlan plan, int total_parts,
+                                                              const int* __restrict__ slice_base,
+                                                              float* __restrict__ gparams) {
+    const int p = blockIdx.x;
+    if (p >= total_parts || slice_base[p + 1] - slice_base[p] <= 1) return;
+    int l = 0;
+    while (plan.pbase[l + 1] <= p) ++l;
+    const int64_t e0 = (int64_t)(p - plan.pbase[l]) * kPartEntries;
+    const int ne = (int)min((int64_t)kPartEntries, lt.offset[l + 1] - lt.offset[l] - e0);
+    float4* dst = reinterpret_cast<float4*>(gparams + 2 * (lt.offset[l] + e0));
+    for (int i = threadIdx.x; i < ne / 2; i += 256) dst[i] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 constexpr int64_t kMaxBwdWorkspaceBytes = int64_t(1) << 31;  // 2 GiB (config 4: 283 MB)
@@ -1067,23 +1089,29 @@ extern "C" int avr_hashgrid_bwd_workspace(int64_t N, int32_t n_levels, const int
     return 0;
 }
 
-extern "C" int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const float* x, const void* grad_out,
-                                            int32_t grad_dtype, const int64_t* level_offset,
-                                            const float* level_scale, const int32_t* level_res,
-                                            float* grad_params, void* workspace, int64_t workspace_bytes,
-                                            void* stream) {
+namespace {
+int bwd_partitioned(int64_t N, int32_t n_levels, const float* x, const void* grad_out, int32_t grad_dtype,
+                    const int64_t* level_offset, const float* level_scale, const int32_t* level_res,
+                    float* grad_params, void* workspace, int64_t workspace_bytes, void* stream, bool overwrite) {
     AVR_REQUIRE(N >= 0 && x && grad_out && level_offset && level_scale && level_res && grad_params && workspace,
                 "avr_hashgrid_bwd_partitioned: bad args");
     AVR_REQUIRE(reinterpret_cast<uintptr_t>(grad_params) % 16 == 0 && reinterpret_cast<uintptr_t>(workspace) % 256 == 0,
                 "avr_hashgrid_bwd_partitioned: grad_params must be 16-byte, workspace 256-byte aligned");
     AVR_REQUIRE(grad_dtype == AVR_DTYPE_F32 || grad_dtype == AVR_DTYPE_F16,
                 "avr_hashgrid_bwd_partitioned: unknown grad dtype");
-    if (N == 0) return 0;
     LevelTable lt;
     if (int e = make_table(n_levels, level_offset, level_scale, level_res, &lt)) return e;
     hipStream_t st = as_stream(stream);
     const int L = n_levels;
+    // the overwrite form's atomic paths (few points, shapes the partitioned
+    // passes do not take) add into a cleared gradient
+    auto clear = [&]() -> bool {
+        return !overwrite ||
+               hipMemsetAsync(grad_params, 0, (size_t)(2 * level_offset[L]) * sizeof(float), st) == hipSuccess;
+    };
+    if (N == 0) return clear() ? 0 : fail(AVR_E_ARG, "avr_hashgrid_bwd_partitioned_set: clear failed");
     if (N < kPartitionedMinPoints) {  // few points: the atomic kernel (same += result)
+        if (!clear()) return fail(AVR_E_ARG, "avr_hashgrid_bwd_partitioned_set: clear failed");
         if (grad_dtype == AVR_DTYPE_F32)
             launch_bwd<float>(st, N, L, x, (const float*)grad_out, lt, grad_params);
         else
@@ -1093,6 +1121,7 @@ extern "C" int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const f
     BwdLayout b;
     if (bwd_layout(N, n_levels, level_offset, level_res, &b) != 0 || !b.scatter_ok) {
         // shapes the partitioned passes do not take: the atomic kernel (same += result)
+        if (!clear()) return fail(AVR_E_ARG, "avr_hashgrid_bwd_partitioned_set: clear failed");
         if (grad_dtype == AVR_DTYPE_F32)
             launch_bwd<float>(st, N, L, x, (const float*)grad_out, lt, grad_params);
         else
@@ -1124,8 +1153,35 @@ extern "C" int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const f
     else
         hipLaunchKernelGGL(hg_bwd_scatter_kernel<__half>, grid, dim3(256), lds_scat, st, N, L, x,
                            (const __half*)grad_out, lt, b.plan, counts, part_start, contrib);
+    if (overwrite)
+        hipLaunchKernelGGL(hg_bwd_zero_hot_kernel, dim3((unsigned)b.total_parts), dim3(256), 0, st, lt, b.plan,
+                           b.total_parts, slice_base, grad_params);
     hipLaunchKernelGGL(hg_bwd_reduce_kernel, dim3((unsigned)((b.max_slices + kReduceWaves - 1) / kReduceWaves)),
                        dim3(64 * kReduceWaves), 0, st, L, lt, b.plan, b.total_parts, totals, part_start, slice_base,
-                       contrib, grad_params);
+                       contrib, grad_params, (int)overwrite);
     return check_launch("avr_hashgrid_bwd_partitioned");
+}
+}  // namespace
+
+extern "C" int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const float* x, const void* grad_out,
+                                            int32_t grad_dtype, const int64_t* level_offset,
+                                            const float* level_scale, const int32_t* level_res,
+                                            float* grad_params, void* workspace, int64_t workspace_bytes,
+                                            void* stream) {
+    return bwd_partitioned(N, n_levels, x, grad_out, grad_dtype, level_offset, level_scale, level_res, grad_params,
+                           workspace, workspace_bytes, stream, false);
+}
+
+// The same gradient written instead of added: grad_params need not be
+// cleared first (every entry of every level is written exactly once, zeros
+// where no point contributes; the partitions several reduce slices share
+// are cleared by their own pass).  Saves the caller's fill of the table
+// and the reduce pass's read of it.
+extern "C" int avr_hashgrid_bwd_partitioned_set(int64_t N, int32_t n_levels, const float* x, const void* grad_out,
+                                                int32_t grad_dtype, const int64_t* level_offset,
+                                                const float* level_scale, const int32_t* level_res,
+                                                float* grad_params, void* workspace, int64_t workspace_bytes,
+                                                void* stream) {
+    return bwd_partitioned(N, n_levels, x, grad_out, grad_dtype, level_offset, level_scale, level_res, grad_params,
+                           workspace, workspace_bytes, stream, true);
 }

@@ -110,7 +110,13 @@ __device__ __forceinline__ uint16_t bits16(float v) { return __builtin_bit_cast(
 // ReLU of two packed 16-bit floats (v_pk_max_i16 with 0: a set sign bit is a
 // negative int16; bf16 and fp16 alike).  One VALU op per two values; a NaN
 // with the sign bit set becomes 0.
-__device__ __forceinline__ float relu(float v) { return v < 0.0f ? 0.0f : v; }  // NaN passes
+// (IEEE-754 2019 maximum: NaN passes, one v_maximum3_f32 instead of a
+// compare and a select)
+#if AVR_SIGMA_RELU_SELECT  // (the round-4 form, for A/B: v_cmp + v_cndmask)
+__device__ __forceinline__ float relu(float v) { return v < 0.0f ? 0.0f : v; }
+#else
+__device__ __forceinline__ float relu(float v) { return __builtin_elementwise_maximum(v, 0.0f); }
+#endif
 
 __device__ __forceinline__ uint32_t relu16x2(uint32_t u) {
     const s16x2 r = __builtin_elementwise_max(__builtin_bit_cast(s16x2, u), (s16x2){0, 0});

@@ -80,19 +80,25 @@ class _HashGridFn(torch.autograd.Function):
         g = grad_out.contiguous()
         if g.dtype not in (torch.float32, torch.float16):
             g = g.float()
-        gp = torch.zeros(enc.n_params, dtype=torch.float32, device=x.device)
         st = torch.cuda.current_stream(x.device).cuda_stream
         N = x.size(0)
         if os.environ.get("AVR_HASHGRID_BWD", "partitioned") == "atomic":
+            gp = torch.zeros(enc.n_params, dtype=torch.float32, device=x.device)
             _lib.call("avr_hashgrid_bwd", N, enc.n_levels, x.data_ptr(), g.data_ptr(),
                       _code(g.dtype), enc._off.ctypes.data, enc._scale.ctypes.data,
                       enc._res.ctypes.data, gp.data_ptr(), st)
             return None, gp, None, None
-        # partitioned (no global atomics): workspace from the caching allocator
+        # partitioned (no global atomics), written rather than added: no
+        # clearing pass over the table (AVR_HASHGRID_BWD=partitioned_add: the
+        # += form into a cleared table, for A/B); workspace from the caching
+        # allocator
+        add = os.environ.get("AVR_HASHGRID_BWD") == "partitioned_add"
+        gp = (torch.zeros if add else torch.empty)(enc.n_params, dtype=torch.float32, device=x.device)
         nbytes = ctypes.c_int64()
         _lib.call("avr_hashgrid_bwd_workspace", N, enc.n_levels, enc._off.ctypes.data, ctypes.byref(nbytes))
         ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=x.device)
-        _lib.call("avr_hashgrid_bwd_partitioned", N, enc.n_levels, x.data_ptr(), g.data_ptr(),
+        _lib.call("avr_hashgrid_bwd_partitioned" if add else "avr_hashgrid_bwd_partitioned_set", N, enc.n_levels,
+                  x.data_ptr(), g.data_ptr(),
                   _code(g.dtype), enc._off.ctypes.data, enc._scale.ctypes.data, enc._res.ctypes.data,
                   gp.data_ptr(), ws.data_ptr(), nbytes.value, st)
         return None, gp, None, None

@@ -291,6 +291,14 @@ int avr_hashgrid_bwd_partitioned(int64_t N, int32_t n_levels, const float* x, co
                                  int32_t grad_dtype, const int64_t* level_offset, const float* level_scale,
                                  const int32_t* level_res, float* grad_params, void* workspace,
                                  int64_t workspace_bytes, void* stream);
+/* The same, writing the gradient instead of adding it (=, not +=): every
+ * entry of grad_params is written, zeros where no point contributes, so the
+ * caller skips clearing the table and the pass skips reading it (the
+ * training step's grids). */
+int avr_hashgrid_bwd_partitioned_set(int64_t N, int32_t n_levels, const float* x, const void* grad_out,
+                                     int32_t grad_dtype, const int64_t* level_offset, const float* level_scale,
+                                     const int32_t* level_res, float* grad_params, void* workspace,
+                                     int64_t workspace_bytes, void* stream);
 
 /* ---- a6: weight gradient of the networks' bias-free linear layers -------
  * grad_w[M][K] (fp32) = sum_n grad_y[n][M] * x[n][K], both operands bf16,

@@ -186,3 +186,41 @@ def test_partitioned_backward_accumulates(n):
     torch.cuda.synchronize()
     scale = float(a.abs().max())
     assert float((b - base - a).abs().max()) <= 1e-5 * scale + 1e-6
+
+
+@pytest.mark.parametrize("n", [0, 1, 3000, 16897, 40000, 262144])
+def test_partitioned_backward_set_overwrites(n):
+    """avr_hashgrid_bwd_partitioned_set writes the gradient (=) over a table
+    full of garbage (NaN): equal to the += form into zeros wherever a single
+    reduce slice owns the partition (bit for bit), within fp32 reassociation
+    where several slices add atomically, and zero everywhere nothing
+    contributes.  n = 0 clears; below 16384 points the atomic path runs on a
+    cleared table; 262,144 points include multi-slice (hot) partitions."""
+    import ctypes
+
+    from avr_amd import _lib
+    from avr_amd.encoding import _code
+
+    enc = HashGridEncoding(3, dict(CFG, log2_hashmap_size=16), dtype=torch.float16, seed=10).to(DEV)
+    m = max(n, 8)
+    x = torch.from_numpy(_points(m, 12)[-n:].copy() if n else _points(8, 12)[:0].copy()).to(DEV)
+    L = enc.n_levels
+    g = torch.randn(n, 2 * L, device=DEV).half()
+    st = torch.cuda.current_stream(DEV).cuda_stream
+    meta = (enc._off.ctypes.data, enc._scale.ctypes.data, enc._res.ctypes.data)
+    nb = ctypes.c_int64()
+    _lib.call("avr_hashgrid_bwd_workspace", n, L, enc._off.ctypes.data, ctypes.byref(nb))
+    ws = torch.empty(max(nb.value, 256), dtype=torch.uint8, device=DEV)
+    a = torch.zeros(enc.n_params, device=DEV)
+    _lib.call("avr_hashgrid_bwd_partitioned", n, L, x.data_ptr() if n else a.data_ptr(),
+              g.data_ptr() if n else a.data_ptr(), _code(g.dtype), *meta, a.data_ptr(), ws.data_ptr(),
+              nb.value, st)
+    b = torch.full((enc.n_params,), float("nan"), device=DEV)
+    _lib.call("avr_hashgrid_bwd_partitioned_set", n, L, x.data_ptr() if n else a.data_ptr(),
+              g.data_ptr() if n else a.data_ptr(), _code(g.dtype), *meta, b.data_ptr(), ws.data_ptr(),
+              nb.value, st)
+    torch.cuda.synchronize()
+    assert torch.isfinite(b).all()
+    scale = float(a.abs().max()) if n else 1.0
+    assert float((b - a).abs().max()) <= 1e-5 * scale
+    assert torch.equal(a == 0, b == 0)

@@ -52,6 +52,31 @@ def timeit(fn, steps, warmup):
     return (time.perf_counter() - t0) / steps
 
 
+def gpu_and_host_ms(fn, steps, spin_cycles=int(4e8)):
+    """(GPU ms per step, host issue ms per step, spin ms): the loop is issued
+    behind a spin kernel, so the events around it time the GPU's own work
+    back to back while the host's issue time is measured apart.  The GPU
+    figure is valid when the whole issue took less than the spin."""
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s0.record()
+    torch.cuda._sleep(spin_cycles)
+    s1.record()
+    torch.cuda.synchronize()
+    spin_ms = s0.elapsed_time(s1)
+    torch.cuda._sleep(spin_cycles)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    host_total = (time.perf_counter() - t0) * 1e3
+    e1.record()
+    torch.cuda.synchronize()
+    gpu = e0.elapsed_time(e1) / steps if host_total < 0.8 * spin_ms else None
+    return gpu, host_total / steps, spin_ms
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c3_raf_furnished_b4")
@@ -66,6 +91,8 @@ def main():
     ap.add_argument("--profile", action="store_true", help="torch.profiler table of a few steps")
     ap.add_argument("--loss", default="criterion", choices=["criterion", "l1"])
     ap.add_argument("--nan-check", action="store_true", help="reference's per-step isnan().item()")
+    ap.add_argument("--sync-debug", action="store_true", help="report the torch ops of one step that "
+                    "synchronise with the device (torch.cuda.set_sync_debug_mode), with their stacks")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     w = WORKLOADS[args.workload]
@@ -130,6 +157,20 @@ def main():
         opt.step()
 
     t = timeit(train_step, args.steps, args.warmup)
+    if args.sync_debug:
+        import traceback
+        import warnings
+
+        def show(message, category, filename, lineno, file=None, line=None):
+            print(f"SYNC: {message}", file=sys.stderr)
+            print("".join(traceback.format_stack(limit=14)[:-2]), file=sys.stderr)
+
+        warnings.showwarning = show
+        warnings.simplefilter("always")
+        torch.cuda.set_sync_debug_mode("warn")
+        train_step()
+        torch.cuda.set_sync_debug_mode("default")
+        torch.cuda.synchronize()
     if args.profile:
         from torch.profiler import ProfilerActivity, profile
 
@@ -139,6 +180,10 @@ def main():
             torch.cuda.synchronize()
         print(prof.key_averages().table(sort_by="cpu_time_total", row_limit=40), file=sys.stderr)
     res["train_step_ms"] = t * 1e3
+    gpu, host, spin = gpu_and_host_ms(train_step, args.steps)
+    res["train_step_gpu_ms"] = gpu  # the steps' GPU work back to back (None: issue outlasted the spin)
+    res["train_step_host_issue_ms"] = host
+    res["spin_ms"] = spin
     res["train_ray_samples_per_s"] = w.ray_samples / t
     res["mlp_dtype"] = args.mlp_dtype
     res["fused_head"] = not args.no_fused
