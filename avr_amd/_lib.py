@@ -124,6 +124,7 @@ _SIGS = {
     "avr_weights_bwd": (ctypes.c_int, [_vp, _c_i32, _vp, _c_i32, _vp, _vp, _vp, _vp]),
     "avr_hashgrid_fwd": (ctypes.c_int, [_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp, _c_i32, _vp]),
     "avr_hashgrid_fwd_lm": (ctypes.c_int, [_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp, _c_i32, _vp]),
+    "avr_hashgrid_fwd_lm_unit": (ctypes.c_int, [_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp, _c_i32, _vp]),
     "avr_ray_pose_bias": (ctypes.c_int, [_c_i32, _c_i32, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp,
                                          _c_i32, _vp, _vp, _vp, _vp, _c_i32, _c_i32, _c_i32, _vp, _vp,
                                          _c_i32, _vp, _vp]),

@@ -217,11 +217,15 @@ struct EntryGroup<__half> {
 template <typename Tp, typename To, bool ROW_MAJOR = false, bool GROUP = false>
 __global__ __launch_bounds__(256) void hashgrid_fwd_lm_kernel(int64_t N, const float* __restrict__ x,
                                                               const Tp* __restrict__ params,
-                                                              LevelTable lt, To* __restrict__ out) {
+                                                              LevelTable lt, To* __restrict__ out, int unit) {
     const int l = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= N) return;
-    const float xi[3] = {x[i * 3 + 0], x[i * 3 + 1], x[i * 3 + 2]};
+    float xi[3] = {x[i * 3 + 0], x[i * 3 + 1], x[i * 3 + 2]};
+    if (unit) {  // (x + 1) / 2 as 0.5 + 0.5 x: the halving is exact, one rounding (model.py:187-189)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) xi[d] = 0.5f + 0.5f * xi[d];
+    }
     const Corner c = locate(xi, lt.scale[l]);
     const uint32_t size = (uint32_t)(lt.offset[l + 1] - lt.offset[l]);
     const uint32_t res = lt.res[l];
@@ -379,16 +383,16 @@ int make_table(int L, const int64_t* off, const float* scale, const int32_t* res
 
 template <typename Tp, typename To, bool ROW_MAJOR>
 void launch_lm(dim3 grid, hipStream_t st, int64_t N, const float* x, const void* params, LevelTable lt,
-               void* out, bool grp) {
+               void* out, bool grp, int unit) {
     if constexpr (std::is_same_v<Tp, __half>) {
         if (grp) {
             hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<Tp, To, ROW_MAJOR, true>), grid, dim3(256), 0, st, N,
-                               x, (const Tp*)params, lt, (To*)out);
+                               x, (const Tp*)params, lt, (To*)out, unit);
             return;
         }
     }
     hipLaunchKernelGGL((hashgrid_fwd_lm_kernel<Tp, To, ROW_MAJOR, false>), grid, dim3(256), 0, st, N, x,
-                           (const Tp*)params, lt, (To*)out);
+                           (const Tp*)params, lt, (To*)out, unit);
 }
 
 // Level-major forward launch; grouped corner loads for fp16 tables whose
@@ -399,16 +403,16 @@ void launch_lm(dim3 grid, hipStream_t st, int64_t N, const float* x, const void*
 // 116-118 us row-major (profiles/r02_hashgrid_group_ab.jsonl)
 template <bool ROW_MAJOR>
 int launch_fwd_lm(dim3 grid, hipStream_t st, int64_t N, const float* x, const void* params,
-                  int32_t param_dtype, const LevelTable& lt, void* out, int32_t out_dtype) {
+                  int32_t param_dtype, const LevelTable& lt, void* out, int32_t out_dtype, int unit = 0) {
     const bool grp = group_loads() && ((uintptr_t)params & 15) == 0;
     if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F32)
-        launch_lm<float, float, ROW_MAJOR>(grid, st, N, x, params, lt, out, grp);
+        launch_lm<float, float, ROW_MAJOR>(grid, st, N, x, params, lt, out, grp, unit);
     else if (param_dtype == AVR_DTYPE_F32 && out_dtype == AVR_DTYPE_F16)
-        launch_lm<float, __half, ROW_MAJOR>(grid, st, N, x, params, lt, out, grp);
+        launch_lm<float, __half, ROW_MAJOR>(grid, st, N, x, params, lt, out, grp, unit);
     else if (param_dtype == AVR_DTYPE_F16 && out_dtype == AVR_DTYPE_F16)
-        launch_lm<__half, __half, ROW_MAJOR>(grid, st, N, x, params, lt, out, grp);
+        launch_lm<__half, __half, ROW_MAJOR>(grid, st, N, x, params, lt, out, grp, unit);
     else if (param_dtype == AVR_DTYPE_F16 && out_dtype == AVR_DTYPE_F32)
-        launch_lm<__half, float, ROW_MAJOR>(grid, st, N, x, params, lt, out, grp);
+        launch_lm<__half, float, ROW_MAJOR>(grid, st, N, x, params, lt, out, grp, unit);
     else
         return fail(AVR_E_ARG, "avr_hashgrid_fwd: unknown dtype");
     return 0;
@@ -913,10 +917,10 @@ extern "C" int avr_hashgrid_bwd(int64_t N, int32_t n_levels, const float* x, con
     return check_launch("avr_hashgrid_bwd");
 }
 
-extern "C" int avr_hashgrid_fwd_lm(int64_t N, int32_t n_levels, const float* x, const void* params,
-                                   int32_t param_dtype, const int64_t* level_offset,
-                                   const float* level_scale, const int32_t* level_res, void* out,
-                                   int32_t out_dtype, void* stream) {
+namespace {
+int fwd_lm(int64_t N, int32_t n_levels, const float* x, const void* params, int32_t param_dtype,
+           const int64_t* level_offset, const float* level_scale, const int32_t* level_res, void* out,
+           int32_t out_dtype, void* stream, int unit) {
     AVR_REQUIRE(N >= 0 && x && params && level_offset && level_scale && level_res && out,
                 "avr_hashgrid_fwd_lm: bad args");
     if (N == 0) return 0;
@@ -924,8 +928,27 @@ extern "C" int avr_hashgrid_fwd_lm(int64_t N, int32_t n_levels, const float* x, 
     if (int e = make_table(n_levels, level_offset, level_scale, level_res, &lt)) return e;
     const dim3 grid((unsigned)((N + 255) / 256), (unsigned)n_levels);
     hipStream_t st = as_stream(stream);
-    if (int e = launch_fwd_lm<false>(grid, st, N, x, params, param_dtype, lt, out, out_dtype)) return e;
+    if (int e = launch_fwd_lm<false>(grid, st, N, x, params, param_dtype, lt, out, out_dtype, unit)) return e;
     return check_launch("avr_hashgrid_fwd_lm");
+}
+}  // namespace
+
+extern "C" int avr_hashgrid_fwd_lm(int64_t N, int32_t n_levels, const float* x, const void* params,
+                                   int32_t param_dtype, const int64_t* level_offset,
+                                   const float* level_scale, const int32_t* level_res, void* out,
+                                   int32_t out_dtype, void* stream) {
+    return fwd_lm(N, n_levels, x, params, param_dtype, level_offset, level_scale, level_res, out, out_dtype, stream,
+                  0);
+}
+
+// The same on points in [-1, 1]: the encoding of (x + 1) / 2 (model.py:187-189),
+// the map applied on load instead of by a separate pass over x.
+extern "C" int avr_hashgrid_fwd_lm_unit(int64_t N, int32_t n_levels, const float* x, const void* params,
+                                        int32_t param_dtype, const int64_t* level_offset,
+                                        const float* level_scale, const int32_t* level_res, void* out,
+                                        int32_t out_dtype, void* stream) {
+    return fwd_lm(N, n_levels, x, params, param_dtype, level_offset, level_scale, level_res, out, out_dtype, stream,
+                  1);
 }
 
 // ----------------------------------------------------------------------------
@@ -1035,6 +1058,70 @@ __global__ __launch_bounds__(256) void ray_pose_bias_kernel(int B, int R, int S,
     }
 }
 
+// Rays of one pose per workgroup (R % kBias2Rays == 0): one output per
+// thread (512 threads), the whole k range of that output's weight column in
+// flight at once (one L2 round trip per grid instead of one per 8 k), and the
+// pose's tx term computed once for the workgroup's rays.  The same fma chains
+// (k ascending) and the same final sd + st as ray_pose_bias_kernel: the
+// results are equal bit for bit.
+constexpr int kBias2Rays = 8;
+#ifndef AVR_BIAS_V1  // (A/B: 1 keeps the round-4 kernel for every R)
+#define AVR_BIAS_V1 0
+#endif
+constexpr int kBias2Threads = 512;
+
+template <typename Tp>
+__global__ __launch_bounds__(kBias2Threads) void ray_pose_bias2_kernel(
+    int B, int R, int S, const float* __restrict__ view, const float* __restrict__ tx, const Tp* __restrict__ dp,
+    LevelTable dl, int dL, const Tp* __restrict__ tp, LevelTable tl, int tL, int f16, int mlp_f16,
+    const float* __restrict__ wd, const float* __restrict__ wt, int nout, float* __restrict__ bias) {
+    __shared__ float ed[kBias2Rays][2 * kMaxLevels];
+    __shared__ float et[2 * kMaxLevels];
+    const int64_t g0 = (int64_t)blockIdx.x * kBias2Rays;  // R % kBias2Rays == 0: one pose
+    const int64_t b = g0 / R;
+    for (int q = threadIdx.x; q < (kBias2Rays + 1) * kMaxLevels; q += kBias2Threads) {
+        const int j = q / kMaxLevels, l = q % kMaxLevels;
+        const bool is_tx = j == kBias2Rays;
+        if (l >= (is_tx ? tL : dL)) continue;
+        const int64_t r = (g0 + j) % R;
+        const float* src = is_tx ? tx + b * R * S * 3 : view + (b * R * S + r * S) * 3;
+        const float xi[3] = {(src[0] + 1.0f) / 2.0f, (src[1] + 1.0f) / 2.0f, (src[2] + 1.0f) / 2.0f};
+        const float2 v = is_tx ? encode_point_level(xi, tp, tl, l) : encode_point_level(xi, dp, dl, l);
+        float* e = is_tx ? et : ed[j];
+        e[2 * l] = round_feature(v.x, f16, mlp_f16);
+        e[2 * l + 1] = round_feature(v.y, f16, mlp_f16);
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < nout; o += kBias2Threads) {
+        // weight rows 16 at a time, all in flight before their FMAs
+        constexpr int KB = 16;
+        float st = 0.0f;
+        for (int k0 = 0; k0 < 2 * tL; k0 += KB) {
+            float w[KB];
+#pragma unroll
+            for (int u = 0; u < KB; ++u) w[u] = k0 + u < 2 * tL ? wt[(int64_t)(k0 + u) * nout + o] : 0.0f;
+#pragma unroll
+            for (int u = 0; u < KB; ++u)
+                if (k0 + u < 2 * tL) st = fmaf(et[k0 + u], w[u], st);
+        }
+        float sd[kBias2Rays];
+#pragma unroll
+        for (int r = 0; r < kBias2Rays; ++r) sd[r] = 0.0f;
+        for (int k0 = 0; k0 < 2 * dL; k0 += KB) {
+            float w[KB];
+#pragma unroll
+            for (int u = 0; u < KB; ++u) w[u] = k0 + u < 2 * dL ? wd[(int64_t)(k0 + u) * nout + o] : 0.0f;
+#pragma unroll
+            for (int u = 0; u < KB; ++u)
+                if (k0 + u < 2 * dL)
+#pragma unroll
+                    for (int r = 0; r < kBias2Rays; ++r) sd[r] = fmaf(ed[r][k0 + u], w[u], sd[r]);
+        }
+#pragma unroll
+        for (int r = 0; r < kBias2Rays; ++r) bias[(g0 + r) * nout + o] = sd[r] + st;
+    }
+}
+
 }  // namespace
 
 extern "C" int avr_ray_pose_bias(int32_t B, int32_t R, int32_t S, const float* view, const float* tx,
@@ -1057,6 +1144,22 @@ extern "C" int avr_ray_pose_bias(int32_t B, int32_t R, int32_t S, const float* v
     const dim3 grid((unsigned)((rays + kBiasRays - 1) / kBiasRays));
     const int f16 = enc_dtype == AVR_DTYPE_F16;
     hipStream_t st = as_stream(stream);
+    if (R % kBias2Rays == 0 && !AVR_BIAS_V1) {
+        const dim3 grid2((unsigned)(rays / kBias2Rays));
+        if (param_dtype == AVR_DTYPE_F16)
+            hipLaunchKernelGGL(ray_pose_bias2_kernel<__half>, grid2, dim3(kBias2Threads), 0, st, (int)B, (int)R,
+                               (int)S, view, tx, (const __half*)dir_params, dl, (int)dir_levels,
+                               (const __half*)tx_params, tl, (int)tx_levels, f16, mlp_f16, w_dir, w_tx, (int)n_out,
+                               bias);
+        else if (param_dtype == AVR_DTYPE_F32)
+            hipLaunchKernelGGL(ray_pose_bias2_kernel<float>, grid2, dim3(kBias2Threads), 0, st, (int)B, (int)R,
+                               (int)S, view, tx, (const float*)dir_params, dl, (int)dir_levels,
+                               (const float*)tx_params, tl, (int)tx_levels, f16, mlp_f16, w_dir, w_tx, (int)n_out,
+                               bias);
+        else
+            return fail(AVR_E_ARG, "avr_ray_pose_bias: unknown param dtype");
+        return check_launch("avr_ray_pose_bias");
+    }
     if (param_dtype == AVR_DTYPE_F16)
         hipLaunchKernelGGL(ray_pose_bias_kernel<__half>, grid, dim3(256), 0, st, (int)B, (int)R, (int)S, view, tx,
                            (const __half*)dir_params, dl, (int)dir_levels, (const __half*)tx_params, tl,

@@ -137,9 +137,11 @@ class HashGridEncoding(nn.Module):
         """The level tables in the module's param precision."""
         return cast_weight(self.params, self.param_dtype, cache)
 
-    def forward_level_major(self, x):
+    def forward_level_major(self, x, unit_map=False):
         """Inference-only encoding with level-major output [L, N, 2]
-        (`avr_hashgrid_fwd_lm`): the same values as forward(x) transposed."""
+        (`avr_hashgrid_fwd_lm`): the same values as forward(x) transposed.
+        unit_map: x in [-1, 1] is encoded as (x + 1) / 2, the map applied on
+        load (`avr_hashgrid_fwd_lm_unit`, bit-identical to mapping first)."""
         if not x.is_cuda:
             raise RuntimeError("HashGridEncoding needs a HIP tensor (no CPU fallback)")
         x = x.reshape(-1, 3).float().contiguous()
@@ -147,7 +149,8 @@ class HashGridEncoding(nn.Module):
         out = torch.empty(self.n_levels, N, 2, dtype=self.dtype, device=x.device)
         st = torch.cuda.current_stream(x.device).cuda_stream
         table = self.table(not torch.is_grad_enabled())
-        _lib.call("avr_hashgrid_fwd_lm", N, self.n_levels, x.data_ptr(), table.data_ptr(),
+        fn = "avr_hashgrid_fwd_lm_unit" if unit_map else "avr_hashgrid_fwd_lm"
+        _lib.call(fn, N, self.n_levels, x.data_ptr(), table.data_ptr(),
                   _code(table.dtype), self._off.ctypes.data, self._scale.ctypes.data,
                   self._res.ctypes.data, out.data_ptr(), _code(out.dtype), st)
         return out

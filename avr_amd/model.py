@@ -524,7 +524,7 @@ class AVRModel(nn.Module):
         attn [B, N, 1] and the signal network's input [N, 208] (bf16)."""
         B, R, S = L
         bs, n = pts.size(0), pts.size(1)
-        pos_enc = self._pos_encoding.forward_level_major(_unit(pts.reshape(-1, 3)))
+        pos_enc = self._pos_encoding.forward_level_major(pts.reshape(-1, 3), unit_map=True)
         dir_e = self._dir_encoding(_unit(_per_ray(view.reshape(-1, 3), L)))
         tx_e = self._tx_encoding(_unit(_per_pose(tx.reshape(-1, 3), L)))
         packed = self._sigma_pack.get(_sigma.MESHRIR, _sigma_params(self), self._model_encoder_sigma.dtype)
@@ -540,7 +540,7 @@ class AVRModel(nn.Module):
         and h1 = relu(layer 1) [N, 512] bf16."""
         B, R, S = L
         bs, n = pts.size(0), pts.size(1)
-        pos_enc = self._pos_encoding.forward_level_major(_unit(pts.reshape(-1, 3)))
+        pos_enc = self._pos_encoding.forward_level_major(pts.reshape(-1, 3), unit_map=True)
         w1 = self._model_signal.layers[0].weight
         dt = self._model_encoder_sigma.dtype
         wd, wt = _bias_columns(w1, dt)
@@ -672,15 +672,16 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
         launch: attn [B, N, 1] and the signal network's input [N, 416]."""
         B, R, S = L
         bs, n = pts.size(0), pts.size(1)
-        p = _unit(pts.reshape(-1, 3))
+        p = pts.reshape(-1, 3)  # (the per-sample grids map (x + 1) / 2 on load)
         t = _unit(_per_pose(tx.reshape(-1, 3), L))
         v = _unit(_per_ray(view.reshape(-1, 3), L))
         tv = _unit(_per_pose(tx_view.reshape(-1, 3), L))
         packed = self._sigma_pack.get(_sigma.RAF, _sigma_params(self), self._model_encoder_sigma.dtype)
         attn, base = _sigma.sigma_fwd(
             _sigma.RAF, packed, bs * n,
-            [(self._pos_encoding.forward_level_major(p), 1), (self._tx_pos_encoding(t), R * S)],
+            [(self._pos_encoding.forward_level_major(p, unit_map=True), 1), (self._tx_pos_encoding(t), R * S)],
             [(self._dir_encoding(v), S), (self._tx_dir_encoding(tv), R * S),
-             (self._pos_signal_encoding.forward_level_major(p), 1), (self._tx_pos_signal_encoding(t), R * S)],
+             (self._pos_signal_encoding.forward_level_major(p, unit_map=True), 1),
+             (self._tx_pos_signal_encoding(t), R * S)],
             256, self.leaky_relu)
         return attn.view(bs, n, 1), base

@@ -254,6 +254,12 @@ int avr_hashgrid_fwd(int64_t N, int32_t n_levels, const float* x, const void* pa
 int avr_hashgrid_fwd_lm(int64_t N, int32_t n_levels, const float* x, const void* params,
                         int32_t param_dtype, const int64_t* level_offset, const float* level_scale,
                         const int32_t* level_res, void* out, int32_t out_dtype, void* stream);
+/* The same for points in [-1, 1]: encodes (x + 1) / 2 (model.py:187-189),
+ * mapped on load as 0.5 + 0.5 x (exact halving, one rounding: bit-identical
+ * to the separate elementwise map). */
+int avr_hashgrid_fwd_lm_unit(int64_t N, int32_t n_levels, const float* x, const void* params,
+                             int32_t param_dtype, const int64_t* level_offset, const float* level_scale,
+                             const int32_t* level_res, void* out, int32_t out_dtype, void* stream);
 
 /* AVRModel inference: the signal network's first-layer bias of every ray,
  * from the per-ray view direction and the per-pose tx position (model.py:221

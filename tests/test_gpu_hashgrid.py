@@ -224,3 +224,21 @@ def test_partitioned_backward_set_overwrites(n):
     scale = float(a.abs().max()) if n else 1.0
     assert float((b - a).abs().max()) <= 1e-5 * scale
     assert torch.equal(a == 0, b == 0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+def test_level_major_unit_map_is_bit_identical(dtype):
+    """avr_hashgrid_fwd_lm_unit (the (x + 1) / 2 map applied on load) equals
+    mapping first and encoding (model.py:187-189), bit for bit, including
+    the end points of [-1, 1]."""
+    from avr_amd.model import _unit
+
+    enc = HashGridEncoding(3, CFG, dtype=dtype, seed=13).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(14)
+    x = torch.rand(100003, 3, device=DEV, generator=g) * 2 - 1
+    x[:3] = torch.tensor([[-1.0, 1.0, 0.0], [1.0, -1.0, -1 + 2 ** -24], [0.5, -0.5, 1 - 2 ** -24]], device=DEV)
+    with torch.no_grad():
+        a = enc.forward_level_major(x, unit_map=True)
+        b = enc.forward_level_major(_unit(x))
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)

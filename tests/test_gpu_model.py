@@ -133,15 +133,18 @@ def test_one_output_layer_dgrad_is_the_gemm():
         assert torch.equal(gy * w, gy @ w)
 
 
+@pytest.mark.parametrize("workload", ["c2_meshrir_1024x256x512", "c5_simu_4096x512x2048"])
 @pytest.mark.parametrize("enc_dtype", [torch.float16, torch.float32])
-def test_ray_pose_bias_kernel_matches_torch_ops(enc_dtype):
+def test_ray_pose_bias_kernel_matches_torch_ops(enc_dtype, workload):
     """avr_ray_pose_bias against the torch ops it replaces in the fused
     inference trunk: per-ray / per-pose selection, (x + 1) / 2, the dir and tx
     grids, fp16 -> bf16 -> fp32 rounding, two skinny fp32 GEMMs and their sum
-    (only the GEMMs' fp32 summation order differs)."""
+    (only the GEMMs' fp32 summation order differs).  Config 2 (1024 rays per
+    pose) takes the one-pose-per-workgroup kernel, config 5 (4094 rays, not a
+    multiple of 8) the general one."""
     from avr_amd.model import _bias_columns, _per_pose, _per_ray, _ray_pose_bias
 
-    w = WORKLOADS["c2_meshrir_1024x256x512"]
+    w = WORKLOADS[workload]
     cfg = dict(MESHRIR_MODEL, signal_output_dim=w.T)
     model = AVRModel(cfg, mlp_dtype=torch.bfloat16, enc_dtype=enc_dtype).to(DEV)
     with torch.no_grad():
@@ -162,6 +165,9 @@ def test_ray_pose_bias_kernel_matches_torch_ops(enc_dtype):
         ref = (ref.view(B, L[1], -1) + (tx_e.to(torch.bfloat16).float() @ wt).view(B, 1, -1)).reshape(B * L[1], -1)
     assert got is not None and got.shape == ref.shape
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6 * float(ref.abs().max()))
+    with torch.no_grad():
+        again = _ray_pose_bias(model._dir_encoding, model._tx_encoding, view, tx, wd, wt, L)
+    assert torch.equal(got, again)
 
 
 def test_unit_map_is_bit_identical():
