@@ -164,9 +164,11 @@ def _mlp512x2(x, w1_master, w2_master, dtype):
     return y
 
 
-# hipBLASLt's solution for the width-512 layers at config-2 inference, picked
-# by PyTorch TunableOp over every hipBLASLt / rocBLAS candidate on MI355X
-# (tools/tune_gemms.sh; bit-identical output, 0.12 vs 0.16-0.21 ms per layer).
+# hipBLASLt's solutions for the width-512 layers at config-2 and config-5
+# inference, picked by PyTorch TunableOp over every hipBLASLt / rocBLAS
+# candidate on MI355X (tools/tune_gemms.sh, C5=1 for config 5; bit-identical
+# output; 0.12 vs 0.16-0.21 ms per layer at 262,144 rows, 0.99 vs 1.27 ms at
+# 2,097,152).
 # TunableOp is process-global state, so it is switched on only for the
 # duration of one of the file's own GEMM shapes (`_tuned_window`) and left as
 # the caller had it afterwards: every other GEMM of the process keeps the

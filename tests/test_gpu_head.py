@@ -36,6 +36,11 @@ CASES = [
     ("meshrir_k512", MESHRIR, 16, 8, 64, 1022, 512, 2),
     ("simu_long_k512", SIMU, 8, 4, 48, 4094, 512, 1),
     ("ragged_k512", dict(MESHRIR, xyz_min=0, xyz_max=10), 5, 3, 40, 510, 512, 3),
+    # short items: one and two 64-t tiles per work item (the shape class that
+    # corrupted the round-4 bf16x3 DFT), oracle parity + repeats
+    # (a lower fs keeps the receiver delay within the short IR's path-loss table)
+    ("one_tile_k512", dict(MESHRIR, fs=4000), 6, 5, 32, 62, 512, 2),
+    ("two_tiles_k512", dict(MESHRIR, fs=6000, xyz_min=0, xyz_max=10), 7, 4, 24, 126, 512, 3),
     # ray counts for every form of the delay sort: 1154 rays (config 4's
     # RAF-E sphere) sort 2048 keys, 2562 rays 4096 keys, 8 keys per thread /
     # 16 keys per thread in registers (650 and 1024 rays above: 4)

@@ -17,21 +17,25 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_results_file_format():
     """Validators pin the libraries and gfx950; one entry per MLP dtype for
-    the config-2 inference shape (M = 262,144 rows, 512 -> 512)."""
+    the config-2 and config-5 inference shapes (M = 262,144 and 2,097,152
+    rows, 512 -> 512)."""
     rows = list(csv.reader(open(model._TUNED_FILE)))
     val = {r[1]: r[2] for r in rows if r[0] == "Validator"}
     assert val["GCN_ARCH_NAME"].startswith("gfx950")
     for k in ("PT_VERSION", "HIP_VERSION", "HIPBLASLT_VERSION", "ROCBLAS_VERSION"):
         assert k in val
-    ops = {r[0]: r[1:] for r in rows if r[0] != "Validator"}
+    ops = {(r[0], r[1]): r[2:] for r in rows if r[0] != "Validator"}
+    assert len(ops) == 4
     for dt in ("Half", "BFloat16"):
-        sig, sol, ms = ops[f"GemmAndBiasTunableOp_{dt}_TN"]
-        assert sig == "tn_512_262144_512_ld_512_512_512" and sol.startswith("Gemm_") and float(ms) > 0
+        for m in (262144, 2097152):
+            sol, ms = ops[(f"GemmAndBiasTunableOp_{dt}_TN", f"tn_512_{m}_512_ld_512_512_512")]
+            assert sol.startswith("Gemm_") and float(ms) > 0
 
 
 def test_tuned_shapes_parsed():
     """Only the file's own shapes take the TunableOp window."""
-    assert model._TUNED_SHAPES == {(torch.float16, 262144, 512, 512), (torch.bfloat16, 262144, 512, 512)}
+    assert model._TUNED_SHAPES == {(dt, m, 512, 512) for dt in (torch.float16, torch.bfloat16)
+                                   for m in (262144, 2097152)}  # configs 2 and 5
     x = torch.empty(1000, 512, dtype=torch.float16)
     w = torch.empty(512, 512, dtype=torch.float16)
     assert not model._tuned_gemm(x, w)  # shape not in the file: no device call at all
@@ -52,16 +56,18 @@ def _state():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("rows", [262144, 2097152], ids=["c2", "c5"])
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["fp16", "bf16"])
-def test_tuned_layer_bit_identical(dtype):
+def test_tuned_layer_bit_identical(dtype, rows):
     """relu(x W^T) through _LinearReLU with the shipped solution equals the
     default hipBLASLt solution's output bit for bit (TunableOp off), with the
-    tuned entry verifiably loaded, and TunableOp left as it was."""
+    tuned entry verifiably loaded, and TunableOp left as it was: config 2's
+    262,144 rows and config 5's 2,097,152."""
     if os.environ.get("AVR_TUNABLEOP", "1") == "0":
         pytest.skip("AVR_TUNABLEOP=0: the shipped solution is switched off")
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(3)
-    x = torch.relu(torch.randn(262144, 512, device=dev, generator=g)).to(dtype)
+    x = torch.relu(torch.randn(rows, 512, device=dev, generator=g)).to(dtype)
     w = torch.randn(512, 512, device=dev, generator=g) / 512 ** 0.5
     bias = torch.zeros(512, dtype=dtype, device=dev)
     before = _state()
@@ -70,7 +76,7 @@ def test_tuned_layer_bit_identical(dtype):
     assert model._enable_tuned_gemms(dev), "shipped TunableOp results rejected (validators?)"
     name = "Half" if dtype == torch.float16 else "BFloat16"
     res = {(r[0], r[1]): r[2] for r in torch.cuda.tunable.get_results()}
-    assert res.get((f"GemmAndBiasTunableOp_{name}_TN", "tn_512_262144_512_ld_512_512_512"), "").startswith(
+    assert res.get((f"GemmAndBiasTunableOp_{name}_TN", f"tn_512_{rows}_512_ld_512_512_512"), "").startswith(
         "Gemm_Hipblaslt_")
     assert model._tuned_gemm(x, w.to(dtype))
     with torch.no_grad():

@@ -8,7 +8,14 @@ OUT=gpurun_out/tune
 mkdir -p $OUT
 export TMPDIR=/tmp
 rm -f $OUT/tunableop_gfx950*.csv
-# TRAIN=1: only the training shapes, added to the shipped inference results
+# TRAIN=1: only the training shapes, added to the shipped inference results;
+# C5=1: only config 5's (2,097,152-row width-512 layers, fp16), likewise
+if [ "${C5:-0}" = 1 ]; then
+  cp avr_amd/tunableop_gfx950.csv $OUT/tunableop_gfx950.csv
+  (export PYTORCH_TUNABLEOP_ENABLED=1 PYTORCH_TUNABLEOP_TUNING=1 PYTORCH_TUNABLEOP_FILENAME=$OUT/tunableop_gfx950.csv AVR_TUNABLEOP=0; timeout -k 10 900 python bench.py --mode ray-shard --network --mlp-dtype ${C5_DTYPE:-fp16} --steps 1 --warmup 1 --no-cpu-baseline) > $OUT/tune_c5.log 2>&1 || { tail -20 $OUT/tune_c5.log; exit 1; }
+  cat $OUT/tunableop_gfx950*.csv
+  exit 0
+fi
 [ "${TRAIN:-0}" = 1 ] && cp avr_amd/tunableop_gfx950.csv $OUT/tunableop_gfx950.csv
 for dt in fp16 bf16; do
   [ "${TRAIN:-0}" = 1 ] && break
