@@ -6,7 +6,7 @@ set -u
 OUT=${1:-gpurun_out/pmc_infer}
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD="python tools/bench_infer.py --mlp-dtype fp16 --variants fused --steps 4 --warmup 2"
+CMD=${PMC_CMD:-"python tools/bench_infer.py --mlp-dtype fp16 --variants fused --steps 4 --warmup 2"}
 i=0
 for pass in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT" \
             "SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_WAVES" \
