@@ -164,6 +164,42 @@ def _mlp512x2(x, w1_master, w2_master, dtype):
     return y
 
 
+# One width-512 layer at inference on the hand-written GEMM (csrc/linear512.hip)
+# instead of hipBLASLt (AVR_LINEAR512=1).
+_LINEAR512 = os.environ.get("AVR_LINEAR512", "0") == "1"
+
+
+def _linear512_ok(x, lin, dtype):
+    return (_LINEAR512 and x.is_cuda and not torch.is_grad_enabled() and dtype in (torch.float16, torch.bfloat16)
+            and x.dim() == 2 and x.size(1) == 512 and tuple(lin.weight.shape) == (512, 512) and x.size(0) >= 1)
+
+
+def _linear512(x, w_master, dtype):
+    """relu(x W^T) for x [M, 512] on csrc/linear512.hip; the packed weight is
+    cached on the master weight, keyed by its storage and version (bypassed
+    while a HIP graph is captured, wcache.capturing)."""
+    import ctypes
+
+    from . import _lib
+
+    x = x.to(dtype).contiguous()
+    code = _lib.DTYPE_F16 if dtype == torch.float16 else _lib.DTYPE_BF16
+    st = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    key = (w_master.data_ptr(), w_master._version, code)
+    use_cache = not capturing()
+    wf = cache_lookup(w_master, "_avr_linear512", key) if use_cache else None
+    if wf is None:
+        w = cast_weight(w_master, dtype, use_cache).contiguous()
+        wf = torch.empty(512, 512, dtype=dtype, device=x.device)
+        _lib.call("avr_linear512_pack_w", ctypes.c_void_p(w.data_ptr()), code, ctypes.c_void_p(wf.data_ptr()), st)
+        if use_cache:
+            cache_store(w_master, "_avr_linear512", key, wf)
+    y = torch.empty_like(x)
+    _lib.call("avr_linear512_relu_fwd", x.size(0), ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(wf.data_ptr()),
+              code, ctypes.c_void_p(y.data_ptr()), st)
+    return y
+
+
 # hipBLASLt's solutions for the width-512 layers at config-2 and config-5
 # inference, picked by PyTorch TunableOp over every hipBLASLt / rocBLAS
 # candidate on MI355X (tools/tune_gemms.sh, C5=1 for config 5; bit-identical
@@ -321,7 +357,10 @@ class MLP(nn.Module):
                 x = _mlp512x2(x, hid[i].weight, hid[i + 1].weight, self.dtype)
                 i += 2
                 continue
-            x = _LinearReLU.apply(x, hid[i].weight, self.dtype, not torch.is_grad_enabled())
+            if _linear512_ok(x, hid[i], self.dtype):
+                x = _linear512(x, hid[i].weight, self.dtype)
+            else:
+                x = _LinearReLU.apply(x, hid[i].weight, self.dtype, not torch.is_grad_enabled())
             i += 1
         return x
 

@@ -313,6 +313,16 @@ int avr_hashgrid_bwd_partitioned_set(int64_t N, int32_t n_levels, const float* x
  * avr_runner.py:190).  Split-K over n: `workspace` holds splits*M*K fp32
  * partials (splits from avr_linear_wgrad_splits), summed deterministically. */
 int avr_linear_wgrad_splits(int64_t N, int32_t M, int32_t K, int32_t* splits);
+/* One width-512 hidden layer at inference, y = relu(x W^T): x, y [M][512],
+ * W [512][512] (out x in), 16-bit (AVR_DTYPE_F16 / AVR_DTYPE_BF16), fp32
+ * accumulation, one rounding of the output (model.py:176-180, tcnn
+ * CutlassMLP).  Replaces the hipBLASLt GEMM with ReLU epilogue the per-layer
+ * path runs (torch._addmm_activation).  avr_linear512_pack_w lays W out in
+ * MFMA fragment order into Wf (512 KiB, 16-byte aligned), once per weight
+ * version; x, y 16-byte aligned. */
+int avr_linear512_pack_w(const void* W, int32_t dtype, void* Wf, void* stream);
+int avr_linear512_relu_fwd(int64_t M, const void* x, const void* Wf, int32_t dtype, void* y, void* stream);
+
 /* Two consecutive width-512 hidden layers of the signal network in one
  * launch (model.py:176-180, AVRModel's `_model_signal` layers 1 and 2 at
  * inference): y = relu(relu(x W1^T) W2^T), x / y [M][512], W1 / W2 [512][512]

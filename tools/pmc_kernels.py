@@ -11,7 +11,7 @@ import os
 import statistics
 import sys
 
-KEYS = ("hashgrid_fwd_lm", "sigma_meshrir_h1", "head_exact_kernel", "Cijk", "ray_reduce", "dft_phase",
+KEYS = ("hashgrid_fwd_lm", "sigma_meshrir_h1", "head_exact_kernel", "Cijk", "ray_reduce", "dft_phase", "linear512",
         "linear_xs", "hashgrid")
 
 
