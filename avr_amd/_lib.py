@@ -137,6 +137,8 @@ _SIGS = {
     "avr_linear_wgrad_splits": (ctypes.c_int, [_c_i64, _c_i32, _c_i32, _vp]),
     "avr_linear512_pack_w": (ctypes.c_int, [_vp, _c_i32, _vp, _vp]),
     "avr_linear512_relu_fwd": (ctypes.c_int, [_c_i64, _vp, _vp, _c_i32, _vp, _vp]),
+    "avr_linear512_pack_w2": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp, _vp]),
+    "avr_linear512_mask_fwd": (ctypes.c_int, [_c_i64, _vp, _vp, _c_i32, _vp, _vp, _vp]),
     "avr_mlp512x2_pack_w": (ctypes.c_int, [_vp, _vp, _c_i32, _vp, _vp]),
     "avr_mlp512x2_fwd": (ctypes.c_int, [_c_i64, _vp, _vp, _c_i32, _vp, _vp]),
     "avr_linear_wgrad": (ctypes.c_int, [_c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i32, _vp, _vp]),

@@ -119,10 +119,25 @@ __device__ __forceinline__ uint32_t relu_pack(float a, float b) {
     return pack16<E>(__builtin_elementwise_maximum(a, 0.0f), __builtin_elementwise_maximum(b, 0.0f));
 }
 
+// v's 16-bit halves where m's are not <= 0 (threshold_backward's test,
+// `m <= 0 ? 0 : v`: +0, -0 and the negatives down to -inf zero it; positives,
+// +inf and every NaN keep v)
 template <typename E>
+__device__ __forceinline__ uint32_t keep_where_positive(uint32_t v, uint32_t m) {
+    constexpr uint32_t kInf = std::is_same<E, __half>::value ? 0x7c00u : 0x7f80u;
+    const uint32_t lo = m & 0xffffu, hi = m >> 16;
+    const bool zlo = lo == 0u || lo - 0x8000u <= kInf, zhi = hi == 0u || hi - 0x8000u <= kInf;
+    return (zlo ? 0u : (v & 0xffffu)) | (zhi ? 0u : (v & 0xffff0000u));
+}
+
+// kMask = false: y = relu(x W^T).  kMask = true: y = (x W^T) where
+// mask > 0, else 0 (mask [M][512] of E, y's shape): a ReLU layer's data
+// gradient with the input ReLU's backward fused, gx = (g W) . [x > 0], with
+// Wf packed from W^T (avr_linear512_pack_w with transpose = 1)
+template <typename E, bool kMask>
 __global__ __launch_bounds__(512, 1) void linear512_relu_kernel(int64_t M, const E* __restrict__ x,
                                                                 const frag8* __restrict__ Wf, E* __restrict__ y,
-                                                                int ntiles, int nrt) {
+                                                                int ntiles, int nrt, const E* __restrict__ mask) {
     extern __shared__ __attribute__((aligned(16))) char lds_l[];
     const int lane = threadIdx.x & 63, half = lane >> 5, j = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -255,15 +270,34 @@ __global__ __launch_bounds__(512, 1) void linear512_relu_kernel(int64_t M, const
         const int64_t nrows = std::max<int64_t>(0, std::min<int64_t>(128, M - r0));
         const __amdgpu_buffer_rsrc_t yres = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(y + r0 * kLK), (short)0, (int)(nrows * kLK * 2), 0x00020000);
+        __amdgpu_buffer_rsrc_t mres;
+        if constexpr (kMask)
+            mres = __builtin_amdgcn_make_buffer_rsrc((void*)(mask + r0 * kLK), (short)0, (int)(nrows * kLK * 2),
+                                                     0x00020000);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+            frag8 mk[4];
+            if constexpr (kMask) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int row = 8 * u + (lane >> 3), ch = lane & 7;
+                    mk[u] = __builtin_amdgcn_raw_buffer_load_b128(
+                        mres, ((32 * q + row) * kLK + kLTileCols * nh + 64 * wc + 8 * ch) * 2, 0, 0);
+                }
+            }
 #pragma unroll
             for (int a = 0; a < 2; ++a) {
 #pragma unroll
                 for (int gg = 0; gg < 4; ++gg) {
                     const f32x16& v = acc[a][q];
-                    const uint32_t w0 = relu_pack<E>(v[4 * gg], v[4 * gg + 1]);
-                    const uint32_t w1 = relu_pack<E>(v[4 * gg + 2], v[4 * gg + 3]);
+                    uint32_t w0, w1;
+                    if constexpr (kMask) {
+                        w0 = pack16<E>(v[4 * gg], v[4 * gg + 1]);
+                        w1 = pack16<E>(v[4 * gg + 2], v[4 * gg + 3]);
+                    } else {
+                        w0 = relu_pack<E>(v[4 * gg], v[4 * gg + 1]);
+                        w1 = relu_pack<E>(v[4 * gg + 2], v[4 * gg + 3]);
+                    }
                     const int ch = (4 * a + gg) ^ (j & 7);
                     *reinterpret_cast<u32x2*>(stage + j * 128 + ch * 16 + 8 * half) = u32x2{w0, w1};
                 }
@@ -272,7 +306,11 @@ __global__ __launch_bounds__(512, 1) void linear512_relu_kernel(int64_t M, const
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int row = 8 * u + (lane >> 3), ch = lane & 7;
-                const frag8 v = *reinterpret_cast<const frag8*>(stage + row * 128 + ((ch ^ (row & 7)) * 16));
+                frag8 v = *reinterpret_cast<const frag8*>(stage + row * 128 + ((ch ^ (row & 7)) * 16));
+                if constexpr (kMask) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = keep_where_positive<E>(v[e], mk[u][e]);
+                }
                 if (!(AVR_L512_DBG & 4) || M < 0)
                     __builtin_amdgcn_raw_buffer_store_b128(
                         v, yres, ((32 * q + row) * kLK + kLTileCols * nh + 64 * wc + 8 * ch) * 2, 0, 0);
@@ -287,33 +325,45 @@ __global__ __launch_bounds__(512, 1) void linear512_relu_kernel(int64_t M, const
 // 32-column tile ct, the 64 lanes' A fragments of v_mfma_f32_32x32x16 (lane
 // (j, half): W[256 nh + 32 ct + j][kLKC c + 16 s + 8 half + 0..7]) contiguous
 __global__ __launch_bounds__(256) void linear512_pack_kernel(const uint16_t* __restrict__ W, frag8* __restrict__ Wf,
-                                                             int64_t n) {
+                                                             int64_t n, int transpose) {
     for (int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         const int lane = (int)(i & 63);
         const int64_t f = i >> 6;  // fragment index ((nh * kLChunks + c) * kLKS + s) * 8 + ct
         const int ct = (int)(f & 7), s = (int)((f >> 3) % kLKS), c = (int)((f >> 3) / kLKS % kLChunks),
                   nh = (int)(f >> 8);
         const int row = 256 * nh + 32 * ct + (lane & 31), k = kLKC * c + 16 * s + 8 * (lane >> 5);
-        Wf[i] = *reinterpret_cast<const frag8*>(W + (int64_t)row * kLK + k);
+        if (transpose) {  // fragments of W^T: W[k + 0..7][row], gathered
+            uint16_t h[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) h[e] = W[(int64_t)(k + e) * kLK + row];
+            Wf[i] = frag8{h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16, h[4] | (uint32_t)h[5] << 16,
+                          h[6] | (uint32_t)h[7] << 16};
+        } else {
+            Wf[i] = *reinterpret_cast<const frag8*>(W + (int64_t)row * kLK + k);
+        }
     }
 }
 
 }  // namespace
 
 extern "C" int avr_linear512_pack_w(const void* W, int32_t dtype, void* Wf, void* stream) {
-    AVR_REQUIRE(W && Wf, "avr_linear512_pack_w: bad args");
+    return avr_linear512_pack_w2(W, dtype, 0, Wf, stream);
+}
+
+extern "C" int avr_linear512_pack_w2(const void* W, int32_t dtype, int32_t transpose, void* Wf, void* stream) {
+    AVR_REQUIRE(W && Wf && (transpose == 0 || transpose == 1), "avr_linear512_pack_w: bad args");
     AVR_REQUIRE(dtype == AVR_DTYPE_F16 || dtype == AVR_DTYPE_BF16, "avr_linear512_pack_w: fp16 or bf16");
     AVR_REQUIRE(reinterpret_cast<uintptr_t>(W) % 16 == 0 && reinterpret_cast<uintptr_t>(Wf) % 16 == 0,
                 "avr_linear512_pack_w: W and Wf must be 16-byte aligned");
     const int64_t n = (int64_t)kLK * kLK / 8;  // 16-byte fragments rows
     hipLaunchKernelGGL(linear512_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream),
-                       (const uint16_t*)W, (frag8*)Wf, n);
+                       (const uint16_t*)W, (frag8*)Wf, n, (int)transpose);
     return check_launch("avr_linear512_pack_w");
 }
 
-extern "C" int avr_linear512_relu_fwd(int64_t M, const void* x, const void* Wf, int32_t dtype, void* y,
-                                      void* stream) {
-    AVR_REQUIRE(M >= 1 && x && Wf && y, "avr_linear512_relu_fwd: bad args");
+namespace {
+int linear512_launch(int64_t M, const void* x, const void* Wf, int32_t dtype, const void* mask, void* y,
+                     void* stream) {
     AVR_REQUIRE(dtype == AVR_DTYPE_F16 || dtype == AVR_DTYPE_BF16, "avr_linear512_relu_fwd: fp16 or bf16 operands");
     AVR_REQUIRE(reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(Wf) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(y) % 16 == 0,
@@ -330,16 +380,29 @@ extern "C" int avr_linear512_relu_fwd(int64_t M, const void* x, const void* Wf, 
     // that block b's tiles and block b + 8's are a row tile's two halves
     const int64_t g = std::min<int64_t>(ntiles, std::max(16, cus / 16 * 16));
     hipStream_t st = as_stream(stream);
-    auto go = [&](auto e_tag) {
+    auto go = [&](auto e_tag, auto m_tag) {
         using E = decltype(e_tag);
-        auto kern = linear512_relu_kernel<E>;
+        auto kern = linear512_relu_kernel<E, decltype(m_tag)::value>;
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kLLds);
         hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(512), kLLds, st, M, (const E*)x, (const frag8*)Wf, (E*)y,
-                           (int)ntiles, (int)nrt);
+                           (int)ntiles, (int)nrt, (const E*)mask);
     };
     if (dtype == AVR_DTYPE_F16)
-        go(__half{});
+        mask ? go(__half{}, std::true_type{}) : go(__half{}, std::false_type{});
     else
-        go(__hip_bfloat16{});
-    return check_launch("avr_linear512_relu_fwd");
+        mask ? go(__hip_bfloat16{}, std::true_type{}) : go(__hip_bfloat16{}, std::false_type{});
+    return check_launch(mask ? "avr_linear512_mask_fwd" : "avr_linear512_relu_fwd");
+}
+}  // namespace
+
+extern "C" int avr_linear512_relu_fwd(int64_t M, const void* x, const void* Wf, int32_t dtype, void* y,
+                                      void* stream) {
+    return linear512_launch(M, x, Wf, dtype, nullptr, y, stream);
+}
+
+extern "C" int avr_linear512_mask_fwd(int64_t M, const void* x, const void* Wf, int32_t dtype, const void* mask,
+                                      void* y, void* stream) {
+    AVR_REQUIRE(mask && reinterpret_cast<uintptr_t>(mask) % 16 == 0,
+                "avr_linear512_mask_fwd: mask must be non-null and 16-byte aligned");
+    return linear512_launch(M, x, Wf, dtype, mask, y, stream);
 }

@@ -11,14 +11,17 @@
 //
 // Split-K MFMA kernel: a 256-thread workgroup owns a 128 x 128 tile of dW and
 // a range of n; four waves each compute 64 x 64 with v_mfma_f32_32x32x16_bf16.
-// Both operands are stored n-major (the reduction index is the ROW), so the
-// 32-row slabs are staged row-major in LDS (16-byte coalesced loads, the next
-// slab's loads in flight under the current slab's MFMAs) and read back with
+// Both operands are stored n-major (the reduction index is the ROW), so
+// 32-row slabs are kept row-major in LDS and read back with
 // ds_read_b64_tr_b16, the CDNA4 transposing LDS read, which hands each lane
 // 4 consecutive rows of one column.  The image is XOR-swizzled per 16-byte
 // chunk (cdna_hip_programming.md T10 image (b)) so those reads are
-// conflict-free.  fp32 partials per n-range are summed in a fixed order by a
-// second kernel (deterministic).
+// conflict-free.  The slabs stream into a four-slot LDS ring by LDS-DMA
+// (global_load_lds_dwordx4): three slabs in flight per workgroup, one
+// barrier per slab (round 5; the round-1..4 form staged one slab through
+// registers with two barriers per slab and was bitwise equal and 14-30 %
+// slower, tools/bench_wgrad.py).  fp32 partials per n-range are summed in a
+// fixed order by a second kernel (deterministic).
 #include "common.h"
 
 #include <stdlib.h>
@@ -31,7 +34,6 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
 constexpr int kTile = 128;   // dW tile edge (both m and k)
 constexpr int kSlab = 32;    // rows of n per LDS slab
@@ -47,75 +49,81 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds_base, int byte_off) {
         (__attribute__((address_space(3))) s16x4*)(lds_base + byte_off));
 }
 
-// Block -> (split, tile): with xcd_map, block id b runs on XCD b % 8 and
-// all tiles of a split go to the same XCD (split = b % 8 + 8 * (b / 8 / tiles)),
-// so the split's row range of gy and x is read from HBM/MALL once into that
-// XCD's L2 and re-read from there by its other tiles; otherwise tiles are
-// fastest (each split's tiles spread over all XCDs).
-__global__ __launch_bounds__(256) void linear_wgrad_kernel(int64_t N, int M, int K, int64_t rows_per_split,
-                                                            int used, int xcd_map,
-                                                            const __hip_bfloat16* __restrict__ gy,
-                                                            const __hip_bfloat16* __restrict__ x,
-                                                            float* __restrict__ partial) {
-    __shared__ __attribute__((aligned(16))) char lds[2 * kImg];  // [A image][B image]
+// Each DMA instruction fills 4 image rows (1 KiB, lane l at byte 16 l): lane
+// l of rows 4j .. 4j+3 fetches the logical chunk that img_off places at its
+// physical chunk (the XOR swizzle is an involution).  Rows past the split's
+// end read a zero row in device memory.
+__device__ __attribute__((aligned(16))) uint32_t g_wgrad_zero_row[64];  // 256 B of zeros (.bss)
+
+__device__ __forceinline__ void wg_dma16(const void* g, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(g)
+                 : "memory", "m0");
+}
+
+// s_waitcnt vmcnt(n), n in {0, 4, 8} (expcnt / lgkmcnt not waited on)
+#define AVR_WG_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 0xF) | (0x7 << 4) | (0xF << 8) | (((N) >> 4) << 14))
+__device__ __forceinline__ void wg_wait_slabs(int ahead) {
+    if (ahead >= 2)
+        AVR_WG_VMCNT(8);
+    else if (ahead == 1)
+        AVR_WG_VMCNT(4);
+    else
+        AVR_WG_VMCNT(0);
+}
+
+constexpr int kWgSlots = 4;  // ring slots of one slab (A and B images, 16 KiB)
+
+__global__ __launch_bounds__(256) void linear_wgrad_dma_kernel(int64_t N, int M, int K, int64_t rows_per_split,
+                                                                int used, const __hip_bfloat16* __restrict__ gy,
+                                                                const __hip_bfloat16* __restrict__ x,
+                                                                float* __restrict__ partial) {
+    __shared__ __attribute__((aligned(1024))) char lds[kWgSlots * 2 * kImg];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tiles_k = (K + kTile - 1) / kTile;
     const int tiles = tiles_k * ((M + kTile - 1) / kTile);
     const int b = blockIdx.x;
-    int tile, split;
-    if (xcd_map) {
-        tile = (b >> 3) % tiles;
-        split = (b & 7) + 8 * ((b >> 3) / tiles);
-    } else {
-        tile = b % tiles;
-        split = b / tiles;
-    }
+    // block b runs on XCD b % 8; all tiles of a split go to the same XCD, so
+    // the split's rows are read from HBM once into that XCD's L2
+    const int tile = (b >> 3) % tiles;
+    const int split = (b & 7) + 8 * ((b >> 3) / tiles);
     if (split >= used) return;  // padding blocks of the XCD map (block-uniform)
     const int m0 = (tile / tiles_k) * kTile, k0 = (tile % tiles_k) * kTile;
     const int64_t n_begin = (int64_t)split * rows_per_split;
     const int64_t n_end = min(N, n_begin + rows_per_split);
+    const int nslab = (int)((n_end - n_begin + kSlab - 1) / kSlab);
 
-    // staging: thread -> chunks q = tid + 256u (u = 0, 1): row q/16, chunk q%16
-    u32x4v ra[2], rb[2];
-    int srow[2], sch[2];
+    // this wave's DMA instructions: image rows 4j .. 4j+3, j = 2 wave + u, of
+    // both operands; lane l -> row 4j + l/16, physical chunk l%16
+    const uint32_t lds_base = (uint32_t)(uintptr_t)lds;
+    int drow[2], acol[2], bcol[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        const int q = tid + 256 * u;
-        srow[u] = q >> 4;
-        sch[u] = q & 15;
+        const int row = 4 * (2 * wave + u) + (lane >> 4);
+        const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        drow[u] = row;
+        // columns past M / K clamped to a valid chunk (never stored)
+        acol[u] = min(m0 + 8 * ch, M - 8);
+        bcol[u] = min(k0 + 8 * ch, K - 8);
     }
-    // columns past M / K are clamped to a valid chunk: they only feed dW rows
-    // / columns that are never stored
-    const int64_t acol0 = min(m0 + 8 * sch[0], M - 8), acol1 = min(m0 + 8 * sch[1], M - 8);
-    const int64_t bcol0 = min(k0 + 8 * sch[0], K - 8), bcol1 = min(k0 + 8 * sch[1], K - 8);
-    auto issue = [&](int64_t n0) {
+    auto issue = [&](int s) {
+        const uint32_t slot = lds_base + (uint32_t)((s % kWgSlots) * 2 * kImg);
+        const int64_t n0 = n_begin + (int64_t)s * kSlab;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int64_t n = min(n0 + srow[u], n_end - 1);
-            const int64_t ac = u ? acol1 : acol0, bc = u ? bcol1 : bcol0;
-            ra[u] = *reinterpret_cast<const u32x4v*>(gy + n * M + ac);
-            rb[u] = *reinterpret_cast<const u32x4v*>(x + n * K + bc);
-        }
-    };
-    auto commit = [&](int64_t n0) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            // rows past the split's end contribute zero
-            const bool ok = n0 + srow[u] < n_end;
-            const u32x4v z = {0u, 0u, 0u, 0u};
-            const int off = img_off(srow[u], sch[u]);
-            *reinterpret_cast<u32x4v*>(lds + off) = ok ? ra[u] : z;
-            *reinterpret_cast<u32x4v*>(lds + kImg + off) = ok ? rb[u] : z;
+            const int64_t n = n0 + drow[u];
+            const bool ok = n < n_end;
+            const void* ga = ok ? (const void*)(gy + n * M + acol[u]) : (const void*)g_wgrad_zero_row;
+            const void* gb = ok ? (const void*)(x + n * K + bcol[u]) : (const void*)g_wgrad_zero_row;
+            const uint32_t off = (uint32_t)(1024 * (2 * wave + u));
+            wg_dma16(ga, __builtin_amdgcn_readfirstlane(slot + off));
+            wg_dma16(gb, __builtin_amdgcn_readfirstlane(slot + kImg + off));
         }
     };
 
-    // transposed-read addresses: lane = 16g + 4q + p; group g takes columns
-    // 16(g&1) .. +15 of a 32-column block and rows 8(g>>1) .. +7 of a 16-row
-    // half-slab; lane 4q+p points at row r0+q, columns c0+4p .. c0+4p+3
     const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
     const int wm = wave & 1, wk = wave >> 1;
     auto tr_addr = [&](int colblock, int kh, int second) {
-        const int c0 = colblock + 16 * (g & 1);       // element column of the group
+        const int c0 = colblock + 16 * (g & 1);
         const int row = 16 * kh + 8 * (g >> 1) + 4 * second + qq;
         return img_off(row, (c0 >> 3) + (pp >> 1)) + 8 * (pp & 1);
     };
@@ -138,23 +146,26 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(int64_t N, int M, int
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-    if (n_begin < n_end) issue(n_begin);
-    for (int64_t n0 = n_begin; n0 < n_end; n0 += kSlab) {
+    for (int s = 0; s < kWgSlots - 1 && s < nslab; ++s) issue(s);
+    for (int s = 0; s < nslab; ++s) {
+        // this wave's DMA of slab s landed (slabs s+1, s+2 may still fly);
+        // the barrier makes every wave's landed and frees slot (s-1) % 4
+        wg_wait_slabs(min(kWgSlots - 2, nslab - 1 - s));
         __syncthreads();
-        commit(n0);
-        __syncthreads();
-        if (n0 + kSlab < n_end) issue(n0 + kSlab);  // next slab under the MFMAs
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + kWgSlots - 1 < nslab) issue(s + kWgSlots - 1);
+        const char* img = lds + (s % kWgSlots) * 2 * kImg;
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) {
             bf16x8 av[2], bv[2];
 #pragma unroll
             for (int blk = 0; blk < 2; ++blk) {
-                const s16x4 a0 = tr_read(lds, aoff[blk][kh][0]), a1 = tr_read(lds, aoff[blk][kh][1]);
-                const s16x4 b0 = tr_read(lds, boff[blk][kh][0]), b1 = tr_read(lds, boff[blk][kh][1]);
+                const s16x4 a0 = tr_read(img, aoff[blk][kh][0]), a1 = tr_read(img, aoff[blk][kh][1]);
+                const s16x4 b0 = tr_read(img, boff[blk][kh][0]), b1 = tr_read(img, boff[blk][kh][1]);
                 const s16x8 a = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-                const s16x8 b = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+                const s16x8 bb = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
                 av[blk] = __builtin_bit_cast(bf16x8, a);
-                bv[blk] = __builtin_bit_cast(bf16x8, b);
+                bv[blk] = __builtin_bit_cast(bf16x8, bb);
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i)
@@ -162,8 +173,8 @@ __global__ __launch_bounds__(256) void linear_wgrad_kernel(int64_t N, int M, int
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);
     }
-    // D layout: row (reg&3) + 8*(reg>>2) + 4*(lane>>5), column lane&31
     float* out = partial + (int64_t)split * M * K;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -235,10 +246,11 @@ extern "C" int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* gra
     const int used = (int)((N + rows - 1) / rows);
     hipStream_t st = as_stream(stream);
     const int tiles = ((K + kTile - 1) / kTile) * ((M + kTile - 1) / kTile);
-    const int xcd_map = 1;  // all tiles of a split on one XCD (its rows re-read from that L2)
-    const int64_t blocks = xcd_map ? (int64_t)tiles * ((used + 7) / 8 * 8) : (int64_t)tiles * used;
-    hipLaunchKernelGGL(linear_wgrad_kernel, dim3((unsigned)blocks), dim3(256), 0, st, N, (int)M, (int)K, rows,
-                       used, xcd_map, (const __hip_bfloat16*)grad_y, (const __hip_bfloat16*)x, workspace);
+    // all tiles of a split on one XCD (its rows re-read from that L2): block
+    // b runs on XCD b % 8, split = b % 8 + 8 * (b / 8 / tiles)
+    const int64_t blocks = (int64_t)tiles * ((used + 7) / 8 * 8);
+    hipLaunchKernelGGL(linear_wgrad_dma_kernel, dim3((unsigned)blocks), dim3(256), 0, st, N, (int)M, (int)K, rows,
+                       used, (const __hip_bfloat16*)grad_y, (const __hip_bfloat16*)x, workspace);
     if (int e = check_launch("avr_linear_wgrad")) return e;
     const int64_t MK = (int64_t)M * K;
     int G = 1;

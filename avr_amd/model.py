@@ -291,15 +291,57 @@ def _tuned_gemm(x, w):
             and _enable_tuned_gemms(x.device))
 
 
+# The data gradient of a width-512 ReLU layer whose input is the previous
+# layer's ReLU output, with that ReLU's backward fused into the GEMM's
+# epilogue (csrc/linear512.hip, `avr_linear512_mask_fwd`); AVR_FUSED_DGRAD=0
+# keeps hipBLASLt + threshold_backward.
+_FUSED_DGRAD = os.environ.get("AVR_FUSED_DGRAD", "1") != "0"
+
+
+def _dgrad512_ok(x, w_master, dtype):
+    """x: the chain's input (device and grad mode); the layer's own input is
+    512 wide when its weight is 512 x 512."""
+    return (_FUSED_DGRAD and x.is_cuda and torch.is_grad_enabled() and dtype in (torch.float16, torch.bfloat16)
+            and x.dim() == 2 and tuple(w_master.shape) == (512, 512))
+
+
+def _dgrad512_masked(g, w, x):
+    """(g W) where x > 0, else 0, for g, x [N, 512] and W [512, 512] of the
+    16-bit type: threshold_backward(g @ W, x, 0) in one launch."""
+    import ctypes
+
+    from . import _lib
+
+    code = _lib.DTYPE_F16 if w.dtype == torch.float16 else _lib.DTYPE_BF16
+    st = ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)
+    w = w.contiguous()
+    wf = torch.empty(512, 512, dtype=w.dtype, device=g.device)
+    _lib.call("avr_linear512_pack_w2", ctypes.c_void_p(w.data_ptr()), code, 1, ctypes.c_void_p(wf.data_ptr()), st)
+    g = g.contiguous()
+    x = x.contiguous()
+    out = torch.empty_like(g)
+    _lib.call("avr_linear512_mask_fwd", g.size(0), ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(wf.data_ptr()),
+              code, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()), st)
+    return out
+
+
 class _LinearReLU(torch.autograd.Function):
     """y = relu(x W^T) with the ReLU in the GEMM epilogue: hipBLASLt's
     `_addmm_activation` with a zero bias (one kernel instead of GEMM + an
     elementwise pass over the [N, width] activation, bit-identical output).
     The backward is ReLU's own (threshold on the saved output), then the
-    same data / weight gradients as `_Linear`."""
+    same data / weight gradients as `_Linear`.
+
+    In a chain of such layers (`MLP.hidden`) two flags move each ReLU's
+    backward into the GEMM that produces its gradient: `mask_gx` (x is the
+    previous layer's ReLU output and this layer its only consumer) returns
+    the data gradient already masked by x > 0 (`_dgrad512_masked`), and
+    `gy_masked` (the consumer of y did so) skips the threshold.  The mask is
+    the same selection threshold_backward makes (y > 0 with y = the next
+    layer's x), applied to the same rounded values."""
 
     @staticmethod
-    def forward(ctx, x, w_master, dtype, cache=False):
+    def forward(ctx, x, w_master, dtype, cache=False, mask_gx=False, gy_masked=False):
         w = cast_weight(w_master, dtype, cache)
         if x.is_cuda:
             bias = _zero_bias(w.size(0), dtype, x.device)
@@ -311,15 +353,18 @@ class _LinearReLU(torch.autograd.Function):
         else:
             y = torch.relu(x @ w.t())
         ctx.save_for_backward(x, w, y)
+        ctx.mask_gx, ctx.gy_masked = mask_gx, gy_masked
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
-        g = torch.ops.aten.threshold_backward(gy, y, 0).contiguous()
-        gx = g @ w if ctx.needs_input_grad[0] else None
+        g = gy.contiguous() if ctx.gy_masked else torch.ops.aten.threshold_backward(gy, y, 0).contiguous()
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = _dgrad512_masked(g, w, x) if ctx.mask_gx else g @ w
         gw = _wgrad(g, x) if ctx.needs_input_grad[1] else None
-        return gx, gw, None, None
+        return gx, gw, None, None, None, None
 
 
 class MLP(nn.Module):
@@ -341,8 +386,13 @@ class MLP(nn.Module):
         """All layers but the last (each followed by ReLU): the features the
         output layer is applied to."""
         x = x.to(self.dtype).contiguous()
-        for lin in self.layers[:-1]:
-            x = _LinearReLU.apply(x, lin.weight, self.dtype, not torch.is_grad_enabled())
+        hid = list(self.layers[:-1])
+        # layer i >= 1 takes layer i-1's ReLU output only: its data gradient
+        # can carry that ReLU's backward (_LinearReLU's flags)
+        fuse = [i > 0 and _dgrad512_ok(x, lin.weight, self.dtype) for i, lin in enumerate(hid)]
+        for i, lin in enumerate(hid):
+            x = _LinearReLU.apply(x, lin.weight, self.dtype, not torch.is_grad_enabled(), fuse[i],
+                                  i + 1 < len(hid) and fuse[i + 1])
         return x
 
     def hidden_from(self, x, start):

@@ -322,6 +322,18 @@ int avr_linear_wgrad_splits(int64_t N, int32_t M, int32_t K, int32_t* splits);
  * version; x, y 16-byte aligned. */
 int avr_linear512_pack_w(const void* W, int32_t dtype, void* Wf, void* stream);
 int avr_linear512_relu_fwd(int64_t M, const void* x, const void* Wf, int32_t dtype, void* y, void* stream);
+/* avr_linear512_pack_w with transpose = 1 packs W^T (for a data gradient,
+ * g W = g (W^T)^T); transpose = 0 is avr_linear512_pack_w. */
+int avr_linear512_pack_w2(const void* W, int32_t dtype, int32_t transpose, void* Wf, void* stream);
+/* The data gradient of a ReLU layer whose input x is itself a ReLU output
+ * consumed only by this layer, with that ReLU's backward fused:
+ * y = 0 where mask <= 0, else x Wf^T (threshold_backward's selection: NaN
+ * keeps the value; mask, y [M][512], mask = the layer's
+ * input activation, Wf packed from W^T).  Replaces `grad @ W` (hipBLASLt) +
+ * threshold_backward(., x, 0) in the MLP backward (tcnn's fused MLP
+ * backward, model.py:21-31, through avr_runner.py:190). */
+int avr_linear512_mask_fwd(int64_t M, const void* x, const void* Wf, int32_t dtype, const void* mask, void* y,
+                           void* stream);
 
 /* Two consecutive width-512 hidden layers of the signal network in one
  * launch (model.py:176-180, AVRModel's `_model_signal` layers 1 and 2 at

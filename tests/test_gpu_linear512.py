@@ -94,3 +94,74 @@ def test_mlp_hidden_on_linear512_matches_hipblaslt(dtype, monkeypatch):
     a, b = outs
     rel = float((a - b).norm() / b.norm())
     assert float(b.norm()) > 0 and rel < 1e-2, rel
+
+
+# ---- the masked data gradient (avr_linear512_mask_fwd, W^T packing) ----
+
+def _run_mask(g, w, mask):
+    """0 where mask <= 0, else g W: W^T packed by avr_linear512_pack_w2."""
+    st = ctypes.c_void_p(torch.cuda.current_stream(DEV).cuda_stream)
+    wf = torch.empty(512, 512, dtype=g.dtype, device=DEV)
+    _lib.call("avr_linear512_pack_w2", ctypes.c_void_p(w.data_ptr()), CODE[g.dtype], 1,
+              ctypes.c_void_p(wf.data_ptr()), st)
+    y = torch.full_like(g, float("nan"))
+    _lib.call("avr_linear512_mask_fwd", g.size(0), ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(wf.data_ptr()),
+              CODE[g.dtype], ctypes.c_void_p(mask.data_ptr()), ctypes.c_void_p(y.data_ptr()), st)
+    return y
+
+
+def _mask_values(M, dtype, gen):
+    """Activations with every class threshold_backward distinguishes:
+    positive, +0, -0, negative, +inf, -inf, NaN, the smallest subnormal."""
+    m = torch.randn(M, 512, device=DEV, generator=gen).to(dtype)
+    specials = torch.tensor([0.0, -0.0, float("inf"), float("-inf"), float("nan"), -1.0], dtype=dtype, device=DEV)
+    tiny = torch.tensor([1], dtype=torch.int16, device=DEV).view(dtype)  # smallest positive subnormal
+    idx = torch.randint(0, 8, (M, 512), device=DEV, generator=gen)
+    for i in range(6):
+        m = torch.where(idx == i, specials[i], m)
+    return torch.where(idx == 6, tiny, m).contiguous()
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["fp16", "bf16"])
+@pytest.mark.parametrize("M", [1, 257, 2048 + 7, 83200])
+def test_masked_dgrad_exact_on_integer_operands(dtype, M):
+    """Small-integer g and W: g W exact in fp32, so the kernel equals
+    threshold_backward(g @ W, mask, 0) bit for bit, for every mask class."""
+    gen = torch.Generator(device=DEV).manual_seed(M + 11)
+    g = torch.randint(-2, 3, (M, 512), device=DEV, generator=gen).to(dtype)
+    w = torch.randint(-1, 2, (512, 512), device=DEV, generator=gen).to(dtype)
+    mask = _mask_values(M, dtype, gen)
+    y = _run_mask(g, w, mask)
+    torch.cuda.synchronize()
+    ref = torch.ops.aten.threshold_backward((g.float() @ w.float()).to(dtype), mask, 0)
+    assert torch.equal(y, ref), int((y != ref).sum())
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16], ids=["fp16", "bf16"])
+def test_mlp_training_chain_fused_dgrad(dtype, monkeypatch):
+    """MLP.hidden's backward with each ReLU's backward fused into the next
+    layer's data gradient (AVR_FUSED_DGRAD, the default) against the unfused
+    chain (hipBLASLt g @ W + threshold_backward): the same masks, fp32 sums in
+    another order; the fused kernel is the one that ran."""
+    from avr_amd import model
+
+    torch.manual_seed(2)
+    mlp = model.MLP(416, 64, {"n_neurons": 512, "n_hidden_layers": 4}, dtype=dtype).to(DEV)
+    x = torch.randn(20000, 416, device=DEV).to(dtype).requires_grad_(True)
+    calls = []
+    fn = model._dgrad512_masked
+    monkeypatch.setattr(model, "_dgrad512_masked", lambda *a: calls.append(1) or fn(*a))
+    r = torch.randn(20000, 64, device=DEV)  # loss weights: O(1) gradients (no 16-bit underflow)
+    grads = []
+    for on in (True, False):
+        monkeypatch.setattr(model, "_FUSED_DGRAD", on)
+        mlp.zero_grad(set_to_none=True)
+        x.grad = None
+        out = mlp(x)
+        (out.float() * r).sum().backward()
+        grads.append([x.grad.float().clone()] + [p.grad.clone() for p in mlp.parameters()])
+    torch.cuda.synchronize()
+    assert len(calls) == 3  # layers 1..3 (512 x 512), not the 416-wide first
+    for a, b in zip(*grads):
+        rel = float((a - b).norm() / b.norm())
+        assert float(b.norm()) > 0 and rel < 2e-2, rel

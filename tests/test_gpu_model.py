@@ -88,7 +88,8 @@ def test_ray_layout_grouped_encoding_matches_flat(cls):
 
 
 @pytest.mark.parametrize("N,M,K", [(83200, 512, 512), (83200, 1600, 512), (5003, 512, 336),
-                                   (300, 128, 80), (33, 8, 16), (147712, 256, 128)])
+                                   (300, 128, 80), (33, 8, 16), (147712, 256, 128), (147712, 512, 416),
+                                   (77, 136, 24)])
 def test_linear_wgrad_kernel_matches_fp32(N, M, K):
     """avr_linear_wgrad (split-K bf16 MFMA) against an fp32 GEMM of the same
     bf16 operands (products are exact in fp32; only the summation order
@@ -105,6 +106,20 @@ def test_linear_wgrad_kernel_matches_fp32(N, M, K):
     assert err < 5e-5, err
     # deterministic
     assert torch.equal(out, _wgrad_hip(gy, x))
+
+
+def test_linear_wgrad_exact_on_small_integers():
+    """Small-integer operands: every partial sum is an integer below 2^24, so
+    the fp32 result is exact whatever the order; equal to the int64 GEMM."""
+    from avr_amd.model import _wgrad_hip
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    N, M, K = 20011, 264, 200
+    gy = torch.randint(-3, 4, (N, M), device=DEV, generator=g)
+    x = torch.randint(-3, 4, (N, K), device=DEV, generator=g)
+    out = _wgrad_hip(gy.to(torch.bfloat16), x.to(torch.bfloat16))
+    ref = (gy.t().double() @ x.double()).to(torch.int64)
+    assert torch.equal(out.to(torch.int64), ref)
 
 
 @pytest.mark.parametrize("M", [1, 3])
