@@ -154,6 +154,8 @@ _SIGS = {
     "avr_head_bwd_workspace": (ctypes.c_int, [_vp, _c_i32, _c_i32, _c_i32, _vp]),
     "avr_head_bwd": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _c_i64, _vp]),
+    "avr_head_bwd2": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                     _c_i32, _vp, _vp, _vp, _vp, _c_i64, _vp]),
     "avr_criterion_window_len": (ctypes.c_int, []),
     "avr_criterion_workspace": (ctypes.c_int, [_c_i32, _c_i32, _vp]),
     "avr_criterion_fwd": (ctypes.c_int, [_c_i32, _c_i32] + [_vp] * 10 + [_c_i64, _vp]),

@@ -648,6 +648,11 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(avr_render_params pp
 }
 
 // ------------------------------------------------- backward: dL/dh, dL/dw
+// relu_mask: h is a ReLU output consumed only by the head, and grad_h leaves
+// with that ReLU's backward applied, threshold_backward(grad_h, h, 0)'s
+// selection (0 where h <= 0; NaN keeps), on the rounded value
+__device__ __forceinline__ bool relu_keeps(float hv) { return !(hv <= 0.0f); }
+
 // SB > 1 (16-bit h): each ray's h is loaded and its grad_h stored SB feature
 // blocks at a time (32 bytes per row for SB = 2) instead of 16 bytes per
 // block; the grad_h of the SB blocks waits packed in registers.
@@ -659,7 +664,7 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
                                                               const int32_t* __restrict__ delay,
                                                               const float* __restrict__ gz,
                                                               Th* __restrict__ grad_h,
-                                                              float* __restrict__ gw_part) {
+                                                              float* __restrict__ gw_part, int relu_mask) {
     extern __shared__ float Q[];  // [KB][QS]
     const int T = pp.T, S = pp.n_samples;
     const int QS = q_stride(T);
@@ -715,7 +720,7 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
 #pragma unroll
                         for (int k = 0; k < KB; ++k) {
                             const float q = Q[k * QS + d];
-                            gh[k] = wr * q;
+                            gh[k] = (!relu_mask || relu_keeps(hv[u][k])) ? wr * q : 0.0f;
                             acc = fmaf(hv[u][k], q, acc);
                         }
                         gw[u] = acc;
@@ -750,7 +755,9 @@ __global__ __launch_bounds__(kThreads) void head_bwd_h_kernel(avr_render_params 
                         const float q1 = live ? Q[(k + 1) * QS + d] : 0.0f;
                         acc = fmaf(hv[u][sb * KB + k], q0, acc);
                         acc = fmaf(hv[u][sb * KB + k + 1], q1, acc);
-                        ghp[u][sb * KB / 2 + k / 2] = pack16<Th>(live ? wr * q0 : 0.0f, live ? wr * q1 : 0.0f);
+                        const bool k0 = live && (!relu_mask || relu_keeps(hv[u][sb * KB + k]));
+                        const bool k1 = live && (!relu_mask || relu_keeps(hv[u][sb * KB + k + 1]));
+                        ghp[u][sb * KB / 2 + k / 2] = pack16<Th>(k0 ? wr * q0 : 0.0f, k1 ? wr * q1 : 0.0f);
                     }
                     if (live) gw[u] = acc;
                 }
@@ -1078,7 +1085,17 @@ extern "C" int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, co
                             const int32_t* perm, const float* ws, const int32_t* cnt, const float* gz,
                             void* grad_h, float* grad_w, float* grad_W, float* workspace,
                             int64_t workspace_bytes, void* stream) {
+    return avr_head_bwd2(p, B, K, h, W, dtype, w, delay, perm, ws, cnt, gz, 0, grad_h, grad_w, grad_W, workspace,
+                         workspace_bytes, stream);
+}
+
+extern "C" int avr_head_bwd2(const avr_render_params* p, int32_t B, int32_t K, const void* h,
+                             const void* W, int32_t dtype, const float* w, const int32_t* delay,
+                             const int32_t* perm, const float* ws, const int32_t* cnt, const float* gz,
+                             int32_t relu_mask, void* grad_h, float* grad_w, float* grad_W, float* workspace,
+                             int64_t workspace_bytes, void* stream) {
     if (int e = head_check(p, B, K, h, W, dtype)) return e;
+    AVR_REQUIRE(relu_mask == 0 || relu_mask == 1, "avr_head_bwd: relu_mask must be 0 or 1");
     AVR_REQUIRE(w && delay && perm && ws && cnt && gz && grad_h && grad_w && grad_W && workspace,
                 "avr_head_bwd: bad args");
     const int R = n_rays(*p), S = p->n_samples, T = p->T;
@@ -1115,7 +1132,7 @@ extern "C" int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, co
     auto go_h = [&](auto kern, auto hp, auto wp, auto gp) {
         allow_lds(kern, hs.lds_q);
         hipLaunchKernelGGL(kern, dim3(hs.n_kg, S, B), dim3(kThreads), hs.lds_q, st, *p, (int)B, R, (int)K,
-                           hs.kg, hp, wp, w, delay, gz, gp, gw_part);
+                           hs.kg, hp, wp, w, delay, gz, gp, gw_part, (int)relu_mask);
     };
     auto go_w = [&](auto kern, auto hp) {
         allow_lds(kern, hs.lds_c);

@@ -96,7 +96,7 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x, w_master, dtype, cache=False):
         w = cast_weight(w_master, dtype, cache)
         ctx.save_for_backward(x, w)
-        return x @ w.t()
+        return _mm_dgrad(x, w.t())  # (a g @ W-shaped GEMM: the tuned file's "NN" entries)
 
     @staticmethod
     def backward(ctx, gy):
@@ -107,7 +107,7 @@ class _Linear(torch.autograd.Function):
             # one output (sigma decoder's last layer): the K = 1 GEMM is an
             # outer product; the broadcast multiply rounds the same exact
             # fp32 products once, at write speed (hipBLASLt's K=1 tile: 2 TB/s)
-            gx = gy * w if w.size(0) == 1 else gy @ w
+            gx = gy * w if w.size(0) == 1 else _mm_dgrad(gy, w)
         gw = _wgrad(gy, x) if ctx.needs_input_grad[1] else None
         return gx, gw, None, None
 
@@ -200,11 +200,13 @@ def _linear512(x, w_master, dtype):
     return y
 
 
-# hipBLASLt's solutions for the width-512 layers at config-2 and config-5
-# inference, picked by PyTorch TunableOp over every hipBLASLt / rocBLAS
-# candidate on MI355X (tools/tune_gemms.sh, C5=1 for config 5; bit-identical
-# output; 0.12 vs 0.16-0.21 ms per layer at 262,144 rows, 0.99 vs 1.27 ms at
-# 2,097,152).
+# hipBLASLt / rocBLAS solutions picked by PyTorch TunableOp over every
+# candidate on MI355X (tools/tune_gemms.sh; bit-identical output to the
+# default solution, which only changes tiling): the width-512 layers at
+# config-2 and config-5 inference (0.12 vs 0.16-0.21 ms per layer at 262,144
+# rows, 0.99 vs 1.27 ms at 2,097,152; C5=1) and the MLP GEMMs of the config-3
+# and -4 training steps, forward and data gradient (TRAIN=1; e.g. the
+# 128 -> 80 data gradient 23 vs 40 us, 512 -> 416 73 vs 102 us at 83,200 rows).
 # TunableOp is process-global state, so it is switched on only for the
 # duration of one of the file's own GEMM shapes (`_tuned_window`) and left as
 # the caller had it afterwards: every other GEMM of the process keeps the
@@ -216,20 +218,29 @@ _TUNED = [None]  # None: not loaded yet; then True (entries loaded) or False
 
 
 def _tuned_shapes(path=_TUNED_FILE):
-    """(torch dtype, M, N, K) of the `_addmm_activation` entries in the file:
-    `GemmAndBiasTunableOp_<dtype>_TN,tn_<N>_<M>_<K>_...` for y[M,N] = x[M,K] W^T."""
+    """The file's GEMMs as (kind, torch dtype, rows, out, in):
+    kind "relu": `GemmAndBiasTunableOp_<dtype>_TN,tn_<out>_<rows>_<in>_...`,
+    y[rows, out] = relu(x[rows, in] W^T) (`_addmm_activation`);
+    kind "dgrad": `GemmTunableOp_<dtype>_NN,nn_<in>_<rows>_<out>_...`,
+    gx[rows, in] = g[rows, out] W[out, in] (`g @ W`)."""
     names = {"Half": torch.float16, "BFloat16": torch.bfloat16}
     out = set()
     if not os.path.exists(path):
         return out
     for line in open(path):
         f = line.strip().split(",")
-        if len(f) < 3 or not f[0].startswith("GemmAndBiasTunableOp_") or not f[1].startswith("tn_"):
+        if len(f) < 3 or f[2] == "Default":
             continue
-        dt = names.get(f[0][len("GemmAndBiasTunableOp_"):].rsplit("_", 1)[0])
-        n, m, k = (int(v) for v in f[1].split("_")[1:4])
-        if dt is not None:
-            out.add((dt, m, n, k))
+        if f[0].startswith("GemmAndBiasTunableOp_") and f[1].startswith("tn_"):
+            dt = names.get(f[0][len("GemmAndBiasTunableOp_"):].rsplit("_", 1)[0])
+            n, m, k = (int(v) for v in f[1].split("_")[1:4])
+            if dt is not None:
+                out.add(("relu", dt, m, n, k))
+        elif f[0].startswith("GemmTunableOp_") and f[0].endswith("_NN") and f[1].startswith("nn_"):
+            dt = names.get(f[0][len("GemmTunableOp_"):].rsplit("_", 1)[0])
+            m, n, k = (int(v) for v in f[1].split("_")[1:4])
+            if dt is not None:
+                out.add(("dgrad", dt, n, k, m))
     return out
 
 
@@ -280,15 +291,29 @@ def _enable_tuned_gemms(device):
     with _tuned_window():
         ok = bool(tun.read_file(_TUNED_FILE))
         loaded = {r[1] for r in tun.get_results()} if ok else set()
-    _TUNED[0] = ok and any(f"tn_{n}_{m}_{k}_" in s for _, m, n, k in _TUNED_SHAPES for s in loaded)
+    _TUNED[0] = ok and len(loaded) > 0
     return _TUNED[0]
 
 
 def _tuned_gemm(x, w):
     """True when relu(x W^T) is one of the shipped tuned shapes and the
     results loaded: the caller then runs the GEMM inside `_tuned_window`."""
-    return ((x.dtype, x.size(0), w.size(0), x.size(1)) in _TUNED_SHAPES and x.is_cuda
+    return (("relu", x.dtype, x.size(0), w.size(0), x.size(1)) in _TUNED_SHAPES and x.is_cuda
             and _enable_tuned_gemms(x.device))
+
+
+def _tuned_dgrad(g, w):
+    """As `_tuned_gemm` for the data gradient g @ W (g [rows, out], W [out, in])."""
+    return (("dgrad", g.dtype, g.size(0), w.size(0), w.size(1)) in _TUNED_SHAPES and g.is_cuda
+            and _enable_tuned_gemms(g.device))
+
+
+def _mm_dgrad(g, w):
+    """g @ W, inside the TunableOp window for the file's shapes."""
+    if _tuned_dgrad(g, w):
+        with _tuned_window():
+            return g @ w
+    return g @ w
 
 
 # The data gradient of a width-512 ReLU layer whose input is the previous
@@ -341,7 +366,7 @@ class _LinearReLU(torch.autograd.Function):
     layer's x), applied to the same rounded values."""
 
     @staticmethod
-    def forward(ctx, x, w_master, dtype, cache=False, mask_gx=False, gy_masked=False):
+    def forward(ctx, x, w_master, dtype, cache=False, mask_gx=False, gy_masked=False, link=None):
         w = cast_weight(w_master, dtype, cache)
         if x.is_cuda:
             bias = _zero_bias(w.size(0), dtype, x.device)
@@ -353,18 +378,19 @@ class _LinearReLU(torch.autograd.Function):
         else:
             y = torch.relu(x @ w.t())
         ctx.save_for_backward(x, w, y)
-        ctx.mask_gx, ctx.gy_masked = mask_gx, gy_masked
+        ctx.mask_gx, ctx.gy_masked, ctx.link = mask_gx, gy_masked, link
         return y
 
     @staticmethod
     def backward(ctx, gy):
         x, w, y = ctx.saved_tensors
-        g = gy.contiguous() if ctx.gy_masked else torch.ops.aten.threshold_backward(gy, y, 0).contiguous()
+        masked = ctx.gy_masked or (ctx.link is not None and ctx.link[0])
+        g = gy.contiguous() if masked else torch.ops.aten.threshold_backward(gy, y, 0).contiguous()
         gx = None
         if ctx.needs_input_grad[0]:
-            gx = _dgrad512_masked(g, w, x) if ctx.mask_gx else g @ w
+            gx = _dgrad512_masked(g, w, x) if ctx.mask_gx else _mm_dgrad(g, w)
         gw = _wgrad(g, x) if ctx.needs_input_grad[1] else None
-        return gx, gw, None, None, None, None
+        return gx, gw, None, None, None, None, None
 
 
 class MLP(nn.Module):
@@ -382,9 +408,11 @@ class MLP(nn.Module):
         self.dtype = dtype
         self.n_output_dims = n_out
 
-    def hidden(self, x):
+    def hidden(self, x, link=None):
         """All layers but the last (each followed by ReLU): the features the
-        output layer is applied to."""
+        output layer is applied to.  `link` (a one-element list, False): the
+        last layer's backward skips its ReLU mask once a consumer that
+        applies it sets link[0] (the fused head, renderer.FusedHeadCore)."""
         x = x.to(self.dtype).contiguous()
         hid = list(self.layers[:-1])
         # layer i >= 1 takes layer i-1's ReLU output only: its data gradient
@@ -392,7 +420,7 @@ class MLP(nn.Module):
         fuse = [i > 0 and _dgrad512_ok(x, lin.weight, self.dtype) for i, lin in enumerate(hid)]
         for i, lin in enumerate(hid):
             x = _LinearReLU.apply(x, lin.weight, self.dtype, not torch.is_grad_enabled(), fuse[i],
-                                  i + 1 < len(hid) and fuse[i + 1])
+                                  i + 1 < len(hid) and fuse[i + 1], link if i + 1 == len(hid) else None)
         return x
 
     def hidden_from(self, x, start):
@@ -707,7 +735,10 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
 
     def forward_fused(self, pts, view, tx, tx_view, ray_layout=None):
         attn, base = self._trunk(pts, view, tx, tx_view, ray_layout)
-        h = self._model_signal.hidden(base)
+        link = [False]  # the fused head may take over h's ReLU backward (MLP.hidden)
+        h = self._model_signal.hidden(base, link)
+        if torch.is_grad_enabled() and len(self._model_signal.layers) > 1:
+            self._relu_link = link
         return (attn, h.view(pts.size(0), pts.size(1), -1), self._model_signal.layers[-1].weight,
                 self._model_signal.dtype)
 

@@ -332,6 +332,12 @@ def _packed_exact_weight(w_master, W, cache, pref, shape_key, nbytes, st):
     return cache_store(w_master, "_avr_exactpack", key, Wf) if cache else Wf
 
 
+# The fused head's backward applies the last hidden layer's ReLU mask when
+# that layer hands it over (AVR_HEAD_RELU=0: the layer keeps its own
+# threshold_backward; bitwise the same gradients)
+_HEAD_RELU = os.environ.get("AVR_HEAD_RELU", "1") != "0"
+
+
 class FusedHeadCore(torch.autograd.Function):
     """Render core with the signal network's last linear layer folded in
     (kernels in csrc/head.hip).
@@ -344,7 +350,8 @@ class FusedHeadCore(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, attn, h, w_master, dtype, p, tables, rays_o, position_tx, dirs, cache=False, exact=False):
+    def forward(ctx, attn, h, w_master, dtype, p, tables, rays_o, position_tx, dirs, cache=False, exact=False,
+                relu_h=False):
         dev = h.device
         B, K = h.size(0), h.size(-1)
         S, T = p.n_samples, p.T
@@ -378,7 +385,7 @@ class FusedHeadCore(torch.autograd.Function):
             _lib.call("avr_head_fwd", pref, B, K, _ptr(h), _ptr(Wp), code, _ptr(perm), _ptr(ws), _ptr(cnt),
                       n_split, _ptr(part), st)
         out = _spectrum(p, tables, part, n_split, B, dev, st)
-        ctx.p, ctx.tables = p, tables
+        ctx.p, ctx.tables, ctx.relu_h = p, tables, relu_h
         ctx.save_for_backward(attn, h, W, w, delay, perm, ws, cnt)
         return out
 
@@ -399,12 +406,14 @@ class FusedHeadCore(torch.autograd.Function):
         grad_h = torch.empty_like(h)
         grad_w = torch.empty(B, R, S, dtype=torch.float32, device=dev)
         grad_W = torch.empty(T, K, dtype=torch.float32, device=dev)
-        _lib.call("avr_head_bwd", pref, B, K, _ptr(h), _ptr(W), code, _ptr(w), _ptr(delay), _ptr(perm),
-                  _ptr(ws), _ptr(cnt), _ptr(gz), _ptr(grad_h), _ptr(grad_w), _ptr(grad_W),
+        # relu_h: grad_h leaves with h's ReLU backward applied (the layer
+        # that produced h was told so through its link and skips its own)
+        _lib.call("avr_head_bwd2", pref, B, K, _ptr(h), _ptr(W), code, _ptr(w), _ptr(delay), _ptr(perm),
+                  _ptr(ws), _ptr(cnt), _ptr(gz), int(ctx.relu_h), _ptr(grad_h), _ptr(grad_w), _ptr(grad_W),
                   _ptr(work), nbytes.value, st)
         grad_attn = _grad_attn(p, tables, attn, grad_w, st) if ctx.needs_input_grad[0] else None
         return (grad_attn, grad_h if ctx.needs_input_grad[1] else None,
-                grad_W if ctx.needs_input_grad[2] else None, None, None, None, None, None, None, None, None)
+                grad_W if ctx.needs_input_grad[2] else None, None, None, None, None, None, None, None, None, None)
 
 
 def _poison_nonfinite(out, tensors, ir_out=None):
@@ -681,10 +690,13 @@ class AVRRender(nn.Module):
         """The output-rounding-exact head runs for 16-bit networks (csrc/head_exact.hip)."""
         return self.exact_head and dtype in (torch.float16, torch.bfloat16) and K % 16 == 0 and K <= 512
 
-    def render_from_hidden(self, attn, h, weight, dtype, geom):
+    def render_from_hidden(self, attn, h, weight, dtype, geom, relu_link=None):
         """Render core with the signal head fused (FusedHeadCore): `h` is the
         signal network's last hidden activation [B, R*S, K], `weight` its
-        last layer's weight [T, K] (signal = h @ weight^T)."""
+        last layer's weight [T, K] (signal = h @ weight^T).  `relu_link`
+        (the network's, see model.MLP.hidden): h is a ReLU output the head
+        alone consumes; the head's backward then applies that ReLU's mask
+        and the link tells the layer to skip its own."""
         dev, B = geom["device"], geom["B"]
         S = int(self.n_samples)
         attn = attn.to(dev).reshape(B, -1)
@@ -701,8 +713,12 @@ class AVRRender(nn.Module):
             tables = get_tables(p, dev)
             check_config(p, tables)
             exact = self._exact_for(dtype, K)
+            relu_h = relu_link is not None and torch.is_grad_enabled()
             out = FusedHeadCore.apply(attn, h, weight, dtype, p, tables, geom["rays_o"],
-                                      geom["position_tx"], geom["dirs"], not torch.is_grad_enabled(), exact)
+                                      geom["position_tx"], geom["dirs"], not torch.is_grad_enabled(), exact,
+                                      relu_h)
+            if relu_h:
+                relu_link[0] = True
             if self.propagate_nonfinite:
                 # the head kernels skip rays with an empty window, so a
                 # non-finite h / attn of a masked ray never reaches `out`
@@ -740,7 +756,10 @@ class AVRRender(nn.Module):
         if self.fused_head and getattr(self.network_fn, "supports_fused_head", False):
             attn, h, weight, dtype = self.network_fn.forward_fused(*net_in, **kw)
             if self._head_supported(geom, h, weight, dtype):
-                return self.render_from_hidden(attn, h, weight, dtype, geom)
+                # our own networks leave the link of h's ReLU (model.MLP.hidden)
+                link = getattr(self.network_fn, "_relu_link", None) if _HEAD_RELU else None
+                self.network_fn.__dict__.pop("_relu_link", None)
+                return self.render_from_hidden(attn, h, weight, dtype, geom, link)
             signal = self.network_fn.finish_signal(h)
             return self.render_from_network_output(attn, signal, geom)
         if dtx is not None:

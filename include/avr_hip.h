@@ -483,6 +483,15 @@ int avr_head_bwd(const avr_render_params* p, int32_t B, int32_t K, const void* h
                  const float* ws, const int32_t* cnt, const float* gz, void* grad_h,
                  float* grad_w, float* grad_W, float* workspace, int64_t workspace_bytes,
                  void* stream);
+/* avr_head_bwd with relu_mask = 1: h is the last hidden layer's ReLU output
+ * and the head its only consumer (model.py:176-180, tcnn's MLP backward);
+ * grad_h leaves with that ReLU's backward applied (0 where h <= 0, NaN
+ * keeps: threshold_backward's selection), so the layer skips its own.
+ * relu_mask = 0 is avr_head_bwd. */
+int avr_head_bwd2(const avr_render_params* p, int32_t B, int32_t K, const void* h, const void* W,
+                  int32_t dtype, const float* w, const int32_t* delay, const int32_t* perm,
+                  const float* ws, const int32_t* cnt, const float* gz, int32_t relu_mask, void* grad_h,
+                  float* grad_w, float* grad_W, float* workspace, int64_t workspace_bytes, void* stream);
 
 /* ---- §8f rank 2: training criterion (utils/criterion.py:69-98) ---------
  * pred, ori: spectra [B][F][2] fp32 (the renderer's output and the measured

@@ -192,3 +192,51 @@ def test_unit_map_is_bit_identical():
     x = torch.rand(1 << 20, 3, device=DEV, generator=g) * 2 - 1
     x[:4, 0] = torch.tensor([-1.0, 1.0, 0.0, -1 + 2 ** -24], device=DEV)
     assert torch.equal(_unit(x), (x + 1) / 2)
+
+
+def test_head_takes_over_last_relu_backward(monkeypatch):
+    """Training with the fused head: the head's backward applies the last
+    hidden layer's ReLU mask (avr_head_bwd2 relu_mask) and the layer skips
+    its threshold_backward.  The same selection on the same rounded values:
+    every parameter gradient bitwise equal to the unlinked path
+    (AVR_HEAD_RELU=0), and the link was taken."""
+    from avr_amd import model as M
+    from avr_amd import renderer
+
+    w = WORKLOADS["c1_meshrir_plumbing"].replace(name="raf_small", **{k: v for k, v in WORKLOADS[
+        "c3_raf_furnished_b4"].render.items() if k not in ("n_azi", "n_ele", "n_samples")})
+    w = w.replace(T=RAF_MODEL["signal_output_dim"], batch=2)
+    torch.manual_seed(0)
+    net = AVRModel_complex(RAF_MODEL, mlp_dtype=torch.bfloat16).to(DEV)
+    r = AVRRender(net, **w.render).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    ro = torch.rand(w.batch, 3, device=DEV, generator=g) * 2 - 1
+    tx = torch.rand(w.batch, 3, device=DEV, generator=g) * 2 - 1
+    dtx = torch.nn.functional.normalize(torch.randn(w.batch, 3, device=DEV, generator=g), dim=-1)
+    links = []
+    orig = M.MLP.hidden
+    monkeypatch.setattr(M.MLP, "hidden", lambda self, x, link=None: (links.append(link), orig(self, x, link))[1])
+    grads = []
+    for on in (True, False):
+        monkeypatch.setattr(renderer, "_HEAD_RELU", on)
+        r.zero_grad(set_to_none=True)
+        torch.manual_seed(5)
+        out = r(ro, tx, dtx)
+        (out * torch.linspace(-1, 1, out.numel(), device=DEV).view_as(out)).sum().backward()
+        grads.append({n: p.grad.clone() for n, p in r.named_parameters() if p.grad is not None})
+    torch.cuda.synchronize()
+    signal_links = [l for l in links if l is not None]
+    assert [l[0] for l in signal_links] == [True, False]
+    assert grads[0].keys() == grads[1].keys() and len(grads[0]) > 0
+    bad = []
+    for n in grads[0]:
+        a, b = grads[0][n], grads[1][n]
+        if "encoding" in n:
+            # hash-grid tables: the small grids' backward adds with atomics
+            # (fp32 order varies run to run), so equal up to that order
+            rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
+            if rel > 1e-5:
+                bad.append((n, rel))
+        elif not torch.equal(a, b):
+            bad.append((n, float((a - b).abs().max())))
+    assert not bad, bad

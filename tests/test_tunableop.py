@@ -18,27 +18,39 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_results_file_format():
     """Validators pin the libraries and gfx950; one entry per MLP dtype for
     the config-2 and config-5 inference shapes (M = 262,144 and 2,097,152
-    rows, 512 -> 512)."""
+    rows, 512 -> 512), and the bf16 MLP GEMMs of the config-3 / -4 training
+    steps (83,200 and 147,712 rows): forward (TN, with the ReLU epilogue) and
+    data gradient (NN).  No "Default" rows (nothing to switch on for them)."""
     rows = list(csv.reader(open(model._TUNED_FILE)))
     val = {r[1]: r[2] for r in rows if r[0] == "Validator"}
     assert val["GCN_ARCH_NAME"].startswith("gfx950")
     for k in ("PT_VERSION", "HIP_VERSION", "HIPBLASLT_VERSION", "ROCBLAS_VERSION"):
         assert k in val
     ops = {(r[0], r[1]): r[2:] for r in rows if r[0] != "Validator"}
-    assert len(ops) == 4
+    assert len(ops) == len([r for r in rows if r[0] != "Validator"])  # no duplicates
     for dt in ("Half", "BFloat16"):
         for m in (262144, 2097152):
             sol, ms = ops[(f"GemmAndBiasTunableOp_{dt}_TN", f"tn_512_{m}_512_ld_512_512_512")]
             assert sol.startswith("Gemm_") and float(ms) > 0
+    for (op, sig), (sol, ms) in ops.items():
+        assert sol.startswith("Gemm_") and float(ms) > 0, (op, sig)
+        if op.startswith("GemmTunableOp_"):
+            assert op == "GemmTunableOp_BFloat16_NN" and int(sig.split("_")[2]) in (83200, 147712)
+    assert ("GemmTunableOp_BFloat16_NN", "nn_80_83200_128_ld_80_128_80") in ops
 
 
 def test_tuned_shapes_parsed():
     """Only the file's own shapes take the TunableOp window."""
-    assert model._TUNED_SHAPES == {(dt, m, 512, 512) for dt in (torch.float16, torch.bfloat16)
-                                   for m in (262144, 2097152)}  # configs 2 and 5
+    S = model._TUNED_SHAPES
+    assert {("relu", dt, m, 512, 512) for dt in (torch.float16, torch.bfloat16)
+            for m in (262144, 2097152)} <= S  # configs 2 and 5
+    assert ("dgrad", torch.bfloat16, 83200, 128, 80) in S  # g [83200, 128] @ W [128, 80]
+    assert ("relu", torch.bfloat16, 83200, 512, 416) in S
+    assert all(k[0] in ("relu", "dgrad") for k in S)
     x = torch.empty(1000, 512, dtype=torch.float16)
     w = torch.empty(512, 512, dtype=torch.float16)
     assert not model._tuned_gemm(x, w)  # shape not in the file: no device call at all
+    assert not model._tuned_dgrad(x, w)
 
 
 def test_loader_respects_opt_out(monkeypatch):
@@ -76,6 +88,7 @@ def test_tuned_layer_bit_identical(dtype, rows):
     assert model._enable_tuned_gemms(dev), "shipped TunableOp results rejected (validators?)"
     name = "Half" if dtype == torch.float16 else "BFloat16"
     res = {(r[0], r[1]): r[2] for r in torch.cuda.tunable.get_results()}
+    assert len(res) >= 25
     assert res.get((f"GemmAndBiasTunableOp_{name}_TN", f"tn_512_{rows}_512_ld_512_512_512"), "").startswith(
         "Gemm_Hipblaslt_")
     assert model._tuned_gemm(x, w.to(dtype))
@@ -83,6 +96,26 @@ def test_tuned_layer_bit_identical(dtype, rows):
         y = model._LinearReLU.apply(x, w, dtype)
     assert _state() == before
     assert torch.equal(y, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,out,inp", [(83200, 128, 80), (83200, 512, 416), (147712, 256, 128)])
+def test_tuned_dgrad_bit_identical(rows, out, inp):
+    """The data gradient g @ W through `_mm_dgrad` with the shipped solution
+    equals the default solution's output bit for bit, and TunableOp is left
+    as it was (config-3 / -4 training shapes)."""
+    if os.environ.get("AVR_TUNABLEOP", "1") == "0":
+        pytest.skip("AVR_TUNABLEOP=0: the shipped solution is switched off")
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator(device=dev).manual_seed(rows + out)
+    g = torch.randn(rows, out, device=dev, generator=gen).to(torch.bfloat16)
+    w = (torch.randn(out, inp, device=dev, generator=gen) / out ** 0.5).to(torch.bfloat16)
+    before = _state()
+    ref = g @ w
+    assert model._tuned_dgrad(g, w)
+    gx = model._mm_dgrad(g, w)
+    assert _state() == before
+    assert torch.equal(gx, ref)
 
 
 @pytest.mark.gpu

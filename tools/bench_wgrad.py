@@ -42,6 +42,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c3_raf_furnished_b4")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--tuned", default=None, help="TunableOp results file: time the data gradients' "
+                    "GEMMs with it (tuning off)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     w = WORKLOADS[args.workload]
@@ -80,6 +82,15 @@ def main():
         gm = torch.ops.aten.threshold_backward(gy, y, 0)
         t_mask = time_us(lambda: torch.ops.aten.threshold_backward(gy, y, 0), args.iters)
         t_dgrad = time_us(lambda: gm @ wt, args.iters)
+        t_dgrad_tuned = None
+        if args.tuned:
+            import torch.cuda.tunable as tun
+            tun.tuning_enable(False)
+            tun.record_untuned_enable(False)
+            tun.enable(True)
+            tun.read_file(args.tuned)
+            t_dgrad_tuned = time_us(lambda: gm @ wt, args.iters)
+            tun.enable(False)
         t_wgrad = time_us(lambda: M._wgrad(gm, x), args.iters)
         t_fused = None
         if Mo == 512 and K == 512:  # (g W) masked by the input activation in one launch
@@ -90,7 +101,7 @@ def main():
                         dgrad_us=t_dgrad, dgrad_GBps=(N * Mo + N * K) * 2 / t_dgrad / 1e3,
                         wgrad_us=t_wgrad, wgrad_GBps=(N * Mo + N * K) * 2 / t_wgrad / 1e3,
                         wgrad_TFs=2 * N * Mo * K / t_wgrad / 1e6,
-                        fused_dgrad_mask_us=t_fused))
+                        fused_dgrad_mask_us=t_fused, dgrad_tuned_us=t_dgrad_tuned))
         print(json.dumps(out[-1]), flush=True)
     tot = {k: sum(o[k] * o["calls"] for o in out) for k in ("mask_us", "dgrad_us", "wgrad_us")}
     print(json.dumps(dict(workload=w.name, per_step_us=tot)))
