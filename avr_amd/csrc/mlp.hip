@@ -217,6 +217,85 @@ __global__ __launch_bounds__(256) void wgrad_finalize_kernel(int64_t MK, int spl
     }
 }
 
+// ------------------------------------------- a layer with ONE output (a6)
+// The sigma decoder's last layer (model.py:117-121, 259-262: tcnn network
+// to 1 output), y[n] = sum_k x[n][k] w[k], x [N][K] 16-bit, K % 8 == 0,
+// K <= 512.  As a GEMM it is an N x 1 output tile stream at a fraction of
+// HBM speed (22-27 us for 21 MB at config 3); here a row is K/8 lanes of 16
+// bytes, summed in fp32 per lane and then over the row's lanes by a fixed
+// butterfly, rounded once to the 16-bit type.
+template <typename E>
+__global__ __launch_bounds__(256) void linear_out1_fwd_kernel(int64_t N, int K, const E* __restrict__ x,
+                                                               const E* __restrict__ w, E* __restrict__ y) {
+    const int L = K / 8;  // lanes per row (a power of two: 1 .. 64)
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = i / L;
+    const int c = (int)(i % L);
+    float acc = 0.0f;
+    if (n < N) {
+        const u32x4 xv = *reinterpret_cast<const u32x4*>(x + n * K + 8 * c);
+        const u32x4 wv = *reinterpret_cast<const u32x4*>(w + 8 * c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            acc = fmaf(unpack16<E>(xv[e], 0), unpack16<E>(wv[e], 0), acc);
+            acc = fmaf(unpack16<E>(xv[e], 1), unpack16<E>(wv[e], 1), acc);
+        }
+    }
+    for (int m = 1; m < L; m <<= 1) acc += __shfl_xor(acc, m);
+    if (n < N && c == 0) store_f(y, n, acc);
+}
+
+// Backward of the same layer in one pass over x: gx[n][k] = gy[n] w[k]
+// (one product, rounded: the broadcast multiply's arithmetic) and, per
+// workgroup, the fp32 partial sum_n gy[n] x[n][k] over its rows; the
+// partials are summed in workgroup order by wgrad_finalize_kernel.
+template <typename E>
+__global__ __launch_bounds__(256) void linear_out1_bwd_kernel(int64_t N, int K, int64_t rows_per_block,
+                                                               const E* __restrict__ x, const E* __restrict__ w,
+                                                               const E* __restrict__ gy, E* __restrict__ gx,
+                                                               float* __restrict__ partial) {
+    __shared__ f32x4 red[2][256];
+    const int L = K / 8, rpi = 256 / L;  // lanes per row, rows per pass
+    const int c = threadIdx.x % L, r0 = threadIdx.x / L;
+    const int64_t nb = (int64_t)blockIdx.x * rows_per_block, ne = min(N, nb + rows_per_block);
+    const u32x4 wv = *reinterpret_cast<const u32x4*>(w + 8 * c);
+    float wf[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        wf[2 * e] = unpack16<E>(wv[e], 0);
+        wf[2 * e + 1] = unpack16<E>(wv[e], 1);
+    }
+    float acc[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    for (int64_t n = nb + r0; n < ne; n += rpi) {
+        const float g = load_f(gy, n);
+        const u32x4 xv = *reinterpret_cast<const u32x4*>(x + n * K + 8 * c);
+        u32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            acc[2 * e] = fmaf(g, unpack16<E>(xv[e], 0), acc[2 * e]);
+            acc[2 * e + 1] = fmaf(g, unpack16<E>(xv[e], 1), acc[2 * e + 1]);
+            o[e] = pack16<E>(g * wf[2 * e], g * wf[2 * e + 1]);
+        }
+        *reinterpret_cast<u32x4*>(gx + n * K + 8 * c) = o;
+    }
+    // the rpi row groups' sums of each lane column, added in group order
+    red[0][threadIdx.x] = f32x4{acc[0], acc[1], acc[2], acc[3]};
+    red[1][threadIdx.x] = f32x4{acc[4], acc[5], acc[6], acc[7]};
+    __syncthreads();
+    if (threadIdx.x < L) {
+        f32x4 a = red[0][threadIdx.x], b = red[1][threadIdx.x];
+        for (int q = 1; q < rpi; ++q) {
+            a += red[0][q * L + threadIdx.x];
+            b += red[1][q * L + threadIdx.x];
+        }
+        float* out = partial + (int64_t)blockIdx.x * K + 8 * threadIdx.x;
+        *reinterpret_cast<f32x4*>(out) = a;
+        *reinterpret_cast<f32x4*>(out + 4) = b;
+    }
+}
+
+constexpr int kOut1Blocks = 512;  // backward workgroups (partials of K floats each)
+
 int wgrad_splits(int64_t N, int M, int K) {
     const int tiles = ((M + kTile - 1) / kTile) * ((K + kTile - 1) / kTile);
     const int target = 512;  // ~2 workgroups per CU
@@ -259,4 +338,63 @@ extern "C" int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* gra
     hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)((MK / 4 + quads_per_block - 1) / quads_per_block)),
                        dim3(256), 0, st, MK, used, G, workspace, grad_w);
     return check_launch("avr_linear_wgrad_finalize");
+}
+
+namespace {
+int out1_check(int64_t N, int32_t K, int32_t dtype, const char* who) {
+    if (!(N >= 1 && K >= 8 && K <= 512 && (K & (K - 1)) == 0))
+        return fail(AVR_E_ARG, std::string(who) + ": N >= 1 and K a power of two in [8, 512]");
+    if (!(dtype == AVR_DTYPE_F16 || dtype == AVR_DTYPE_BF16))
+        return fail(AVR_E_ARG, std::string(who) + ": fp16 or bf16 operands");
+    return 0;
+}
+}  // namespace
+
+extern "C" int avr_linear_out1_fwd(int64_t N, int32_t K, const void* x, const void* w, int32_t dtype, void* y,
+                                   void* stream) {
+    if (int e = out1_check(N, K, dtype, "avr_linear_out1_fwd")) return e;
+    AVR_REQUIRE(x && w && y && reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(w) % 16 == 0,
+                "avr_linear_out1_fwd: x and w must be non-null and 16-byte aligned");
+    const int64_t threads = N * (K / 8);
+    const dim3 grid((unsigned)((threads + 255) / 256));
+    hipStream_t st = as_stream(stream);
+    if (dtype == AVR_DTYPE_F16)
+        hipLaunchKernelGGL(linear_out1_fwd_kernel<__half>, grid, dim3(256), 0, st, N, (int)K, (const __half*)x,
+                           (const __half*)w, (__half*)y);
+    else
+        hipLaunchKernelGGL(linear_out1_fwd_kernel<__hip_bfloat16>, grid, dim3(256), 0, st, N, (int)K,
+                           (const __hip_bfloat16*)x, (const __hip_bfloat16*)w, (__hip_bfloat16*)y);
+    return check_launch("avr_linear_out1_fwd");
+}
+
+extern "C" int avr_linear_out1_workspace(int32_t K, int64_t* floats) {
+    AVR_REQUIRE(floats && K >= 8, "avr_linear_out1_workspace: bad args");
+    *floats = (int64_t)kOut1Blocks * K;
+    return 0;
+}
+
+extern "C" int avr_linear_out1_bwd(int64_t N, int32_t K, const void* x, const void* w, const void* grad_y,
+                                   int32_t dtype, void* grad_x, float* workspace, float* grad_w, void* stream) {
+    if (int e = out1_check(N, K, dtype, "avr_linear_out1_bwd")) return e;
+    AVR_REQUIRE(x && w && grad_y && grad_x && workspace && grad_w && reinterpret_cast<uintptr_t>(x) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(w) % 16 == 0 && reinterpret_cast<uintptr_t>(grad_x) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(workspace) % 16 == 0 && reinterpret_cast<uintptr_t>(grad_w) % 16 == 0,
+                "avr_linear_out1_bwd: operands must be non-null and 16-byte aligned");
+    const int64_t rows = (N + kOut1Blocks - 1) / kOut1Blocks;
+    const int used = (int)((N + rows - 1) / rows);
+    hipStream_t st = as_stream(stream);
+    if (dtype == AVR_DTYPE_F16)
+        hipLaunchKernelGGL(linear_out1_bwd_kernel<__half>, dim3(used), dim3(256), 0, st, N, (int)K, rows,
+                           (const __half*)x, (const __half*)w, (const __half*)grad_y, (__half*)grad_x, workspace);
+    else
+        hipLaunchKernelGGL(linear_out1_bwd_kernel<__hip_bfloat16>, dim3(used), dim3(256), 0, st, N, (int)K, rows,
+                           (const __hip_bfloat16*)x, (const __hip_bfloat16*)w, (const __hip_bfloat16*)grad_y,
+                           (__hip_bfloat16*)grad_x, workspace);
+    if (int e = check_launch("avr_linear_out1_bwd")) return e;
+    int G = 1;
+    while (G < 64 && 2 * G <= used && (K / 4) * G < 131072) G *= 2;
+    const int64_t quads_per_block = 256 / G;
+    hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)((K / 4 + quads_per_block - 1) / quads_per_block)),
+                       dim3(256), 0, st, (int64_t)K, used, G, workspace, grad_w);
+    return check_launch("avr_linear_out1_finalize");
 }

@@ -112,6 +112,60 @@ class _Linear(torch.autograd.Function):
         return gx, gw, None, None
 
 
+class _LinearOut1(torch.autograd.Function):
+    """A layer with one output, y = x w^T for w [1, K] (the sigma decoder's
+    last), on csrc/mlp.hip's `avr_linear_out1_*`: one pass over x forward,
+    one pass over x backward for both gradients (the N x 1 GEMM, the
+    broadcast-multiply data gradient and the weight-gradient GEMM took
+    ~75 us at config 3's 83,200 rows for 21 MB of x)."""
+
+    @staticmethod
+    def forward(ctx, x, w_master, dtype, cache=False):
+        import ctypes
+
+        from . import _lib
+
+        w = cast_weight(w_master, dtype, cache).contiguous()
+        x = x.contiguous()
+        N, K = x.shape
+        y = torch.empty(N, 1, dtype=dtype, device=x.device)
+        code = _lib.DTYPE_F16 if dtype == torch.float16 else _lib.DTYPE_BF16
+        _lib.call("avr_linear_out1_fwd", N, K, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(w.data_ptr()), code,
+                  ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        import ctypes
+
+        from . import _lib
+
+        x, w = ctx.saved_tensors
+        N, K = x.shape
+        gy = gy.to(x.dtype).contiguous()
+        gx = torch.empty_like(x)
+        nf = ctypes.c_int64(0)
+        _lib.call("avr_linear_out1_workspace", K, ctypes.byref(nf))
+        ws = torch.empty(nf.value, dtype=torch.float32, device=x.device)
+        gw = torch.empty(1, K, dtype=torch.float32, device=x.device)
+        code = _lib.DTYPE_F16 if x.dtype == torch.float16 else _lib.DTYPE_BF16
+        _lib.call("avr_linear_out1_bwd", N, K, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(w.data_ptr()),
+                  ctypes.c_void_p(gy.data_ptr()), code, ctypes.c_void_p(gx.data_ptr()),
+                  ctypes.c_void_p(ws.data_ptr()), ctypes.c_void_p(gw.data_ptr()),
+                  ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+        return (gx if ctx.needs_input_grad[0] else None), (gw if ctx.needs_input_grad[1] else None), None, None
+
+
+_OUT1 = os.environ.get("AVR_OUT1", "1") != "0"
+
+
+def _out1_ok(h, w_master, dtype):
+    K = h.size(-1)
+    return (_OUT1 and h.is_cuda and torch.is_grad_enabled() and dtype in (torch.float16, torch.bfloat16)
+            and w_master.size(0) == 1 and h.dim() == 2 and 8 <= K <= 512 and K & (K - 1) == 0)
+
+
 _ZERO_BIAS: dict = {}
 
 
@@ -443,8 +497,12 @@ class MLP(nn.Module):
         return x
 
     def last(self, h):
-        """The bias-free output layer (output_activation None)."""
-        return _Linear.apply(h.contiguous(), self.layers[-1].weight, self.dtype, not torch.is_grad_enabled())
+        """The bias-free output layer (output_activation None); a one-output
+        layer in training on `_LinearOut1`."""
+        w = self.layers[-1].weight
+        if _out1_ok(h, w, self.dtype):
+            return _LinearOut1.apply(h.to(self.dtype), w, self.dtype, False)
+        return _Linear.apply(h.contiguous(), w, self.dtype, not torch.is_grad_enabled())
 
     def forward(self, x, out_relu=False):
         """The network; `out_relu=True` returns relu(output) with the ReLU in

@@ -313,6 +313,19 @@ int avr_hashgrid_bwd_partitioned_set(int64_t N, int32_t n_levels, const float* x
  * avr_runner.py:190).  Split-K over n: `workspace` holds splits*M*K fp32
  * partials (splits from avr_linear_wgrad_splits), summed deterministically. */
 int avr_linear_wgrad_splits(int64_t N, int32_t M, int32_t K, int32_t* splits);
+/* A bias-free layer with ONE output (the sigma decoder's last, model.py:
+ * 117-121, 259-262), 16-bit x [N][K] and w [K] (fp16 / bf16), K a power of
+ * two in [8, 512], fp32 sums:
+ *   fwd: y[n] = round16(sum_k x[n][k] w[k])                 (y [N])
+ *   bwd: grad_x[n][k] = round16(grad_y[n] w[k]), grad_w[k] = sum_n grad_y[n]
+ *        x[n][k] (fp32, deterministic; `workspace` holds
+ *        avr_linear_out1_workspace() floats).
+ * Replaces the N x 1 GEMM, its broadcast-multiply data gradient and its
+ * weight-gradient GEMM (x @ w^T, gy * w, gy^T @ x). */
+int avr_linear_out1_fwd(int64_t N, int32_t K, const void* x, const void* w, int32_t dtype, void* y, void* stream);
+int avr_linear_out1_workspace(int32_t K, int64_t* floats);
+int avr_linear_out1_bwd(int64_t N, int32_t K, const void* x, const void* w, const void* grad_y, int32_t dtype,
+                        void* grad_x, float* workspace, float* grad_w, void* stream);
 /* One width-512 hidden layer at inference, y = relu(x W^T): x, y [M][512],
  * W [512][512] (out x in), 16-bit (AVR_DTYPE_F16 / AVR_DTYPE_BF16), fp32
  * accumulation, one rounding of the output (model.py:176-180, tcnn

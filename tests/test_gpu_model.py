@@ -240,3 +240,39 @@ def test_head_takes_over_last_relu_backward(monkeypatch):
         elif not torch.equal(a, b):
             bad.append((n, float((a - b).abs().max())))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
+@pytest.mark.parametrize("N,K", [(83200, 128), (1, 8), (1000, 512), (777, 64)])
+def test_linear_out1_matches_torch(dtype, N, K, monkeypatch):
+    """The one-output layer (avr_linear_out1_*) against the torch ops it
+    replaces: forward within one 16-bit rounding of the fp64 sum (small
+    integers: exact), data gradient bitwise equal to gy * w, weight gradient
+    against fp64 (small integers: exact), deterministic."""
+    from avr_amd import model as M
+
+    gen = torch.Generator(device=DEV).manual_seed(N + K)
+    x = torch.randint(-3, 4, (N, K), device=DEV, generator=gen).to(dtype).requires_grad_(True)
+    wm = torch.randint(-2, 3, (1, K), device=DEV, generator=gen).float().requires_grad_(True)
+    gy = torch.randint(-2, 3, (N, 1), device=DEV, generator=gen).to(dtype)
+    assert M._out1_ok(x, wm, dtype)
+    y = M._LinearOut1.apply(x, wm, dtype, False)
+    y.backward(gy)
+    ref_y = (x.detach().double() @ wm.detach().double().t()).to(dtype)
+    assert torch.equal(y, ref_y)
+    assert torch.equal(x.grad, gy * wm.detach().to(dtype))
+    ref_gw = (gy.double().t() @ x.detach().double()).float()
+    assert torch.equal(wm.grad, ref_gw)
+    # random operands: bitwise repeatable; within rounding of fp64
+    xr = torch.randn(N, K, device=DEV, generator=gen).to(dtype).requires_grad_(True)
+    gr = torch.randn(N, 1, device=DEV, generator=gen).to(dtype)
+    outs = []
+    for _ in range(2):
+        xr.grad = None
+        wm.grad = None
+        yr = M._LinearOut1.apply(xr, wm, dtype, False)
+        yr.backward(gr)
+        outs.append((yr.clone(), xr.grad.clone(), wm.grad.clone()))
+    assert all(torch.equal(a, b) for a, b in zip(*outs))
+    gw64 = gr.double().t() @ xr.detach().double()
+    assert float((outs[0][2].double() - gw64).norm() / gw64.norm()) < 1e-5
