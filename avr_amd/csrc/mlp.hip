@@ -60,18 +60,31 @@ __device__ __forceinline__ void wg_dma16(const void* g, uint32_t lds) {
                  : "memory", "m0");
 }
 
-// s_waitcnt vmcnt(n), n in {0, 4, 8} (expcnt / lgkmcnt not waited on)
+// s_waitcnt vmcnt(4 ahead): this wave's DMAs of all but the `ahead` youngest
+// slabs landed (4 per slab; expcnt / lgkmcnt not waited on)
 #define AVR_WG_VMCNT(N) __builtin_amdgcn_s_waitcnt(((N) & 0xF) | (0x7 << 4) | (0xF << 8) | (((N) >> 4) << 14))
 __device__ __forceinline__ void wg_wait_slabs(int ahead) {
-    if (ahead >= 2)
-        AVR_WG_VMCNT(8);
-    else if (ahead == 1)
-        AVR_WG_VMCNT(4);
-    else
-        AVR_WG_VMCNT(0);
+    switch (ahead) {
+        case 0: AVR_WG_VMCNT(0); break;
+        case 1: AVR_WG_VMCNT(4); break;
+        case 2: AVR_WG_VMCNT(8); break;
+        case 3: AVR_WG_VMCNT(12); break;
+        case 4: AVR_WG_VMCNT(16); break;
+        case 5: AVR_WG_VMCNT(20); break;
+        default: AVR_WG_VMCNT(24); break;
+    }
 }
 
-constexpr int kWgSlots = 4;  // ring slots of one slab (A and B images, 16 KiB)
+// AVR_WG_SLOTS: ring slots of one slab (A and B images, 16 KiB each);
+// AVR_WG_DBG (timing probes, results wrong): bit 0 no DMA, bit 1 no MFMAs,
+// bit 2 no barrier
+#ifndef AVR_WG_SLOTS
+#define AVR_WG_SLOTS 4
+#endif
+#ifndef AVR_WG_DBG
+#define AVR_WG_DBG 0
+#endif
+constexpr int kWgSlots = AVR_WG_SLOTS;
 
 __global__ __launch_bounds__(256) void linear_wgrad_dma_kernel(int64_t N, int M, int K, int64_t rows_per_split,
                                                                 int used, const __hip_bfloat16* __restrict__ gy,
@@ -110,6 +123,7 @@ __global__ __launch_bounds__(256) void linear_wgrad_dma_kernel(int64_t N, int M,
         const int64_t n0 = n_begin + (int64_t)s * kSlab;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
+            if (AVR_WG_DBG & 1) break;
             const int64_t n = n0 + drow[u];
             const bool ok = n < n_end;
             const void* ga = ok ? (const void*)(gy + n * M + acol[u]) : (const void*)g_wgrad_zero_row;
@@ -151,7 +165,7 @@ __global__ __launch_bounds__(256) void linear_wgrad_dma_kernel(int64_t N, int M,
         // this wave's DMA of slab s landed (slabs s+1, s+2 may still fly);
         // the barrier makes every wave's landed and frees slot (s-1) % 4
         wg_wait_slabs(min(kWgSlots - 2, nslab - 1 - s));
-        __syncthreads();
+        if (!(AVR_WG_DBG & 4)) __syncthreads();
         __builtin_amdgcn_sched_barrier(0);
         if (s + kWgSlots - 1 < nslab) issue(s + kWgSlots - 1);
         const char* img = lds + (s % kWgSlots) * 2 * kImg;
@@ -170,8 +184,13 @@ __global__ __launch_bounds__(256) void linear_wgrad_dma_kernel(int64_t N, int M,
 #pragma unroll
             for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
+                for (int j = 0; j < 2; ++j) {
+                    if (AVR_WG_DBG & 2) {  // keep the reads: fold them into one register
+                        acc[i][j][0] += (float)av[i][0] + (float)bv[j][0];
+                        continue;
+                    }
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);
+                }
         }
         __builtin_amdgcn_sched_barrier(0);
     }
