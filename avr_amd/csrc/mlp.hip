@@ -315,12 +315,29 @@ __global__ __launch_bounds__(256) void linear_out1_bwd_kernel(int64_t N, int K, 
 
 constexpr int kOut1Blocks = 512;  // backward workgroups (partials of K floats each)
 
+// Workgroups aimed for: two per CU for the width-512 layers (16 tiles and
+// more), one per CU below, where the fp32 partials (splits x M x K x 4
+// bytes, written and read back) are a large share of the traffic: e.g.
+// 128 x 128 at 83,200 rows 19.7 -> 16.5 us (tools/xbench_wgrad.py).
+// AVR_WG_TARGET overrides both; AVR_WG_PCAP keeps the partials below
+// 1 / AVR_WG_PCAP of the operand bytes (N (M + K) x 2), 0 = no cap.
+#ifndef AVR_WG_TARGET
+#define AVR_WG_TARGET 0
+#endif
+#ifndef AVR_WG_PCAP
+#define AVR_WG_PCAP 0
+#endif
 int wgrad_splits(int64_t N, int M, int K) {
     const int tiles = ((M + kTile - 1) / kTile) * ((K + kTile - 1) / kTile);
-    const int target = 512;  // ~2 workgroups per CU
+    const int target = AVR_WG_TARGET > 0 ? AVR_WG_TARGET : (tiles >= 16 ? 512 : 256);
     int splits = (target + tiles - 1) / tiles;
     const int64_t max_by_rows = N / 256 > 1 ? N / 256 : 1;  // >= 8 slabs per split
-    return (int)(splits < max_by_rows ? splits : max_by_rows);
+    if (splits > max_by_rows) splits = (int)max_by_rows;
+    if (AVR_WG_PCAP > 0) {
+        const int64_t cap = N * (M + K) * 2 / ((int64_t)AVR_WG_PCAP * M * K * 4);
+        if (splits > cap) splits = (int)(cap > 8 ? cap : 8);
+    }
+    return splits;
 }
 
 }  // namespace

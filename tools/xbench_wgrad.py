@@ -31,25 +31,27 @@ def main():
     g = torch.Generator(device=dev).manual_seed(1)
     gy = torch.randn(N, M, device=dev, generator=g).bfloat16()
     x = torch.randn(N, K, device=dev, generator=g).bfloat16()
-    sp = ctypes.c_int32(0)
-    _lib.call("avr_linear_wgrad_splits", N, M, K, ctypes.byref(sp))
-    ws = torch.empty(sp.value * M * K, dtype=torch.float32, device=dev)
     st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     libs = [("product", _lib.load())]
     for item in filter(None, a.libs.split(",")):
         name, path = item.split("=")
         libs.append((name, ctypes.CDLL(os.path.join(ROOT, path))))
     outs, times = {}, {n: [] for n, _ in libs}
+    splits = {}
     for name, lib in libs:
+        sp = ctypes.c_int32(0)  # each library's own split count and workspace
+        assert lib.avr_linear_wgrad_splits(ctypes.c_int64(N), M, K, ctypes.byref(sp)) == 0
+        splits[name] = sp.value
+        ws = torch.empty(sp.value * M * K, dtype=torch.float32, device=dev)
         out = torch.empty(M, K, dtype=torch.float32, device=dev)
         f = lib.avr_linear_wgrad
         f.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32] + [ctypes.c_void_p] * 3 + [ctypes.c_int32] + \
             [ctypes.c_void_p] * 2
-        call = (lambda f=f, out=out: f(N, M, K, gy.data_ptr(), x.data_ptr(), ws.data_ptr(), sp.value,
-                                        out.data_ptr(), st))
-        outs[name] = (call, out)
+        call = (lambda f=f, out=out, ws=ws, n=sp.value: f(N, M, K, gy.data_ptr(), x.data_ptr(), ws.data_ptr(), n,
+                                                          out.data_ptr(), st))
+        outs[name] = (call, out, ws)
     for _ in range(a.rounds):
-        for name, (call, out) in outs.items():
+        for name, (call, out, _) in outs.items():
             call()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -62,9 +64,11 @@ def main():
     ref = outs["product"][1]
     for name in times:
         t = sorted(times[name])
-        print(json.dumps(dict(variant=name, shape=[N, M, K], us_median=t[len(t) // 2], us_all=t,
+        same = torch.equal(outs[name][1], ref)
+        close = float((outs[name][1] - ref).norm() / ref.norm())
+        print(json.dumps(dict(variant=name, shape=[N, M, K], splits=splits[name], us_median=t[len(t) // 2], us_all=t,
                               GBps=(N * M + N * K) * 2 / t[len(t) // 2] / 1e3,
-                              bitwise_equal=bool(torch.equal(outs[name][1], ref)))))
+                              bitwise_equal=bool(same), rel_diff=close)))
 
 
 if __name__ == "__main__":
