@@ -143,6 +143,7 @@ _SIGS = {
     "avr_mlp512x2_fwd": (ctypes.c_int, [_c_i64, _vp, _vp, _c_i32, _vp, _vp]),
     "avr_linear_wgrad": (ctypes.c_int, [_c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i32, _vp, _vp]),
     "avr_linear_out1_fwd": (ctypes.c_int, [_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp]),
+    "avr_narrow_mm": (ctypes.c_int, [_c_i64, _c_i32, _c_i32, _vp, _vp, _c_i32, _c_i32, _vp, _vp, _vp]),
     "avr_linear_out1_workspace": (ctypes.c_int, [_c_i32, _vp]),
     "avr_linear_out1_bwd": (ctypes.c_int, [_c_i64, _c_i32, _vp, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp]),
     "avr_head_splits": (ctypes.c_int, [_vp, _c_i32, _c_i32, _c_i32, _vp]),

@@ -26,6 +26,9 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+#include <type_traits>
+
 using namespace avr;
 
 namespace {
@@ -313,6 +316,135 @@ __global__ __launch_bounds__(256) void linear_out1_bwd_kernel(int64_t N, int K, 
     }
 }
 
+// ------------------------------- narrow layers: Y = act(X Bt^T), C <= 256
+// The sigma networks' layers (model.py:117-121, 259-262: widths 80 .. 256)
+// at the training step's 83,200 .. 147,712 rows.  As hipBLASLt GEMMs they
+// run at 1-3 TB/s (the N x C output is a stream of small tiles), and a ReLU
+// layer's data gradient adds a threshold pass.  Here the whole of Bt
+// [C][R] (<= 256 x 256, 16-bit) sits in LDS (rows padded by 16 B: the
+// fragment reads are conflict-free), each wave takes 32 rows of X and forms
+// Y^T = Bt X^T tile by tile (v_mfma_f32_32x32x16: A = Bt fragment from LDS,
+// B = 16 bytes of an X row straight from memory), so a lane ends with one
+// row's 4-column groups.  ACT: 0 none, 1 ReLU (the forward's epilogue),
+// 2 mask (0 where Mk <= 0, NaN keeps: a data gradient with the input ReLU's
+// backward, threshold_backward's selection).  One rounding of the fp32 sum.
+typedef uint32_t frag4u __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+
+template <typename E>
+__device__ __forceinline__ f32x16 mfma16(frag4u a, frag4u b, f32x16 c) {
+    typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+    if constexpr (std::is_same<E, __half>::value)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c,
+                                                      0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                       c, 0, 0, 0);
+}
+
+template <typename E>
+__device__ __forceinline__ uint32_t narrow_keep(uint32_t v, uint32_t m) {
+    constexpr uint32_t kInf = std::is_same<E, __half>::value ? 0x7c00u : 0x7f80u;
+    const uint32_t lo = m & 0xffffu, hi = m >> 16;
+    const bool zlo = lo == 0u || lo - 0x8000u <= kInf, zhi = hi == 0u || hi - 0x8000u <= kInf;
+    return (zlo ? 0u : (v & 0xffffu)) | (zhi ? 0u : (v & 0xffff0000u));
+}
+
+constexpr int kNarrowRows = 128;  // rows per workgroup tile (4 waves x 32)
+#ifndef AVR_NARROW_STAGE
+#define AVR_NARROW_STAGE 1
+#endif
+
+// STAGE: the tile's X rows land in LDS first (coalesced 16-byte loads, rows
+// padded by 16 B like Bt), and the fragments are read from there; otherwise
+// each lane loads its row's 16-byte pieces straight from memory (32 rows x
+// 32 B per wave instruction).
+template <typename E, int NCT, int NKS, int ACT, bool STAGE>
+__global__ __launch_bounds__(256, 2) void narrow_mm_kernel(int64_t N, int R, int C, const E* __restrict__ X,
+                                                         const E* __restrict__ Bt, const E* __restrict__ Mk,
+                                                         E* __restrict__ Y) {
+    extern __shared__ frag4u bl[];  // [NCT * 32][R / 8 + 1] 16-byte pieces, then (STAGE) X [128][R / 8 + 1]
+    const int pieces = R / 8, stride = pieces + 1;
+    frag4u* xs = bl + NCT * 32 * stride;
+    for (int i = threadIdx.x; i < NCT * 32 * pieces; i += 256) {
+        const int c = i / pieces, p = i % pieces;
+        bl[c * stride + p] = c < C ? *reinterpret_cast<const frag4u*>(Bt + (int64_t)c * R + 8 * p) : frag4u{};
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, h = lane >> 5;
+    const int64_t ntiles = (N + kNarrowRows - 1) / kNarrowRows;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t n = tile * kNarrowRows + 32 * wave + j;
+        const bool ok = n < N;
+        frag4u xf[NKS];
+        if constexpr (STAGE) {
+            constexpr int kP = 2 * NKS;  // pieces per row
+            frag4u v[NKS];               // 128 kP pieces over 256 threads: kP / 2 each
+#pragma unroll
+            for (int i = 0; i < NKS; ++i) {
+                const int idx = threadIdx.x + 256 * i, row = idx / kP, p = idx % kP;
+                const int64_t nn = tile * kNarrowRows + row;
+                v[i] = nn < N ? *reinterpret_cast<const frag4u*>(X + nn * R + 8 * p) : frag4u{};
+            }
+            __syncthreads();  // the previous tile's fragment reads are done
+#pragma unroll
+            for (int i = 0; i < NKS; ++i) {
+                const int idx = threadIdx.x + 256 * i, row = idx / kP, p = idx % kP;
+                xs[row * stride + p] = v[i];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int s = 0; s < NKS; ++s) xf[s] = xs[(32 * wave + j) * stride + 2 * s + h];
+        } else {
+            const E* xr = X + (ok ? n : 0) * R + 8 * h;
+#pragma unroll
+            for (int s = 0; s < NKS; ++s) xf[s] = ok ? *reinterpret_cast<const frag4u*>(xr + 16 * s) : frag4u{};
+        }
+        f32x16 acc[NCT];
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) acc[ct] = f32x16{};
+        // Bt fragments one k-step ahead of the MFMAs that use them (the
+        // fences keep hipcc from hoisting every k-step's reads at once)
+        frag4u af[2][NCT];
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) af[0][ct] = bl[(32 * ct + j) * stride + h];
+#pragma unroll
+        for (int s = 0; s < NKS; ++s) {
+            if (s + 1 < NKS) {
+#pragma unroll
+                for (int ct = 0; ct < NCT; ++ct) af[(s + 1) & 1][ct] = bl[(32 * ct + j) * stride + 2 * (s + 1) + h];
+            }
+#pragma unroll
+            for (int ct = 0; ct < NCT; ++ct) acc[ct] = mfma16<E>(af[s & 1][ct], xf[s], acc[ct]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (!ok) continue;  // (STAGE: no barrier follows in this tile)
+        // lane (j, h) holds Y[n][32 ct + 8 q + 4 h + i] in acc[ct][4 q + i]
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int c0 = 32 * ct + 8 * q + 4 * h;
+                if (c0 >= C) continue;
+                const f32x16& v = acc[ct];
+                float a0 = v[4 * q], a1 = v[4 * q + 1], a2 = v[4 * q + 2], a3 = v[4 * q + 3];
+                if (ACT == 1) {
+                    a0 = __builtin_elementwise_maximum(a0, 0.0f);
+                    a1 = __builtin_elementwise_maximum(a1, 0.0f);
+                    a2 = __builtin_elementwise_maximum(a2, 0.0f);
+                    a3 = __builtin_elementwise_maximum(a3, 0.0f);
+                }
+                u32x2v o = {pack16<E>(a0, a1), pack16<E>(a2, a3)};
+                if (ACT == 2) {
+                    const u32x2v m = *reinterpret_cast<const u32x2v*>(Mk + n * C + c0);
+                    o[0] = narrow_keep<E>(o[0], m[0]);
+                    o[1] = narrow_keep<E>(o[1], m[1]);
+                }
+                *reinterpret_cast<u32x2v*>(Y + n * C + c0) = o;
+            }
+    }
+}
+
 constexpr int kOut1Blocks = 512;  // backward workgroups (partials of K floats each)
 
 // Workgroups aimed for: two per CU for the width-512 layers (16 tiles and
@@ -433,4 +565,58 @@ extern "C" int avr_linear_out1_bwd(int64_t N, int32_t K, const void* x, const vo
     hipLaunchKernelGGL(wgrad_finalize_kernel, dim3((unsigned)((K / 4 + quads_per_block - 1) / quads_per_block)),
                        dim3(256), 0, st, (int64_t)K, used, G, workspace, grad_w);
     return check_launch("avr_linear_out1_finalize");
+}
+
+extern "C" int avr_narrow_mm(int64_t N, int32_t R, int32_t C, const void* X, const void* Bt, int32_t dtype,
+                             int32_t act, const void* mask, void* Y, void* stream) {
+    AVR_REQUIRE(N >= 1 && (R == 80 || R == 128 || R == 256) && C >= 65 && C <= 256 && C % 4 == 0 &&
+                    (R < 256 || C <= 128),
+                "avr_narrow_mm: R in {80, 128, 256}, C a multiple of 4 in [68, 256] (<= 128 for R = 256)");
+    AVR_REQUIRE(dtype == AVR_DTYPE_F16 || dtype == AVR_DTYPE_BF16, "avr_narrow_mm: fp16 or bf16 operands");
+    AVR_REQUIRE(act >= 0 && act <= 2 && (act != 2 || mask), "avr_narrow_mm: act 0 (none), 1 (ReLU), 2 (mask)");
+    AVR_REQUIRE(X && Bt && Y && reinterpret_cast<uintptr_t>(X) % 16 == 0 && reinterpret_cast<uintptr_t>(Bt) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(Y) % 8 == 0 && (!mask || reinterpret_cast<uintptr_t>(mask) % 8 == 0),
+                "avr_narrow_mm: X, Bt 16-byte and Y, mask 8-byte aligned");
+    const int nct = (C + 31) / 32;
+    const int64_t ntiles = (N + kNarrowRows - 1) / kNarrowRows;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t grid = std::min<int64_t>(ntiles, 2 * (int64_t)cus);
+    hipStream_t st = as_stream(stream);
+    // the staged form where Bt and the X tile fit two workgroups per CU
+    const size_t bt_lds = (size_t)(nct == 3 ? 3 : nct == 4 ? 4 : 8) * 32 * (R / 8 + 1) * 16;
+    const size_t x_lds = (size_t)kNarrowRows * (R / 8 + 1) * 16;
+    const bool stage = AVR_NARROW_STAGE && bt_lds + x_lds <= 80 * 1024;
+    auto go = [&](auto e_tag, auto n_tag, auto a_tag) {
+        using E = decltype(e_tag);
+        constexpr int kN = decltype(n_tag)::value, kA = decltype(a_tag)::value;
+        // (R = 256 only with C <= 128: the 8-tile form would not fit 256 registers)
+        constexpr int kN16 = kN == 8 ? 8 : 16;
+        auto pick = [&](auto st_tag) {
+            constexpr bool kS = decltype(st_tag)::value;
+            return R == 80 ? narrow_mm_kernel<E, kN, 5, kA, kS>
+                           : (R == 128 ? narrow_mm_kernel<E, kN, 8, kA, kS> : narrow_mm_kernel<E, kN, kN16, kA, kS>);
+        };
+        auto kern = stage ? pick(std::true_type{}) : pick(std::false_type{});
+        const size_t lds = bt_lds + (stage ? x_lds : 0);
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), lds, st, N, (int)R, (int)C, (const E*)X,
+                           (const E*)Bt, (const E*)mask, (E*)Y);
+    };
+    auto by_act = [&](auto e_tag, auto n_tag) {
+        if (act == 0) go(e_tag, n_tag, std::integral_constant<int, 0>{});
+        else if (act == 1) go(e_tag, n_tag, std::integral_constant<int, 1>{});
+        else go(e_tag, n_tag, std::integral_constant<int, 2>{});
+    };
+    auto by_n = [&](auto e_tag) {
+        if (nct == 3) by_act(e_tag, std::integral_constant<int, 3>{});
+        else if (nct == 4) by_act(e_tag, std::integral_constant<int, 4>{});
+        else by_act(e_tag, std::integral_constant<int, 8>{});
+    };
+    if (dtype == AVR_DTYPE_F16)
+        by_n(__half{});
+    else
+        by_n(__hip_bfloat16{});
+    return check_launch("avr_narrow_mm");
 }

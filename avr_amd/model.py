@@ -404,6 +404,46 @@ def _dgrad512_masked(g, w, x):
     return out
 
 
+# The sigma networks' narrow layers (widths 80 .. 256) in training on
+# csrc/mlp.hip's `avr_narrow_mm` (forward with the ReLU, data gradient with
+# the input ReLU's backward); opt-in, AVR_NARROW=1 (default: hipBLASLt +
+# threshold_backward).
+_NARROW = os.environ.get("AVR_NARROW", "0") == "1"
+
+
+def _narrow_ok(x, R, C, dtype, in_backward=False):
+    """Y[N, C] = act(X[N, R] Bt[C, R]^T) fits avr_narrow_mm (training only:
+    grad mode on, or called from a backward)."""
+    return (_NARROW and x.is_cuda and (in_backward or torch.is_grad_enabled())
+            and dtype in (torch.float16, torch.bfloat16)
+            and R in (80, 128, 256) and 68 <= C <= 256 and C % 4 == 0 and (R < 256 or C <= 128))
+
+
+def _narrow(x, bt, act, mask=None):
+    """act(x bt^T) on avr_narrow_mm: act 0 none, 1 ReLU, 2 zero where mask <= 0."""
+    import ctypes
+
+    from . import _lib
+
+    x = x.contiguous()
+    bt = bt.contiguous()
+    N, R = x.shape
+    C = bt.size(0)
+    y = torch.empty(N, C, dtype=x.dtype, device=x.device)
+    code = _lib.DTYPE_F16 if x.dtype == torch.float16 else _lib.DTYPE_BF16
+    m = ctypes.c_void_p(mask.contiguous().data_ptr()) if mask is not None else None
+    _lib.call("avr_narrow_mm", N, R, C, ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(bt.data_ptr()), code, act, m,
+              ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+    return y
+
+
+def _fuse_dgrad_ok(x, w_master, dtype):
+    """The layer's data gradient can carry its input ReLU's backward: the
+    width-512 kernel or the narrow one fits (x: the chain's input)."""
+    return _dgrad512_ok(x, w_master, dtype) or (
+        x.dim() == 2 and _narrow_ok(x, w_master.size(0), w_master.size(1), dtype))
+
+
 class _LinearReLU(torch.autograd.Function):
     """y = relu(x W^T) with the ReLU in the GEMM epilogue: hipBLASLt's
     `_addmm_activation` with a zero bias (one kernel instead of GEMM + an
@@ -422,7 +462,11 @@ class _LinearReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w_master, dtype, cache=False, mask_gx=False, gy_masked=False, link=None):
         w = cast_weight(w_master, dtype, cache)
-        if x.is_cuda:
+        # (grad mode is off inside forward: training is "an input needs grad")
+        if (x.is_cuda and any(ctx.needs_input_grad[:2]) and _narrow_ok(x, w.size(1), w.size(0), dtype, True)
+                and x.dtype == dtype and x.dim() == 2):
+            y = _narrow(x, w, 1)
+        elif x.is_cuda:
             bias = _zero_bias(w.size(0), dtype, x.device)
             if _tuned_gemm(x, w):
                 with _tuned_window():
@@ -442,7 +486,11 @@ class _LinearReLU(torch.autograd.Function):
         g = gy.contiguous() if masked else torch.ops.aten.threshold_backward(gy, y, 0).contiguous()
         gx = None
         if ctx.needs_input_grad[0]:
-            gx = _dgrad512_masked(g, w, x) if ctx.mask_gx else _mm_dgrad(g, w)
+            narrow = _narrow_ok(g, w.size(0), w.size(1), w.dtype, True) and g.dtype == w.dtype
+            if ctx.mask_gx:
+                gx = _narrow(g, w.t(), 2, x) if narrow else _dgrad512_masked(g, w, x)
+            else:
+                gx = _narrow(g, w.t(), 0) if narrow else _mm_dgrad(g, w)
         gw = _wgrad(g, x) if ctx.needs_input_grad[1] else None
         return gx, gw, None, None, None, None, None
 
@@ -467,11 +515,14 @@ class MLP(nn.Module):
         output layer is applied to.  `link` (a one-element list, False): the
         last layer's backward skips its ReLU mask once a consumer that
         applies it sets link[0] (the fused head, renderer.FusedHeadCore)."""
+        return self._chain(x, list(self.layers[:-1]), link)
+
+    def _chain(self, x, hid, link=None):
+        """ReLU layers `hid` in order on x."""
         x = x.to(self.dtype).contiguous()
-        hid = list(self.layers[:-1])
         # layer i >= 1 takes layer i-1's ReLU output only: its data gradient
         # can carry that ReLU's backward (_LinearReLU's flags)
-        fuse = [i > 0 and _dgrad512_ok(x, lin.weight, self.dtype) for i, lin in enumerate(hid)]
+        fuse = [i > 0 and _fuse_dgrad_ok(x, lin.weight, self.dtype) for i, lin in enumerate(hid)]
         for i, lin in enumerate(hid):
             x = _LinearReLU.apply(x, lin.weight, self.dtype, not torch.is_grad_enabled(), fuse[i],
                                   i + 1 < len(hid) and fuse[i + 1], link if i + 1 == len(hid) else None)
@@ -508,11 +559,9 @@ class MLP(nn.Module):
         """The network; `out_relu=True` returns relu(output) with the ReLU in
         the last GEMM's epilogue (for callers that only use the rectified
         output, model.py:316, 323)."""
-        h = self.hidden(x)
-        if out_relu:
-            return _LinearReLU.apply(h.contiguous(), self.layers[-1].weight, self.dtype,
-                                     not torch.is_grad_enabled())
-        return self.last(h)
+        if out_relu:  # the output layer joins the ReLU chain
+            return self._chain(x, list(self.layers))
+        return self.last(self.hidden(x))
 
 
 class _Broadcast(torch.autograd.Function):

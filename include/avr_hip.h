@@ -322,6 +322,16 @@ int avr_linear_wgrad_splits(int64_t N, int32_t M, int32_t K, int32_t* splits);
  *        avr_linear_out1_workspace() floats).
  * Replaces the N x 1 GEMM, its broadcast-multiply data gradient and its
  * weight-gradient GEMM (x @ w^T, gy * w, gy^T @ x). */
+/* A narrow bias-free layer product, Y[N][C] = act(X[N][R] Bt[C][R]^T), 16-bit
+ * operands, fp32 sums rounded once: R in {80, 128, 256}, C a multiple of 4
+ * in [68, 256] (<= 128 when R = 256); act 0 none, 1 ReLU, 2 mask (0 where
+ * mask[N][C] <= 0, NaN keeps: threshold_backward's selection).  The sigma
+ * networks' layers in training (model.py:117-121, 259-262): forward
+ * relu(x W^T) with Bt = W, data gradient (g W) with Bt = W^T, the input
+ * ReLU's backward fused with act 2 (mask = the layer's input).  X, Bt
+ * 16-byte aligned, Y and mask 8-byte aligned. */
+int avr_narrow_mm(int64_t N, int32_t R, int32_t C, const void* X, const void* Bt, int32_t dtype, int32_t act,
+                  const void* mask, void* Y, void* stream);
 int avr_linear_out1_fwd(int64_t N, int32_t K, const void* x, const void* w, int32_t dtype, void* y, void* stream);
 int avr_linear_out1_workspace(int32_t K, int64_t* floats);
 int avr_linear_out1_bwd(int64_t N, int32_t K, const void* x, const void* w, const void* grad_y, int32_t dtype,

@@ -165,3 +165,59 @@ def test_mlp_training_chain_fused_dgrad(dtype, monkeypatch):
     for a, b in zip(*grads):
         rel = float((a - b).norm() / b.norm())
         assert float(b.norm()) > 0 and rel < 2e-2, rel
+
+
+# ---- narrow layers (avr_narrow_mm) ----
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
+@pytest.mark.parametrize("N,R,C", [(83200, 128, 128), (83200, 80, 128), (83200, 128, 256), (83200, 256, 128),
+                                   (83200, 128, 80), (1, 128, 128), (129, 256, 100), (777, 80, 68)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_narrow_mm_exact_on_integer_operands(dtype, N, R, C, act):
+    """Small-integer operands (exact fp32 sums): equal to the fp32 statement
+    rounded once, with no activation, ReLU, or threshold_backward's mask
+    (every class: +-0, +-inf, NaN, subnormal)."""
+    from avr_amd import model as M
+
+    gen = torch.Generator(device=DEV).manual_seed(N + R + C + act)
+    x = torch.randint(-2, 3, (N, R), device=DEV, generator=gen).to(dtype)
+    bt = torch.randint(-1, 2, (C, R), device=DEV, generator=gen).to(dtype)
+    mask = _mask_values(N, dtype, gen)[:, :C].contiguous() if C <= 512 else None
+    y = M._narrow(x, bt, act, mask if act == 2 else None)
+    torch.cuda.synchronize()
+    ref = (x.float() @ bt.float().t()).to(dtype)
+    if act == 1:
+        ref = torch.relu(ref)
+    elif act == 2:
+        ref = torch.ops.aten.threshold_backward(ref, mask, 0)
+    assert torch.equal(y, ref), int((y != ref).sum())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
+def test_narrow_chain_training_matches_hipblaslt(dtype, monkeypatch):
+    """The RAF sigma encoder's chain (80 -> 128 -> 128 -> 128 -> 256, ReLU on
+    every layer) trained through avr_narrow_mm (forward + data gradients with
+    the fused masks) against hipBLASLt + threshold_backward (AVR_NARROW=0):
+    the same roundings, fp32 sums in another order."""
+    from avr_amd import model as M
+
+    torch.manual_seed(4)
+    mlp = M.MLP(80, 256, {"n_neurons": 128, "n_hidden_layers": 3}, dtype=dtype).to(DEV)
+    x = torch.randn(20000, 80, device=DEV).to(dtype).requires_grad_(True)
+    r = torch.randn(20000, 256, device=DEV)
+    calls = []
+    fn = M._narrow
+    monkeypatch.setattr(M, "_narrow", lambda *a: calls.append(a[2]) or fn(*a))
+    res = []
+    for on in (True, False):
+        monkeypatch.setattr(M, "_NARROW", on)
+        mlp.zero_grad(set_to_none=True)
+        x.grad = None
+        out = mlp(x, out_relu=True)
+        (out.float() * r).sum().backward()
+        res.append([out.float().detach(), x.grad.float()] + [p.grad.clone() for p in mlp.parameters()])
+    torch.cuda.synchronize()
+    assert sorted(calls) == [0] + [1] * 4 + [2] * 3  # 4 forwards, 3 masked data gradients, 1 plain
+    for a, b in zip(*res):
+        rel = float((a - b).norm() / b.norm())
+        assert float(b.norm()) > 0 and rel < 2e-2, rel
