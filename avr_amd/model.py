@@ -406,15 +406,22 @@ def _dgrad512_masked(g, w, x):
 
 # The sigma networks' narrow layers (widths 80 .. 256) in training on
 # csrc/mlp.hip's `avr_narrow_mm` (forward with the ReLU, data gradient with
-# the input ReLU's backward); opt-in, AVR_NARROW=1 (default: hipBLASLt +
-# threshold_backward).
-_NARROW = os.environ.get("AVR_NARROW", "0") == "1"
+# the input ReLU's backward).  Timed against the tuned hipBLASLt solutions
+# (tools/bench_narrow.py, GPU time behind a spin): faster only where a side
+# is 80 wide (the RAF sigma encoder's first layer: 13.3 vs 17.9 us forward,
+# 14.4 vs 19.2 data gradient at 83,200 rows), slower at 128 / 256 (e.g.
+# 15.7 vs 14.0, and 32.6 vs 26.6 for the masked data gradient against
+# hipBLASLt + threshold_backward).  AVR_NARROW: "80" (default) those shapes
+# only, "1" every shape it takes, "0" none.
+_NARROW = os.environ.get("AVR_NARROW", "80")
 
 
 def _narrow_ok(x, R, C, dtype, in_backward=False):
     """Y[N, C] = act(X[N, R] Bt[C, R]^T) fits avr_narrow_mm (training only:
     grad mode on, or called from a backward)."""
-    return (_NARROW and x.is_cuda and (in_backward or torch.is_grad_enabled())
+    if _NARROW == "0" or (_NARROW != "1" and 80 not in (R, C)):
+        return False
+    return (x.is_cuda and (in_backward or torch.is_grad_enabled())
             and dtype in (torch.float16, torch.bfloat16)
             and R in (80, 128, 256) and 68 <= C <= 256 and C % 4 == 0 and (R < 256 or C <= 128))
 

@@ -210,7 +210,7 @@ def test_narrow_chain_training_matches_hipblaslt(dtype, monkeypatch):
     monkeypatch.setattr(M, "_narrow", lambda *a: calls.append(a[2]) or fn(*a))
     res = []
     for on in (True, False):
-        monkeypatch.setattr(M, "_NARROW", on)
+        monkeypatch.setattr(M, "_NARROW", "1" if on else "0")
         mlp.zero_grad(set_to_none=True)
         x.grad = None
         out = mlp(x, out_relu=True)
