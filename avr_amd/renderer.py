@@ -351,7 +351,7 @@ class FusedHeadCore(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, attn, h, w_master, dtype, p, tables, rays_o, position_tx, dirs, cache=False, exact=False,
-                relu_h=False):
+                relu_h=False, timer=None):
         dev = h.device
         B, K = h.size(0), h.size(-1)
         S, T = p.n_samples, p.T
@@ -374,8 +374,14 @@ class FusedHeadCore(torch.autograd.Function):
             part = torch.empty(n_split, B, S, T, dtype=torch.float32, device=dev)
             queue = torch.empty(256, dtype=torch.int32, device=dev)  # work-queue counters (zeroed by the call)
             Wf = _packed_exact_weight(w_master, W, cache, pref, (p.T, K, code), wbytes.value, st)
+            # (bench.py's timer: events around the head on its stream, torch's current one)
+            ev0, ev1 = timer.head_events(delay, tables.shift, K) if timer is not None else (None, None)
+            if ev0 is not None:
+                ev0.record()
             _lib.call("avr_head_fwd_exact", pref, B, K, _ptr(h), _ptr(Wf), code, _ptr(perm), _ptr(ws), _ptr(cnt),
                       _ptr(delay), n_split, _ptr(part), _ptr(queue), st)
+            if ev1 is not None:
+                ev1.record()
         else:
             ns = ctypes.c_int32(0)
             _lib.call("avr_head_splits", pref, B, K, code, ctypes.byref(ns))
@@ -413,7 +419,8 @@ class FusedHeadCore(torch.autograd.Function):
                   _ptr(work), nbytes.value, st)
         grad_attn = _grad_attn(p, tables, attn, grad_w, st) if ctx.needs_input_grad[0] else None
         return (grad_attn, grad_h if ctx.needs_input_grad[1] else None,
-                grad_W if ctx.needs_input_grad[2] else None, None, None, None, None, None, None, None, None, None)
+                grad_W if ctx.needs_input_grad[2] else None, None, None, None, None, None, None, None, None, None,
+                None)
 
 
 def _poison_nonfinite(out, tensors, ir_out=None):
@@ -716,7 +723,7 @@ class AVRRender(nn.Module):
             relu_h = relu_link is not None and torch.is_grad_enabled()
             out = FusedHeadCore.apply(attn, h, weight, dtype, p, tables, geom["rays_o"],
                                       geom["position_tx"], geom["dirs"], not torch.is_grad_enabled(), exact,
-                                      relu_h)
+                                      relu_h, self.kernel_timer)
             if relu_h:
                 relu_link[0] = True
             if self.propagate_nonfinite:

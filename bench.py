@@ -94,6 +94,22 @@ class KernelTimer:
         self.used += 1
         return a.cuda_event, b.cuda_event
 
+    def head_events(self, delay=None, shift=None, K=0):
+        """(begin, end) torch events to record around the rounding-exact head's
+        launch (FusedHeadCore, network mode: the fused head replaces the ray
+        reduction), or Nones.  Keeps the launch's delays for the live count."""
+        if not self.enabled:
+            return None, None
+        if not hasattr(self, "head_pool"):
+            self.head_pool, self.head_rows, self.head_K = [], [], K
+        if len(self.head_pool) >= len(self.pool):
+            return None, None
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        self.head_pool.append(ev)
+        self.head_rows.append((delay, shift))
+        self.head_K = K
+        return ev
+
     def mean_ms(self):
         ts = [a.elapsed_time(b) for a, b in self.pool[:self.used]]
         return sum(ts) / len(ts) if ts else float("nan")
@@ -277,6 +293,58 @@ def roofline(w, timer, dt):
         "avg_launch_ms": k_ms,
         "measured": "HIP events around each launch, roofline phase of K steps on one stream",
     }
+
+
+MFMA_PEAK_TFS_16 = 2500.0  # MI355X_MICROARCH.md: fp16 / bf16 dense MFMA, ~2.5 PF/s
+
+
+def head_roofline(w, timer):
+    """Roofline object for the rounding-exact head (network mode): algorithmic
+    FLOPs = 2 K x the live (ray-sample, t) elements of the launch (the
+    [delay, T-1-shift[s]) windows, the only products the render uses), over
+    the launch's HIP-event duration; against the dense 16-bit MFMA peak."""
+    pool = getattr(timer, "head_pool", [])
+    if not pool:
+        return None
+    ts = [a.elapsed_time(b) for a, b in pool]
+    k_ms = sum(ts) / len(ts)
+    T, K = w.T, timer.head_K
+    live = 0.0
+    for delay, shift in timer.head_rows:
+        lim = (T - 1 - shift.long()).clamp(min=0)
+        live += float((lim.view(1, 1, -1) - delay.long()).clamp(min=0).sum())
+    live /= len(timer.head_rows)
+    rows = timer.head_rows[0][0].numel()
+    flops = 2.0 * K * live
+    achieved = flops / (k_ms * 1e-3) / 1e12
+    traffic, src = None, None
+    for path in sorted(glob_profiles("r*_pmc_c5_network_fp16.json")):
+        d = json.load(open(path))
+        for k, v in d.items():
+            if k.startswith("head_exact_kernel<__half") and w.name.startswith("c5_"):
+                traffic = v["derived"]["hbm_read_bytes"] + v["derived"]["hbm_write_bytes"]
+                src = os.path.relpath(path, ROOT)
+    return {
+        "kernel": "head_exact_kernel",
+        "bound": "mfma",
+        "achieved": achieved,
+        "peak": MFMA_PEAK_TFS_16,
+        "unit": "TFLOP/s",
+        "frac": achieved / MFMA_PEAK_TFS_16,
+        "traffic": traffic,
+        "traffic_source": src,
+        "alg_flops_per_launch": flops,
+        "dense_flops_per_launch": 2.0 * K * rows * T,
+        "live_fraction": live / (rows * T) if rows else 0.0,
+        "avg_launch_ms": k_ms,
+        "measured": "HIP events around each head launch on its stream, the timed steps",
+    }
+
+
+def glob_profiles(pattern):
+    import glob
+
+    return glob.glob(os.path.join(ROOT, "profiles", pattern))
 
 
 def cpu_baseline(w, budget_s=15.0, mode="pose"):
@@ -638,8 +706,9 @@ def bench_ray_shard(args, w, world, rank, dev):
     elapsed, t_issue = timed(lambda: run(args.steps), world, dev)
     value = whole_job_rate(w.ray_samples, 1, args.steps, elapsed)  # one pose per step, all ranks
     res = _base_result(args, w, world, value, elapsed, "f32" if dt == torch.float32 else "f16-storage/f32-math")
-    # with the network the fused head replaces the ray reduction (no events)
-    rf = roofline(w, timer, dt) if not args.network else None
+    # with the network the fused head replaces the ray reduction: the head's
+    # own events (FusedHeadCore, rounding-exact 16-bit head)
+    rf = roofline(w, timer, dt) if not args.network else head_roofline(w, timer)
     if args.network:
         res["dtype"] = args.mlp_dtype + " MLP / f32 render"
         res["data"] = "synthetic poses; AVRModel (avr_simu.yml model block), random init, evaluated per ray shard"
