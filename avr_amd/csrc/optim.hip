@@ -75,56 +75,6 @@ extern "C" int avr_scale_sanitize(int32_t n_tensors, float* const* ptrs, const i
 }
 
 // ----------------------------------------------------------------------------
-// The fp32 master weights of every MLP layer cast to the GEMM's 16-bit type
-// in ONE launch per training forward (model.py's layers, wcache.precast):
-// each layer's own `w.to(bf16)` was a ~4 us launch-bound copy, 11 of them
-// per config-3 step.  Round to nearest even, as torch's cast.
-struct CastTable {
-    const float* src[kMaxTensors];
-    uint16_t* dst[kMaxTensors];
-    int64_t n[kMaxTensors];
-};
-
-template <typename E>
-__global__ __launch_bounds__(256) void cast16_multi_kernel(CastTable tab) {
-    const int t = blockIdx.y;
-    const float* __restrict__ src = tab.src[t];
-    uint16_t* __restrict__ dst = tab.dst[t];
-    const int64_t n = tab.n[t];
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const E v = (E)src[i];
-        dst[i] = *reinterpret_cast<const uint16_t*>(&v);
-    }
-}
-
-extern "C" int avr_cast16_multi(int32_t n_tensors, const float* const* src, void* const* dst, const int64_t* sizes,
-                                int32_t dtype, void* stream) {
-    AVR_REQUIRE(n_tensors >= 0 && (n_tensors == 0 || (src && dst && sizes)), "avr_cast16_multi: bad args");
-    AVR_REQUIRE(dtype == AVR_DTYPE_F16 || dtype == AVR_DTYPE_BF16, "avr_cast16_multi: fp16 or bf16 target");
-    for (int base = 0; base < n_tensors; base += kMaxTensors) {
-        CastTable tab{};
-        const int cnt = n_tensors - base < kMaxTensors ? n_tensors - base : kMaxTensors;
-        int64_t biggest = 1;
-        for (int i = 0; i < cnt; ++i) {
-            AVR_REQUIRE((src[base + i] && dst[base + i]) || sizes[base + i] == 0, "avr_cast16_multi: null tensor");
-            tab.src[i] = src[base + i];
-            tab.dst[i] = static_cast<uint16_t*>(dst[base + i]);
-            tab.n[i] = sizes[base + i];
-            if (sizes[base + i] > biggest) biggest = sizes[base + i];
-        }
-        int64_t blocks = (biggest + 255) / 256;
-        if (blocks > 1024) blocks = 1024;
-        const dim3 grid((unsigned)blocks, (unsigned)cnt);
-        if (dtype == AVR_DTYPE_F16)
-            hipLaunchKernelGGL(cast16_multi_kernel<__half>, grid, dim3(256), 0, as_stream(stream), tab);
-        else
-            hipLaunchKernelGGL(cast16_multi_kernel<__hip_bfloat16>, grid, dim3(256), 0, as_stream(stream), tab);
-        if (int e = check_launch("avr_cast16_multi")) return e;
-    }
-    return 0;
-}
-
-// ----------------------------------------------------------------------------
 // Fused gradient post-processing + Adam (avr_runner.py:190-200: clip,
 // NaN/Inf zeroing, optimizer.step() of torch.optim.Adam(betas, eps,
 // weight_decay), amsgrad off): per element, in one pass over p, g, m, v,

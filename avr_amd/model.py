@@ -18,7 +18,7 @@ import torch.nn.functional as F
 from . import sigma as _sigma
 from .concat import grouped_concat
 from .encoding import HashGridEncoding
-from .wcache import cache_lookup, cache_store, capturing, cast_weight, precast
+from .wcache import cache_lookup, cache_store, capturing, cast_weight
 
 
 import os
@@ -165,9 +165,6 @@ def _out1_ok(h, w_master, dtype):
     return (_OUT1 and h.is_cuda and torch.is_grad_enabled() and dtype in (torch.float16, torch.bfloat16)
             and w_master.size(0) == 1 and h.dim() == 2 and 8 <= K <= 512 and K & (K - 1) == 0)
 
-
-# one cast launch for all MLP weights per training forward (AVR_PRECAST=0: per layer)
-_PRECAST = os.environ.get("AVR_PRECAST", "1") != "0"
 
 _ZERO_BIAS: dict = {}
 
@@ -845,21 +842,12 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
     supports_fused_head = True
     draws_no_device_rng = True
 
-    def _precast_mlps(self, pts):
-        """Training: every MLP weight cast to the MLP dtype in one launch
-        (wcache.precast) before the layers ask for their copies."""
-        if _PRECAST and pts.is_cuda and torch.is_grad_enabled():
-            precast([lin.weight for m in (self._model_encoder_sigma, self._model_decoder_sigma, self._model_signal)
-                     for lin in m.layers], self._model_signal.dtype)
-
     def forward(self, pts, view, tx, tx_view, ray_layout=None):
-        self._precast_mlps(pts)
         attn, base = self._trunk(pts, view, tx, tx_view, ray_layout)
         signal = self._model_signal(base)
         return attn, signal.reshape(pts.size(0), pts.size(1), self.signal_output_dim)
 
     def forward_fused(self, pts, view, tx, tx_view, ray_layout=None):
-        self._precast_mlps(pts)
         attn, base = self._trunk(pts, view, tx, tx_view, ray_layout)
         link = [False]  # the fused head may take over h's ReLU backward (MLP.hidden)
         h = self._model_signal.hidden(base, link)

@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import torch
 
-_CACHE_ATTRS = ("_avr_cast", "_avr_bias_cols", "_avr_headpack", "_avr_exactpack", "_avr_linpack", "_avr_precast")
+_CACHE_ATTRS = ("_avr_cast", "_avr_bias_cols", "_avr_headpack", "_avr_exactpack", "_avr_linpack")
 
 
 def capturing() -> bool:
@@ -69,44 +69,10 @@ def cache_store(owner, attr, key, value):
     return value
 
 
-def precast(params, dtype: torch.dtype) -> None:
-    """Cast every fp32 parameter in `params` to `dtype` (fp16 / bf16) in ONE
-    launch (`avr_cast16_multi`) and keep each copy on its parameter under
-    (storage, version, dtype): the training forward's per-layer casts then
-    find them (`cast_weight`, cache or not), one launch instead of one per
-    layer.  A later in-place update bumps the version and the copy is not
-    used again."""
-    if capturing() or dtype not in (torch.float16, torch.bfloat16):
-        return
-    todo = [p for p in params if p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()
-            and cache_lookup(p, "_avr_precast", (p.data_ptr(), p._version, dtype, p.device)) is None]
-    if not todo:
-        return
-    import ctypes
-
-    from . import _lib
-
-    outs = [torch.empty(p.shape, dtype=dtype, device=p.device) for p in todo]
-    n = len(todo)
-    src = (ctypes.c_void_p * n)(*[p.data_ptr() for p in todo])
-    dst = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
-    sizes = (ctypes.c_int64 * n)(*[p.numel() for p in todo])
-    code = _lib.DTYPE_F16 if dtype == torch.float16 else _lib.DTYPE_BF16
-    with torch.cuda.device(todo[0].device):
-        _lib.call("avr_cast16_multi", n, src, dst, sizes, code, torch.cuda.current_stream().cuda_stream)
-    for p, o in zip(todo, outs):
-        cache_store(p, "_avr_precast", (p.data_ptr(), p._version, dtype, p.device), o)
-
-
 def cast_weight(w: torch.Tensor, dtype: torch.dtype, cache: bool = True) -> torch.Tensor:
-    """w.to(dtype).contiguous(), cached on `w` while it is unchanged (and
-    the `precast` copy of the current version wherever one exists)."""
+    """w.to(dtype).contiguous(), cached on `w` while it is unchanged."""
     if w.dtype == dtype and w.is_contiguous():
         return w
-    if not capturing() and getattr(w, "_avr_precast", None) is not None:
-        hit = cache_lookup(w, "_avr_precast", (w.data_ptr(), w._version, dtype, w.device))
-        if hit is not None:
-            return hit
     if not cache or capturing():
         return w.to(dtype).contiguous()
     key = (w.data_ptr(), w._version, dtype, w.device)

@@ -567,12 +567,6 @@ int avr_das_bwd(int32_t n, const float* steer, const float* angles, const float*
  * launch per 32 tensors. */
 int avr_scale_sanitize(int32_t n_tensors, float* const* ptrs, const int64_t* sizes,
                        const float* coef, void* stream);
-/* dst[i] = (16-bit) src[i] for n_tensors fp32 tensors in one launch (round
- * to nearest even, torch's cast): the MLP layers' fp32 master weights cast
- * to the GEMM dtype once per training forward (model.py's tcnn layers run
- * 16-bit GEMMs on fp32-held parameters). dtype AVR_DTYPE_F16 / _BF16. */
-int avr_cast16_multi(int32_t n_tensors, const float* const* src, void* const* dst, const int64_t* sizes,
-                     int32_t dtype, void* stream);
 /* The same post-processing fused with torch.optim.Adam's update (amsgrad
  * off, L2 weight_decay; avr_runner.py:67-69, 190-200), one pass per element:
  *   g = finite(g*coef) ? g*coef : 0;  g += weight_decay * p;

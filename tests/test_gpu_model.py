@@ -276,30 +276,3 @@ def test_linear_out1_matches_torch(dtype, N, K, monkeypatch):
     assert all(torch.equal(a, b) for a, b in zip(*outs))
     gw64 = gr.double().t() @ xr.detach().double()
     assert float((outs[0][2].double() - gw64).norm() / gw64.norm()) < 1e-5
-
-
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16], ids=["bf16", "fp16"])
-def test_precast_equals_torch_cast(dtype):
-    """wcache.precast (avr_cast16_multi, one launch for many weights) gives
-    the bit pattern of w.to(dtype) for every fp32 value class, and
-    cast_weight hands the copy out only while the weight's version matches."""
-    from avr_amd.wcache import cast_weight, precast
-
-    g = torch.Generator(device=DEV).manual_seed(9)
-    ws = [torch.randn(n, device=DEV, generator=g) * s for n, s in ((1, 1.0), (1000, 1e-3), (70000, 3e4), (512, 1e-40))]
-    ws.append(torch.tensor([0.0, -0.0, float("inf"), float("-inf"), float("nan"), 65504.0, 65520.0, 1e-8,
-                            3.3895e38, -1.17549e-38, 2.0 ** -149], device=DEV))
-    ws.append(torch.randn(40, 35, device=DEV, generator=g))  # more tensors than one table holds
-    ws += [torch.randn(17, device=DEV, generator=g) for _ in range(40)]
-    precast(ws, dtype)
-    for w in ws:
-        c = cast_weight(w, dtype, cache=False)
-        ref = w.to(dtype)
-        assert c.dtype == dtype and c.shape == w.shape
-        assert torch.equal(c.view(torch.int16), ref.view(torch.int16))
-    w = ws[1]
-    before = cast_weight(w, dtype, cache=False)
-    w.add_(1.0)  # version bump: the copy is stale
-    after = cast_weight(w, dtype, cache=False)
-    assert after.data_ptr() != before.data_ptr()
-    assert torch.equal(after, w.to(dtype))
