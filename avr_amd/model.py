@@ -461,10 +461,13 @@ class _LinearReLU(torch.autograd.Function):
     In a chain of such layers (`MLP.hidden`) two flags move each ReLU's
     backward into the GEMM that produces its gradient: `mask_gx` (x is the
     previous layer's ReLU output and this layer its only consumer) returns
-    the data gradient already masked by x > 0 (`_dgrad512_masked`), and
+    the data gradient already masked by x > 0 (`_dgrad512_masked` for the
+    512 -> 512 layers, `_narrow` with its mask epilogue where that applies), and
     `gy_masked` (the consumer of y did so) skips the threshold.  The mask is
     the same selection threshold_backward makes (y > 0 with y = the next
-    layer's x), applied to the same rounded values."""
+    layer's x), applied to the same rounded values.  `link` (the last layer
+    of `MLP.hidden`): a one-element list the output's consumer sets when it
+    applies the mask itself (the fused head)."""
 
     @staticmethod
     def forward(ctx, x, w_master, dtype, cache=False, mask_gx=False, gy_masked=False, link=None):
