@@ -938,10 +938,13 @@ int head_check(const avr_render_params* p, int B, int K, const void* h, const vo
 }
 
 // dW workgroups: (feature block, sample group, b), ~1024 of them
+#ifndef AVR_HEAD_DW_TARGET
+#define AVR_HEAD_DW_TARGET 512  // head_bwd_w workgroups aimed for (1024: 4 us slower per config-3 step, plus 3 us of partial sums)
+#endif
 void dw_groups(const HeadShape& hs, int B, int S, int K, int* n_sg, int* s_per) {
     const int nkb = K / hs.kb;
     int n = 1;
-    while (n < S && (int64_t)nkb * n * B < 1024) n *= 2;
+    while (n < S && (int64_t)nkb * n * B < AVR_HEAD_DW_TARGET) n *= 2;
     *s_per = (S + n - 1) / n;
     *n_sg = (S + *s_per - 1) / *s_per;
 }

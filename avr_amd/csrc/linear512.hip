@@ -71,7 +71,6 @@ constexpr int kLSlot = 2 * kLXBytes;              // + the W fragments (same siz
 constexpr int kLStage = 4096;                     // per-wave transpose area
 constexpr int kLLds = kLSlots * kLSlot + 8 * kLStage;  // 160 KiB
 constexpr int kLOpsPerChunk = 2 * kLXBytes / 1024 / 8;  // DMA instructions per wave and chunk
-constexpr int kLStores = 16;                      // y stores per wave and tile
 static_assert(kLKC == 32 || kLKC == 64, "chunk");
 
 // slot of piece p of row r (XOR swizzle: conflict-free fragment reads)
