@@ -13,6 +13,7 @@ from .renderer import (  # noqa: F401
     spectrum_to_ir,
 )
 from .criterion import Criterion  # noqa: F401
+from .options import KernelOptions  # noqa: F401
 from . import workloads  # noqa: F401
 
 __version__ = "0.1.0"

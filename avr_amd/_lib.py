@@ -135,12 +135,8 @@ _SIGS = {
     "avr_hashgrid_bwd_partitioned_set": (ctypes.c_int, [_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp, _vp, _vp, _vp,
                                                     _c_i64, _vp]),
     "avr_linear_wgrad_splits": (ctypes.c_int, [_c_i64, _c_i32, _c_i32, _vp]),
-    "avr_linear512_pack_w": (ctypes.c_int, [_vp, _c_i32, _vp, _vp]),
-    "avr_linear512_relu_fwd": (ctypes.c_int, [_c_i64, _vp, _vp, _c_i32, _vp, _vp]),
     "avr_linear512_pack_w2": (ctypes.c_int, [_vp, _c_i32, _c_i32, _vp, _vp]),
     "avr_linear512_mask_fwd": (ctypes.c_int, [_c_i64, _vp, _vp, _c_i32, _vp, _vp, _vp]),
-    "avr_mlp512x2_pack_w": (ctypes.c_int, [_vp, _vp, _c_i32, _vp, _vp]),
-    "avr_mlp512x2_fwd": (ctypes.c_int, [_c_i64, _vp, _vp, _c_i32, _vp, _vp]),
     "avr_linear_wgrad": (ctypes.c_int, [_c_i64, _c_i32, _c_i32, _vp, _vp, _vp, _c_i32, _vp, _vp]),
     "avr_linear_out1_fwd": (ctypes.c_int, [_c_i64, _c_i32, _vp, _vp, _c_i32, _vp, _vp]),
     "avr_narrow_mm": (ctypes.c_int, [_c_i64, _c_i32, _c_i32, _vp, _vp, _c_i32, _c_i32, _vp, _vp, _vp]),
@@ -182,6 +178,16 @@ _SIGS = {
 
 EXPORTS = tuple(_SIGS)
 
+# entry points of the shapes build only (include/avr_hip.h, AVR_SHAPE_PROBES):
+# typed when a tool loads that library in place of the product one
+_SHAPES_SIGS = {
+    "avr_linear512_pack_w": (ctypes.c_int, [_vp, _c_i32, _vp, _vp]),
+    "avr_linear512_relu_fwd": (ctypes.c_int, [_c_i64, _vp, _vp, _c_i32, _vp, _vp]),
+    "avr_mlp512x2_pack_w": (ctypes.c_int, [_vp, _vp, _c_i32, _vp, _vp]),
+    "avr_mlp512x2_fwd": (ctypes.c_int, [_c_i64, _vp, _vp, _c_i32, _vp, _vp]),
+    "avr_linear_pack_w": (ctypes.c_int, [_c_i32, _c_i32, _vp, _c_i32, _vp, _vp]),
+}
+
 _lock = threading.Lock()
 _lib = None
 
@@ -203,6 +209,11 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        for name, (res, args) in _SHAPES_SIGS.items():
+            if hasattr(lib, name):
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
         if lib.avr_abi_version() != 2:
             raise RuntimeError("avr_amd: libavr_hip.so ABI version mismatch")
         _lib = lib

@@ -21,6 +21,9 @@ namespace avr {
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
 int check_launch(const char* what);
+// compute units of the current device, queried once per device
+// (std::call_once: safe from concurrent host threads, e.g. nn.DataParallel)
+int device_cus();
 
 #define AVR_REQUIRE(cond, msg)                          \
     do {                                                \
@@ -33,6 +36,24 @@ int launch_irfft(int B, int F, const float* spec, const float* spec2, const floa
                  float* ir2, void* stream);
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------- MFMA operand hold
+// A register an MFMA reads as SrcB must not be rewritten while that MFMA may
+// still wait in the matrix pipe's queue (the bf16x3
+// DFT returned stale B-operand lanes when the compiler refilled a B register
+// right behind a queued MFMA).  At the end of an MFMA chain: every MFMA of
+// the chain issues first (sched_barrier: nothing crosses), then 8 wait states
+// (one 32x32 MFMA's passes), then each operand is used once more, so its
+// register is not reallocated before that point.  tests/test_isa_audit.py
+// checks the compiled library for the pattern.
+__device__ __forceinline__ void mfma_queue_wait() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7");
+}
+template <typename T>
+__device__ __forceinline__ void keep_live(const T& v) {
+    asm volatile("" ::"v"(v));
+}
 
 // ---------------------------------------------------------------- dtypes
 __device__ __forceinline__ float load_f(const float* p, int64_t i) { return p[i]; }

@@ -1,6 +1,7 @@
 // Thread-local error reporting for the C-ABI (include/avr_hip.h).
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <string>
 
 #include "common.h"
@@ -23,6 +24,20 @@ int check_launch(const char* what) {
         return (int)e;
     }
     return 0;
+}
+
+int device_cus() {
+    constexpr int kMaxDev = 64;
+    static std::once_flag once[kMaxDev];
+    static int cus[kMaxDev];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return 256;
+    std::call_once(once[dev], [dev] {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+        cus[dev] = n;
+    });
+    return cus[dev];
 }
 
 }  // namespace avr

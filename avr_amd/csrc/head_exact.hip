@@ -83,18 +83,8 @@ __device__ __forceinline__ float round16(float x) {
 // the builtin it inserts vmcnt(0) inside the MFMA chain); completion is
 // waited for explicitly with counted vmcnt.
 __device__ __forceinline__ void dma_row16(const void* g, uint32_t lds) {
-#if AVR_EXACT_XCHAIN_RFL
-    lds = __builtin_amdgcn_readfirstlane(lds);  // kept in an SGPR under pressure
-#endif
-#if AVR_EXACT_DMA_NOMEM
-    // no "memory" clobber: the B-fragment reads of other ring slots may be
-    // scheduled across the DMA (its slot's reuse is ordered by the barriers,
-    // which keep their place relative to this volatile statement)
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(g));
-#else
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(g)
                  : "memory", "m0");
-#endif
 }
 
 // s_waitcnt vmcnt(n) (expcnt / lgkmcnt not waited on; gfx9 encoding)
@@ -128,56 +118,18 @@ __device__ __forceinline__ int opaque_tid() {
 
 // bytes of one 32-t W tile in fragment order: KSM k-steps x 64 lanes x 16 B
 __host__ __device__ constexpr int xs_tile_bytes(int KSM) { return KSM * 1024; }
-// Stagger (MI355X_MICROARCH.md, two waves per SIMD, item 9): waves
-// WAVES/2 .. WAVES-1 defer the epilogue of each tile's last chain past the
-// tile's barrier, into the next tile, so that on every SIMD one wave's
-// epilogue VALU runs beside its partner's MFMA chain instead of both waves
-// rounding at once with the matrix pipe idle.  A tile's wave partials are then
-// complete one barrier later: three partial buffers instead of two.
-#ifndef AVR_EXACT_STAGGER
-#define AVR_EXACT_STAGGER 0
-#endif
-#ifndef AVR_EXACT_DMA_WAVES
-#define AVR_EXACT_DMA_WAVES 0
-#endif
-#ifndef AVR_EXACT_DMA_SPREAD
-#define AVR_EXACT_DMA_SPREAD 0
-#endif
-// Slot flags instead of a workgroup barrier per tile (32-t tiles, a 4-slot
-// ring): per slot a FULL count (loader waves whose pieces landed), a DONE
-// count (waves through the tile; the last one to arrive sums the partials)
-// and a FREE count (the last arriver's release of the slot).  Waves drift
-// apart by up to one tile, so a wave's epilogue and DMA issue fall beside
-// its SIMD partner's MFMA chain.
-#ifndef AVR_EXACT_FLAGS
-#define AVR_EXACT_FLAGS 0
-#endif
-// B fragments read ahead in the MFMA chain; XCHAIN: the two chains of a
-// 64-t tile as one B-fragment stream (the second chain's first fragments are
-// read during the first chain's tail and land under its epilogue)
-#ifndef AVR_EXACT_D
-#define AVR_EXACT_D 8
-#endif
-#ifndef AVR_EXACT_XCHAIN
-#define AVR_EXACT_XCHAIN 0
-#endif
-// PREFETCH = k > 0: k tiles before an item's end, every wave touches each
-// 128-byte line of its next item's 32 rows (four dword loads per lane), so
-// that the next prologue's row loads find them in L2 / the Infinity Cache
-#ifndef AVR_EXACT_PREFETCH
-#define AVR_EXACT_PREFETCH 0
-#endif
-#ifndef AVR_EXACT_NC1  // the barrier form on 32-t tiles and a 4-slot ring (the flags form's shape)
-#define AVR_EXACT_NC1 0
-#endif
-// partial buffers: one per tile in flight (flags: one per ring slot, the
-// partials of tile i live in zr[i % 4] until its last arriver sums them)
-constexpr int kPartBufs = AVR_EXACT_FLAGS ? 4 : (AVR_EXACT_STAGGER ? 3 : 2);
-// (placed after the flag switches below, which need four)
+// wave partials: one buffer per tile in flight (tile i's in zr[i % 2] until
+// the wave that sums it has read them, two barriers later)
+constexpr int kPartBufs = 2;
+// B fragments read ahead from the ring in an MFMA chain, and the MFMAs
+// (each at least two instructions: the MFMA and a ring read) after which a
+// fragment's register may be reused: 8 wait states
+constexpr int kReadAhead = 8;
+constexpr int kHold = 4;
 
 __host__ __device__ constexpr size_t xs_lds_bytes(int KSM, int T, int waves, int rays, int nb, int nc) {
     return (size_t)nb * nc * xs_tile_bytes(KSM) + 4 * (size_t)((T + 3) / 4 * 4) + 4 * (size_t)rays +
-           4 * (size_t)(kPartBufs * waves * 32 * nc) + 4 * (size_t)waves + 8 + 64;
+           4 * (size_t)(kPartBufs * waves * 32 * nc) + 4 * (size_t)waves + 8;
 }
 
 // One work item: RAYS consecutive sorted rays of one column (b, s), WAVES
@@ -194,15 +146,13 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
     constexpr int TT = 32 * NC;
     constexpr int RPW = RAYS / WAVES;    // rays per wave
     constexpr int NQ = RPW / 32;         // 32-ray A tiles per wave
-    // W-tile DMA pieces (1 KiB each): issued by every wave, or only by one
-    // half of the waves (AVR_EXACT_DMA_WAVES 1: waves 0 .. WAVES/2-1, 2: the
-    // other half), so that on every SIMD one wave's DMA issue stalls fall
-    // beside its partner's MFMAs; spread over all the tile's chains or all in
-    // its first live chain (AVR_EXACT_DMA_SPREAD)
-    constexpr int LW = AVR_EXACT_DMA_WAVES == 0 ? WAVES : WAVES / 2;  // loader waves
-    constexpr int DPW = NC * KSM / LW;                                // pieces per loader wave and tile
-    constexpr int PPC = AVR_EXACT_DMA_SPREAD ? DPW / NC : DPW;        // pieces per chain
-    static_assert((NC * KSM) % LW == 0 && NQ == 1 && DPW * NB <= 63 && NT >= RAYS && KSM % PPC == 0, "shape");
+    // W-tile DMA pieces (1 KiB each), issued by every wave inside the tile's
+    // first live chain
+    constexpr int DPW = NC * KSM / WAVES;  // pieces per wave and tile
+    static_assert((NC * KSM) % WAVES == 0 && NQ == 1 && DPW * NB <= 63 && NT >= RAYS && KSM % DPW == 0, "shape");
+    // the partial buffers zr[i % kPartBufs] written in iteration i are read
+    // after its barrier; rewritten in iteration i + kPartBufs, past one more
+    static_assert(kPartBufs == 2, "the tile loop's partial-buffer rotation assumes two buffers");
     AVR_PROBE_DECL;
     extern __shared__ __attribute__((aligned(16))) char lds_x[];
     const int T = pp.T, S = pp.n_samples;
@@ -213,15 +163,9 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
     float* zr = wl + RAYS;                                      // wave partials [kPartBufs][WAVES][TT]
     int* dstart = reinterpret_cast<int*>(zr + kPartBufs * WAVES * TT);  // first live t per wave [WAVES]
     int* qnext = dstart + WAVES;                                // claimed items [2]
-    int* fl_full = qnext + 2;                                   // slot flags [3][4] (AVR_EXACT_FLAGS)
-    int* fl_done = fl_full + 4;
-    int* fl_free = fl_full + 8;
-    constexpr bool kFlags = AVR_EXACT_FLAGS && NC == 1 && NB == 4;
 
     const int64_t ncol = (int64_t)B * S;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool loader = AVR_EXACT_DMA_WAVES == 0 || ((AVR_EXACT_DMA_WAVES == 1) == (wave < WAVES / 2));
-    const int lidx = AVR_EXACT_DMA_WAVES == 2 ? wave - WAVES / 2 : wave;  // loader index (if loader)
     // static priority for the second-dispatched half of the waves (the
     // arbitration loser of every segment; MI355X_MICROARCH.md, two waves per SIMD)
     if (prio && wave >= WAVES / 2) __builtin_amdgcn_s_setprio(1);
@@ -360,7 +304,6 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             }
             if (tid < RAYS) wl[tid] = p0 + tid < nk ? cur.wsv : 0.0f;
             if (lane == 0) dstart[wave] = pw < nk ? cur.dly : 1 << 30;
-            if (kFlags && tid < 12) fl_full[tid] = tid < 3 ? LW : 0;  // tiles 0-2: landed in the prologue
             // staging area free (the ring may fill); cl, wl, dstart written.  A
             // bare barrier: nothing in flight on the vector-memory counter is
             // waited for (the claim's atomic)
@@ -369,15 +312,14 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             AVR_PROBE_MARK(10);
             const int tb = dstart[0] / TT;       // first tile with a live ray of the item
             const int te = (lim + TT - 1) / TT;  // tiles holding t < lim
-            // W tile tau into ring slot `slot`: this loader wave's pieces p0 .. p1-1
-            auto issue_pieces = [&](int tau, int slot, int p0, int p1) {
-                if (AVR_PROBE_SKIP(1) || !loader) return;
+            // W tile tau into ring slot `slot`: this wave's pieces
+            auto issue = [&](int tau, int slot) {
+                if (AVR_PROBE_SKIP(1)) return;
                 const char* src =
-                    reinterpret_cast<const char*>(Wf) + (int64_t)tau * TILE + lidx * DPW * 1024 + 16 * lane;
-                const uint32_t dst = ring_lds + slot * TILE + lidx * DPW * 1024;
-                for (int d = p0; d < p1; ++d) dma_row16(src + d * 1024, dst + d * 1024);
+                    reinterpret_cast<const char*>(Wf) + (int64_t)tau * TILE + wave * DPW * 1024 + 16 * lane;
+                const uint32_t dst = ring_lds + slot * TILE + wave * DPW * 1024;
+                for (int d = 0; d < DPW; ++d) dma_row16(src + d * 1024, dst + d * 1024);
             };
-            auto issue = [&](int tau, int slot) { issue_pieces(tau, slot, 0, DPW); };
             for (int i = 0; i < NB - 1; ++i)
                 if (tb + i < te) issue(tb + i, i);
             // the next item's metadata: in flight under this item, younger than
@@ -411,26 +353,41 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
             // each stalls the wave ~100 cycles behind the previous one
             // (tools/probe_phases.py), while between MFMAs the stall overlaps
             // the matrix pipe.
-            // pieces pbase .. pbase + PPC - 1 of tile dtile (if >= 0) issued
-            // inside the chain, one every KSM / PPC MFMAs
-            auto chain = [&](int slot, int c, int dtile, int dslot, int pbase) {
+            // the wave's DMA pieces of tile dtile (if >= 0) issued inside the
+            // chain, one every KSM / DPW MFMAs
+            auto chain = [&](int slot, int c, int dtile, int dslot) {
                 const char* bsrc = ring + slot * TILE + c * xs_tile_bytes(KSM) + 16 * lane;
-                constexpr int D = KSM < AVR_EXACT_D ? KSM : AVR_EXACT_D;  // B fragments read ahead
-                constexpr int DSTEP = KSM / PPC;      // MFMAs per DMA piece
-                frag8 bw[D];
+                constexpr int D = KSM < kReadAhead ? KSM : kReadAhead;  // B fragments read ahead
+                // a ring of D + kHold fragments: the read for k-step ks + D
+                // (issued after MFMA ks) goes into the slot of k-step
+                // ks - kHold, and the fragments of k-steps ks - kHold + 1 ..
+                // ks are used once more after MFMA ks (program order fixed by
+                // the sched_barrier), so the read is never allocated onto the
+                // B register of one of the last kHold MFMAs, which may still
+                // wait in the matrix pipe's queue (common.h, §15a)
+                constexpr int RS = D + kHold;
+                constexpr int DSTEP = KSM / DPW;      // MFMAs per DMA piece
+                frag8 bw[RS];
 #pragma unroll
                 for (int u = 0; u < D; ++u) bw[u] = *reinterpret_cast<const frag8*>(bsrc + u * 1024);
                 f32x16 acc = f32x16{};
-                const char* dsrc = reinterpret_cast<const char*>(Wf) + (int64_t)dtile * TILE +
-                                   (lidx * DPW + pbase) * 1024 + 16 * lane;
-                const uint32_t ddst = ring_lds + dslot * TILE + (lidx * DPW + pbase) * 1024;
-                const bool dma = dtile >= 0 && loader && !AVR_PROBE_SKIP(1);
+                const char* dsrc =
+                    reinterpret_cast<const char*>(Wf) + (int64_t)dtile * TILE + wave * DPW * 1024 + 16 * lane;
+                const uint32_t ddst = ring_lds + dslot * TILE + wave * DPW * 1024;
+                const bool dma = dtile >= 0 && !AVR_PROBE_SKIP(1);
 #pragma unroll
                 for (int ks = 0; ks < KSM; ++ks) {
-                    acc = mfma16<E>(a[0][ks], bw[ks % D], acc);
-                    if (ks + D < KSM) bw[ks % D] = *reinterpret_cast<const frag8*>(bsrc + (ks + D) * 1024);
+                    acc = mfma16<E>(a[0][ks], bw[ks % RS], acc);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int q = 0; q < kHold; ++q)
+                        if (ks >= q) keep_live(bw[(ks - q) % RS]);
+                    if (ks + D < KSM) bw[(ks + D) % RS] = *reinterpret_cast<const frag8*>(bsrc + (ks + D) * 1024);
                     if (ks % DSTEP == 0 && dma) dma_row16(dsrc + (ks / DSTEP) * 1024, ddst + (ks / DSTEP) * 1024);
                 }
+                mfma_queue_wait();
+#pragma unroll
+                for (int u = 0; u < RS; ++u) keep_live(bw[u]);
                 return acc;
             };
             auto epi = [&](const f32x16& acc, int tau, int c) {
@@ -465,35 +422,6 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                 }
                 return z;
             };
-            // both chains of a 64-t tile (NC == 2) as one B stream; chain 0
-            // carries the DMA pieces; returns chain 1's accumulator, chain 0's
-            // epilogue sum in z0
-            auto chain2 = [&](int slot, int dtile, int dslot, int tau, float& z0) {
-                const char* b0 = ring + slot * TILE + 16 * lane;
-                constexpr int D = AVR_EXACT_D;
-                constexpr int DSTEP = KSM / PPC;
-                frag8 bw[D];
-#pragma unroll
-                for (int u = 0; u < D; ++u) bw[u] = *reinterpret_cast<const frag8*>(b0 + u * 1024);
-                const char* dsrc = reinterpret_cast<const char*>(Wf) + (int64_t)dtile * TILE + (lidx * DPW) * 1024 + 16 * lane;
-                const uint32_t ddst = ring_lds + dslot * TILE + (lidx * DPW) * 1024;
-                const bool dma = dtile >= 0 && loader && !AVR_PROBE_SKIP(1);
-                f32x16 acc = f32x16{};
-#pragma unroll
-                for (int g = 0; g < KSM; ++g) {
-                    acc = mfma16<E>(a[0][g], bw[g % D], acc);
-                    bw[g % D] = *reinterpret_cast<const frag8*>(b0 + (g + D) * 1024);  // g + D < 2 KSM
-                    if (g % DSTEP == 0 && dma) dma_row16(dsrc + (g / DSTEP) * 1024, ddst + (g / DSTEP) * 1024);
-                }
-                z0 = epi(acc, tau, 0);
-                f32x16 acc1 = f32x16{};
-#pragma unroll
-                for (int g = KSM; g < 2 * KSM; ++g) {
-                    acc1 = mfma16<E>(a[0][g - KSM], bw[g % D], acc1);
-                    if (g + D < 2 * KSM) bw[g % D] = *reinterpret_cast<const frag8*>(b0 + (g + D) * 1024);
-                }
-                return acc1;
-            };
             // a chain's per-lane sum, lower + upper lane half (rows 4 half +
             // ...; the same association in every lane), into the partials of
             // buffer `buf`
@@ -514,156 +442,36 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                     if (t < T) zc[t] = v;
                 }
             };
-            // the wave that sums (and stores) a tile's partials right after the
-            // barrier of iteration m: tile m by wave m % WAVES, or with the
-            // stagger tile m - 1 by one of the non-deferring waves
-            // (AVR_EXACT_STAGGER 1: waves WAVES/2.. defer; 2: waves 0 .. WAVES/2-1)
-            constexpr int kSumOff = AVR_EXACT_STAGGER == 2 ? WAVES / 2 : 0;
-            auto summer = [&](int m) {
-                if constexpr (AVR_EXACT_STAGGER) return m >= 1 ? kSumOff + (m - 1) % (WAVES / 2) : -1;
-                else return m % WAVES;
-            };
-            constexpr bool kStag = AVR_EXACT_STAGGER;
-            const bool defer = kStag && ((wave >= WAVES / 2) == (AVR_EXACT_STAGGER == 1));
-            f32x16 dacc = f32x16{};
-            bool dlive = false;  // a deferred last chain is pending
-            if constexpr (kFlags) {
-                // LDS counter ops by lane 0 (one per wave); polls read the
-                // word in every lane (a broadcast) and spin with s_sleep
-                auto lds_add = [&](int* p, int v) {
-                    if (lane == 0) __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                };
-                // (bounded: a protocol error ends the spin after ~30 ms with a
-                // wrong result rather than a hung launch)
-                auto poll_ge = [&](const int* p, int target) {
-                    for (int spin = 0; spin < (1 << 20); ++spin) {
-                        if (__builtin_amdgcn_readfirstlane(
-                                __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >= target)
-                            break;
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                };
-                // vector-memory operations this wave has issued (for counted
-                // vmcnt waits on one tile's pieces) and the count after the
-                // pieces of the tile in each slot
-                int nops = 0;
-                int mark[NB] = {0, 0, 0, 0};
-                for (int k = 0; k < NB - 1; ++k) mark[k] = 0;  // prologue tiles: landed
-                for (int tau = tb; tau < te; ++tau) {
-                    const int i = tau - tb;
-                    const int slot = i & 3, gen = i >> 2;
-                    AVR_PROBE_BEGIN(comp);
-                    // tile i + 3 goes into the slot tile i - 1 used: every wave
-                    // must be through tile i - 1 (its last arriver's release)
-                    const int dtile = tau + 3 < te ? tau + 3 : -1;
-                    const int dslot = (i + 3) & 3;
-                    if (dtile >= 0 && loader && i >= 1) poll_ge(fl_free + dslot, ((i - 1) >> 2) + 1);
-                    // tile i's pieces from every loader wave
-                    if (i >= 3) poll_ge(fl_full + slot, LW * (gen + 1));
-                    float zl = 0.0f;
-                    const int t0 = TT * tau;
-                    bool issued = false;
-                    if (t0 + 31 >= dstart[wave] && t0 < lim) {
-                        const f32x16 acc = chain(slot, 0, dtile, dslot, 0);
-                        issued = dtile >= 0;
-                        zl = epi(acc, tau, 0);
-                    }
-                    if (dtile >= 0 && !issued) issue_pieces(dtile, dslot, 0, DPW);
-                    if (dtile >= 0 && loader) {
-                        nops += DPW;
-                        mark[dslot] = nops;
-                    }
-                    AVR_PROBE_END(comp, 6);
-                    put(zl, slot, 0);
-                    AVR_PROBE_BEGIN(dma);
-                    // tile i + 2's pieces (issued during tile i - 1) landed:
-                    // published for the waves that reach it
-                    if (i >= 1 && tau + 2 < te && loader) {
-                        wait_vm(nops - mark[(i + 2) & 3]);
-                        lds_add(fl_full + ((i + 2) & 3), 1);
-                    }
-                    if (i == min(1, te - 1 - tb)) {
-                        load_dly(nx);
-                        ++nops;
-                        dly_issued = true;
-                    }
-                    AVR_PROBE_END(dma, 4);
-                    AVR_PROBE_BEGIN(bar);
-                    // through tile i: its B reads and the partial written
-                    __builtin_amdgcn_s_waitcnt(0xC07F);
-                    int old = 0;
-                    if (lane == 0)
-                        old = __hip_atomic_fetch_add(fl_done + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    old = __builtin_amdgcn_readfirstlane(old);
-                    AVR_PROBE_END(bar, 5);
-                    if (old == WAVES * gen + WAVES - 1) {
-                        // the last arrival: the partials in wave order, then the
-                        // slot is free for tile i + 4
-                        sum_tile(tau, slot);
-                        ++nops;
-                        __builtin_amdgcn_s_waitcnt(0xC07F);
-                        lds_add(fl_free + slot, 1);
-                    }
-                }
-                touch(nx);
-                touched = true;
-                // every wave through every tile (and every sum done) before the
-                // next item's prologue reuses the ring and resets the flags
-                __builtin_amdgcn_s_waitcnt(0xC07F);
-                __builtin_amdgcn_s_barrier();
-            } else {
-            uint32_t pfs = 0;  // sink of the row prefetch
+            // the wave that sums (and stores) tile i's partials right after
+            // the barrier of iteration i
+            auto summer = [&](int m) { return m % WAVES; };
             for (int tau = tb; tau < te; ++tau) {
                 const int i = tau - tb;
                 AVR_PROBE_BEGIN(comp);
-                if (kStag && defer) {
-                    // the previous tile's last chain: its epilogue now, beside
-                    // the partner wave's first chain of this tile
-                    if (i >= 1) put(dlive ? epi(dacc, tau - 1, NC - 1) : 0.0f, (i - 1) % kPartBufs, NC - 1);
-                    dlive = false;
-                }
                 // tile tau + NB - 1 into the slot tile tau - 1 left: inside the
                 // first live group's chain, else here
                 const int dtile = tau + NB - 1 < te ? tau + NB - 1 : -1;
                 const int dslot = (i + NB - 1) % NB;
-                int pdone = 0;  // pieces of dtile issued (in chain order)
+                bool issued = false;  // dtile's pieces issued
                 float zl[NC];
-                bool both = false;
-                if constexpr (AVR_EXACT_XCHAIN && NC == 2 && !AVR_EXACT_DMA_SPREAD && !kStag) {
-                    // both chains live: one B stream over the two
-                    both = __builtin_amdgcn_readfirstlane((int)(TT * tau + 31 >= dstart[wave] && TT * tau + 32 < lim));
-                    if (both) {
-                        const f32x16 acc1 = chain2(i % NB, dtile, dslot, tau, zl[0]);
-                        zl[1] = epi(acc1, tau, 1);
-                        pdone = DPW;
-                    }
-                }
 #pragma unroll
                 for (int c = 0; c < NC; ++c) {
                     // group c holds a live ray of the wave from the wave's first
                     // live t on (cnt is nondecreasing in t), nothing at or past lim
                     const int t0 = TT * tau + 32 * c;
-                    if (both) continue;
                     zl[c] = 0.0f;
                     if (t0 + 31 >= dstart[wave] && t0 < lim) {
-                        const bool carry = pdone < DPW;
-                        const f32x16 acc = chain(i % NB, c, carry ? dtile : -1, dslot, pdone);
-                        if (carry) pdone += PPC;
-                        if (kStag && defer && c == NC - 1) {
-                            dacc = acc;
-                            dlive = true;
-                        } else {
-                            zl[c] = epi(acc, tau, c);
-                        }
+                        const f32x16 acc = chain(i % NB, c, issued ? -1 : dtile, dslot);
+                        issued = true;
+                        zl[c] = epi(acc, tau, c);
                     }
                 }
-                if (dtile >= 0 && pdone < DPW) issue_pieces(dtile, dslot, pdone, DPW);
+                if (dtile >= 0 && !issued) issue(dtile, dslot);
                 AVR_PROBE_END(comp, 6);
 #pragma unroll
-                for (int c = 0; c < NC; ++c)
-                    if (!(kStag && defer && c == NC - 1)) put(zl[c], i % kPartBufs, c);
+                for (int c = 0; c < NC; ++c) put(zl[c], i % kPartBufs, c);
                 AVR_PROBE_BEGIN(dma);
-                if (tau + 1 < te && loader) {
+                if (tau + 1 < te) {
                     // this wave's pieces of tile tau+1 have landed.  Younger in
                     // vmcnt: the ring's later tiles and this wave's partial
                     // stores since tile tau+1 was issued (a wave stores after
@@ -679,15 +487,6 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                     load_dly(nx);
                     dly_issued = true;
                 }
-                if constexpr (AVR_EXACT_PREFETCH > 0 && ROWDMA) {  // whole 1 KiB rows (K == 512) only
-                    if (i == max(1, te - tb - AVR_EXACT_PREFETCH) && nx.item < nitems) {
-                        const int colp = nx.item % (int)ncol;
-                        const uint32_t* hn = reinterpret_cast<const uint32_t*>(
-                            h + (((int64_t)(colp / S) * R + nx.ray) * S + colp % S) * K);
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) pfs ^= hn[(2 * u + half) * 32];
-                    }
-                }
                 if (tau == te - 1) {  // before the last partial store: nothing young to wait for
                     touch(nx);
                     touched = true;
@@ -697,20 +496,7 @@ __global__ __launch_bounds__(64 * WAVES, 2) void head_exact_kernel(
                 __builtin_amdgcn_s_waitcnt(0xC07F);  // every LDS access of tile tau (and the partials) done
                 __builtin_amdgcn_s_barrier();
                 AVR_PROBE_END(bar, 5);
-                if (wave == summer(i)) {
-                    if constexpr (kStag) sum_tile(tau - 1, (i - 1) % kPartBufs);
-                    else sum_tile(tau, i % kPartBufs);
-                }
-            }
-            if constexpr (AVR_EXACT_PREFETCH > 0) asm volatile("" ::"v"(pfs));
-            }
-            if constexpr (kStag && !kFlags) {
-                // the last tile: its deferred chains, one more barrier, its sum
-                const int n = te - tb;
-                if (defer) put(dlive ? epi(dacc, te - 1, NC - 1) : 0.0f, (n - 1) % kPartBufs, NC - 1);
-                __builtin_amdgcn_s_waitcnt(0xC07F);
-                __builtin_amdgcn_s_barrier();
-                if (wave == kSumOff + (n - 1) % (WAVES / 2)) sum_tile(te - 1, (n - 1) % kPartBufs);
+                if (wave == summer(i)) sum_tile(tau, i % kPartBufs);
             }
             // zero outside the item's tiles (after the tiles: no wait above
             // includes these stores)
@@ -746,271 +532,6 @@ __global__ __launch_bounds__(256) void head_pack_exact_kernel(int T, int K, int 
         frag8 v = frag8{0u, 0u, 0u, 0u};
         if (t < T && k0 < K) v = *reinterpret_cast<const frag8*>(W + (int64_t)t * K + k0);
         Wf[i] = v;
-    }
-}
-
-// ---- AVR_EXACT_V2 (compile-time, off): one wave per SIMD and 64 rays per
-// wave as two 32-ray A tiles (256 registers), so that every B fragment read
-// from the ring feeds two MFMAs: half the ring reads per MFMA of the 8-wave
-// form, whose per-tile LDS traffic (eight waves reading the whole 64 KiB
-// tile, plus its DMA) is the suspected limiter.  With one
-// wave per SIMD nothing else fills the matrix pipe during an epilogue, so
-// each chain carries the previous chain's epilogue, one value per k-step,
-// between its MFMAs; a tile's partials are complete one barrier later
-// (three partial buffers).  K = 512 only (rows by LDS-DMA), 64-t tiles, a
-// two-tile ring, the next tile's DMA inside the tile's first chain.
-#ifndef AVR_EXACT_V2
-#define AVR_EXACT_V2 0
-#endif
-
-__host__ __device__ constexpr size_t xs2_lds_bytes(int T) {
-    return 2 * (size_t)65536 + 4 * (size_t)((T + 3) / 4 * 4) + 4 * 256 + 4 * 3 * 4 * 64 + 4 * 8 + 8;
-}
-
-template <typename E>
-__global__ __launch_bounds__(256, 1) void head_exact2_kernel(
-    avr_render_params pp, int B, int R, int K, const E* __restrict__ h, const frag8* __restrict__ Wf,
-    const int* __restrict__ perm, const float* __restrict__ ws, const int* __restrict__ cnt,
-    const int32_t* __restrict__ delay, float* __restrict__ zpart, int* __restrict__ queue, int nitems) {
-    constexpr int KSM = 32, WAVES = 4, NT = 256, RAYS = 256, RPW = 64, TT = 64, TILE = 65536, NBUF = 3;
-    constexpr int DPW = 2 * KSM / WAVES;  // W pieces (1 KiB) per wave and tile
-    extern __shared__ __attribute__((aligned(16))) char lds_x[];
-    const int T = pp.T, S = pp.n_samples;
-    const int Tp = (T + 3) & ~3;
-    char* ring = lds_x;                                                // [2][TILE]
-    int* cl = reinterpret_cast<int*>(lds_x + 2 * TILE);                // cnt of the column [Tp]
-    float* wl = reinterpret_cast<float*>(cl + Tp);                     // weights of the item's rays [RAYS]
-    float* zr = wl + RAYS;                                             // wave partials [NBUF][WAVES][TT]
-    int* dstart = reinterpret_cast<int*>(zr + NBUF * WAVES * TT);      // first live t per A tile [WAVES][2]
-    int* qnext = dstart + 2 * WAVES;                                   // claimed items [2]
-
-    const int64_t ncol = (int64_t)B * S;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t ring_lds = (uint32_t)(uintptr_t)ring;
-    const int qx = blockIdx.x & 7, gq = gridDim.x >> 3, ql = blockIdx.x >> 3;
-    int* qctr = queue + 32 * qx;
-    auto item_of = [&](int claim) { return qx + 8 * claim; };
-
-    constexpr int CLN = kExactMaxT[0] / NT;
-    struct Meta {
-        int item, nk, ray0, ray1, dly0, dly1;
-        int clv[CLN];
-        float wsv;
-    };
-    auto load_meta = [&](int item, Meta& m) {
-        const int tid = opaque_tid();
-        m.item = item;
-        const int it = min(item, nitems - 1);
-        const int64_t col = (int64_t)it % ncol;
-        const int blk = (int)((int64_t)it / ncol);
-        const int* cc = cnt + col * T;
-        m.nk = cc[T - 1 - (tid >> 12)];
-        const int pb = blk * RAYS + RPW * wave + (tid & 31);
-        m.ray0 = perm[col * R + min(pb, R - 1)];
-        m.ray1 = perm[col * R + min(pb + 32, R - 1)];
-#pragma unroll
-        for (int u = 0; u < CLN; ++u) m.clv[u] = cc[min(tid + NT * u, T - 1)];
-        m.wsv = ws[col * R + min(blk * RAYS + tid, R - 1)];
-    };
-    auto load_dly = [&](Meta& m) {
-        const int it = min(m.item, nitems - 1);
-        const int64_t col = (int64_t)it % ncol;
-        const int s = (int)(col % S), b = (int)(col / S);
-        m.dly0 = delay[((int64_t)b * R + m.ray0) * S + s];
-        m.dly1 = delay[((int64_t)b * R + m.ray1) * S + s];
-    };
-    auto touch = [&](Meta& m) {
-        asm volatile("" ::"v"(m.nk), "v"(m.ray0), "v"(m.ray1), "v"(m.dly0), "v"(m.dly1), "v"(m.wsv));
-#pragma unroll
-        for (int u = 0; u < CLN; ++u) asm volatile("" ::"v"(m.clv[u]));
-    };
-
-    Meta cur, nx;
-    int claim = 0;
-    int item = item_of(ql), nxt = item_of(gq + ql);
-    load_meta(item, cur);
-    load_dly(cur);
-    if (threadIdx.x == 0) qnext[1] = item_of(2 * gq + ql);
-    __syncthreads();
-    for (int iter = 0; item < nitems; ++iter) {
-        const int tid = opaque_tid();
-        const int lane = tid & 63, half = lane >> 5, j = lane & 31;
-        const int col = item % (int)ncol;
-        const int blk = item / (int)ncol;
-        const int s = col % S, b = col / S;
-        const int lim = tail_limit(pp, s);
-        float* zc = zpart + ((int64_t)blk * ncol + col) * T;
-        const int p0 = blk * RAYS;
-        const int pw = p0 + RPW * wave;
-        const int nk = __builtin_amdgcn_readfirstlane(cur.nk);
-        if (tid == 0) {
-            int zero = 0;
-            asm volatile("" : "+v"(zero));
-            claim = __hip_atomic_fetch_add(qctr + zero, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        bool dly_issued = false, touched = false, published = false;
-        if (p0 >= nk || lim <= 0) {
-            load_meta(nxt, nx);
-            for (int t = tid; t < T; t += NT) zc[t] = 0.0f;
-            load_dly(nx);
-            dly_issued = true;
-        } else {
-            // ---- prologue: the wave's 64 rows, two A tiles, by LDS-DMA
-            frag8 a[2][KSM];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-#pragma unroll
-                for (int ks = 0; ks < KSM; ++ks) a[q][ks] = frag8{0u, 0u, 0u, 0u};
-                const E* hrow = h + (((int64_t)b * R + (q ? cur.ray1 : cur.ray0)) * S + s) * K;
-                stat_load_rows512(reinterpret_cast<frag8_t(&)[32]>(a[q]), reinterpret_cast<const uint16_t*>(hrow),
-                                  ring + wave * 16384);
-            }
-#pragma unroll
-            for (int u = 0; u < CLN; ++u) {
-                const int t = tid + NT * u;
-                if (t < T) cl[t] = cur.clv[u];
-            }
-            wl[tid] = p0 + tid < nk ? cur.wsv : 0.0f;
-            if (lane == 0) {
-                dstart[2 * wave] = pw < nk ? cur.dly0 : 1 << 30;
-                dstart[2 * wave + 1] = pw + 32 < nk ? cur.dly1 : 1 << 30;
-            }
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-            __builtin_amdgcn_s_barrier();
-            const int tb = dstart[0] / TT;
-            const int te = (lim + TT - 1) / TT;
-            const int d0 = __builtin_amdgcn_readfirstlane(dstart[2 * wave]);
-            const int d1 = __builtin_amdgcn_readfirstlane(dstart[2 * wave + 1]);
-            // tile tb into slot 0, this wave's pieces
-            if (tb < te) {
-                const char* src = reinterpret_cast<const char*>(Wf) + (int64_t)tb * TILE + wave * DPW * 1024 + 16 * lane;
-                const uint32_t dst = ring_lds + wave * DPW * 1024;
-                for (int d = 0; d < DPW; ++d) dma_row16(src + d * 1024, dst + d * 1024);
-            }
-            load_meta(nxt, nx);
-            AVR_VMCNT(CLN + 4);  // the first tile (and the older claim) landed; the metadata may fly
-            if (tid == 0) {
-                qnext[iter & 1] = item_of(3 * gq + claim);
-                published = true;
-            }
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-            __builtin_amdgcn_s_barrier();
-
-            const float* wq = wl + RPW * wave + 4 * half;
-            const int pos0 = pw + 4 * half;
-            // one chain: the wave's NM (0, 1 or 2) A tiles against 32-t group c
-            // of the tile in `slot` (B read once for both), the DMA pieces of
-            // tile dtile (if >= 0) one every two k-steps, and the epilogue of
-            // the previous chain's accumulators (q0, q1 at t0 = pt0; none if
-            // pt0 < 0), one value per k-step: returns its per-lane sum
-            auto chain = [&](auto NM, int slot, int c, int dtile, int dslot, const f32x16& q0, const f32x16& q1,
-                             int pt0, f32x16& n0, f32x16& n1) {
-                constexpr int nm = decltype(NM)::value;
-                constexpr int D = 4;
-                const char* bsrc = ring + slot * TILE + c * xs_tile_bytes(KSM) + 16 * lane;
-                const int pt = pt0 + j;
-                const int ct = (pt0 >= 0 && pt < lim) ? cl[min(pt, T - 1)] : 0;
-                const char* dsrc = reinterpret_cast<const char*>(Wf) + (int64_t)dtile * TILE + wave * DPW * 1024 +
-                                   16 * lane;
-                const uint32_t ddst = ring_lds + dslot * TILE + wave * DPW * 1024;
-                frag8 bw[D];
-                if constexpr (nm > 0) {
-#pragma unroll
-                    for (int u = 0; u < D; ++u) bw[u] = *reinterpret_cast<const frag8*>(bsrc + u * 1024);
-                }
-                n0 = f32x16{};
-                n1 = f32x16{};
-                float z = 0.0f;
-                float4 w4 = float4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int ks = 0; ks < KSM; ++ks) {
-                    if constexpr (nm > 0) n0 = mfma16<E>(a[0][ks], bw[ks % D], n0);
-                    if constexpr (nm > 1) n1 = mfma16<E>(a[1][ks], bw[ks % D], n1);
-                    if constexpr (nm > 0)
-                        if (ks + D < KSM) bw[ks % D] = *reinterpret_cast<const frag8*>(bsrc + (ks + D) * 1024);
-                    if (ks % 2 == 0 && dtile >= 0) dma_row16(dsrc + (ks / 2) * 1024, ddst + (ks / 2) * 1024);
-                    // value r of A tile rt: ray pos0 + 32 rt + 8 (r >> 2) + (r & 3)
-                    const int rt = ks >> 4, r = ks & 15, e = r & 3;
-                    if (e == 0) w4 = *reinterpret_cast<const float4*>(wq + 32 * rt + 8 * (r >> 2));
-                    const float wv = e == 0 ? w4.x : (e == 1 ? w4.y : (e == 2 ? w4.z : w4.w));
-                    const float v = round16<E>(rt ? q1[r] : q0[r]);
-                    z = fmaf(wv, (pos0 + 32 * rt + 8 * (r >> 2) + e < ct) ? v : 0.0f, z);
-                }
-                return z;
-            };
-            auto put = [&](float zlc, int buf, int c) {
-                const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(zlc), __float_as_uint(zlc), false,
-                                                                false);
-                const float v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-                if (half == 0) zr[buf * (WAVES * TT) + wave * TT + 32 * c + j] = v;
-            };
-            auto sum_tile = [&](int tau, int buf) {
-                const float* zz = zr + buf * (WAVES * TT) + lane;
-                float v = zz[0];
-#pragma unroll
-                for (int w = 1; w < WAVES; ++w) v += zz[TT * w];
-                const int t = TT * tau + lane;
-                if (t < T) zc[t] = v;
-            };
-            f32x16 q0 = f32x16{}, q1 = f32x16{};
-            int qt = -1, qbuf = 0;  // the pending chain's t0 and partial buffer
-            for (int tau = tb; tau < te; ++tau) {
-                const int i = tau - tb;
-                const int dtile = tau + 1 < te ? tau + 1 : -1;
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    const int t0 = TT * tau + 32 * c;
-                    const bool live0 = t0 + 31 >= d0 && t0 < lim, live1 = t0 + 31 >= d1 && t0 < lim;
-                    const int dt = c == 0 ? dtile : -1;
-                    f32x16 n0, n1;
-                    float zp;
-                    if (live1)
-                        zp = chain(std::integral_constant<int, 2>{}, i & 1, c, dt, (i + 1) & 1, q0, q1, qt, n0, n1);
-                    else if (live0)
-                        zp = chain(std::integral_constant<int, 1>{}, i & 1, c, dt, (i + 1) & 1, q0, q1, qt, n0, n1);
-                    else
-                        zp = chain(std::integral_constant<int, 0>{}, i & 1, c, dt, (i + 1) & 1, q0, q1, qt, n0, n1);
-                    if (qt >= 0) put(zp, qbuf, c ^ 1);
-                    q0 = n0;
-                    q1 = n1;
-                    qt = t0;
-                    qbuf = i % NBUF;
-                }
-                if (dtile >= 0) AVR_VMCNT(0);  // this wave's pieces of the next tile landed
-                if (i == min(1, te - 1 - tb)) {
-                    load_dly(nx);
-                    dly_issued = true;
-                }
-                if (tau == te - 1) {
-                    touch(nx);
-                    touched = true;
-                }
-                __builtin_amdgcn_s_waitcnt(0xC07F);
-                __builtin_amdgcn_s_barrier();
-                // tile i - 1's partials are complete (its second chain's
-                // epilogue ran in tile i's first chain)
-                if (i >= 1 && wave == (i - 1) % WAVES) sum_tile(tau - 1, (i - 1) % NBUF);
-            }
-            if (te > tb) {
-                // the last chain's epilogue, then the last tile's sum
-                const int n = te - tb;
-                f32x16 n0, n1;
-                const float zp = chain(std::integral_constant<int, 0>{}, 0, 0, -1, 0, q0, q1, qt, n0, n1);
-                put(zp, qbuf, 1);
-                __builtin_amdgcn_s_waitcnt(0xC07F);
-                __builtin_amdgcn_s_barrier();
-                if (wave == (n - 1) % WAVES) sum_tile(te - 1, (n - 1) % NBUF);
-            }
-            for (int t = tid; t < T; t += NT)
-                if (t < TT * tb || t >= TT * te) zc[t] = 0.0f;
-        }
-        if (!dly_issued) load_dly(nx);
-        if (!touched) touch(nx);
-        if (tid == 0 && !published) qnext[iter & 1] = item_of(3 * gq + claim);
-        if (p0 >= nk || lim <= 0) __syncthreads();
-        item = nxt;
-        nxt = qnext[(iter + 1) & 1];
-        cur = nx;
     }
 }
 
@@ -1056,8 +577,6 @@ size_t exact_lds(int R, int T, int K) {
     const int KSM = exact_ksm(K);
     const ExactShape sh = exact_shape(R, T, K);
     if (sh.rays == 128) return xs_lds_bytes(KSM, T, 4, 128, 2, 1);
-    if (AVR_EXACT_V2 != 0 && K == 512) return xs2_lds_bytes(T);
-    if ((AVR_EXACT_FLAGS != 0 || AVR_EXACT_NC1 != 0) && K == 512) return xs_lds_bytes(KSM, T, 8, 256, 4, 1);
     if (sh.tt64) return xs_lds_bytes(KSM, T, 8, 256, 2, 2);
     return xs_lds_bytes(KSM, T, 8, 256, 4, 1);
 }
@@ -1074,20 +593,6 @@ template <typename Kern>
 void allow_lds(Kern k, size_t lds) {
     if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-}
-
-// CUs of the current device (cached per device)
-int device_cus() {
-    static int cus[64] = {};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (dev < 0 || dev >= 64) return 256;
-    if (!cus[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
-        cus[dev] = n;
-    }
-    return cus[dev];
 }
 
 }  // namespace
@@ -1141,9 +646,6 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
     // config-2 fp16 fused render (tools/ab_shapes.py, 5 interleaved rounds);
     // the 4-wave items (two workgroups per CU) lose with it (252 vs 244)
     int prio = small ? 0 : 1;
-#ifdef AVR_EXACT_NOPRIO
-    prio = 0;
-#endif
     if (const char* pe = AVR_PROBE_ENV("AVR_EXACT_PRIO_PROBE")) prio = atoi(pe);
     auto run = [&](auto e_tag) {
         using E = decltype(e_tag);
@@ -1168,19 +670,6 @@ extern "C" int avr_head_fwd_exact(const avr_render_params* p, int32_t B, int32_t
             else if (KSM == 16) go(head_exact_kernel<E, 16, 4, 128, 2, 1, false>, 16, 4, 128, 2, 1, h);
             else if (rowdma) go(head_exact_kernel<E, 32, 4, 128, 2, 1, true>, 32, 4, 128, 2, 1, h);
             else go(head_exact_kernel<E, 32, 4, 128, 2, 1, false>, 32, 4, 128, 2, 1, h);
-#if AVR_EXACT_V2
-        } else if (rowdma) {
-            auto kern = head_exact2_kernel<E>;
-            const size_t lds = xs2_lds_bytes(T);
-            allow_lds(kern, lds);
-            const int64_t gq = std::min<int64_t>((int64_t)device_cus() / 8, (items + 7) / 8);
-            const int grid = 8 * (int)std::max<int64_t>(gq, 1);
-            (void)hipMemsetAsync(queue, 0, kExactQueueInts * sizeof(int32_t), st);
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, *p, (int)B, R, (int)K, (const E*)h,
-                               (const frag8*)Wf, perm, ws, cnt, delay, zpart, (int*)queue, (int)items);
-#endif
-        } else if ((AVR_EXACT_FLAGS != 0 || AVR_EXACT_NC1 != 0) && rowdma) {
-            go(head_exact_kernel<E, 32, 8, 256, 4, 1, true>, 32, 8, 256, 4, 1, h);
         } else if (tt64 && rowdma) {
             go(head_exact_kernel<E, 32, 8, 256, 2, 2, true>, 32, 8, 256, 2, 2, h);
         } else {

@@ -41,26 +41,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint32_t frag8 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-// AVR_L512_PIPE 1: each k-step's fragments read during the previous k-step's
-// MFMAs, the order pinned (measured slower).
-#ifndef AVR_L512_PIPE
-#define AVR_L512_PIPE 0
-#endif
-// AVR_L512_DBG (timing probes, wrong results): bit 0 no DMA in the loop,
-// bit 1 no barrier, bit 2 no stores (skipped at run time).
-#ifndef AVR_L512_DBG
-#define AVR_L512_DBG 0
-#endif
-
-// AVR_L512_KC: k per chunk, 64 (two LDS slots, one chunk in flight) or 32
-// (four slots, three in flight: measured slower, more barriers per tile)
-#ifndef AVR_L512_KC
-#define AVR_L512_KC 64
-#endif
 constexpr int kLK = 512;                  // K = N = 512
-constexpr int kLKC = AVR_L512_KC;         // k per chunk
+constexpr int kLKC = 64;                  // k per chunk
 constexpr int kLChunks = kLK / kLKC;
-constexpr int kLSlots = kLKC == 64 ? 2 : 4;  // 32 / 64 KiB slots in 128 KiB
+constexpr int kLSlots = 2;                // two 64 KiB slots: one chunk in flight
 constexpr int kLAhead = kLSlots - 1;      // chunks in flight
 constexpr int kLKS = kLKC / 16;           // k-steps per chunk
 constexpr int kLPieces = kLKC / 8;        // 16-byte pieces of a row's chunk
@@ -92,7 +76,7 @@ __device__ __forceinline__ f32x16 mma(frag8 a, frag8 b, f32x16 c) {
 // the compiler neither counts it nor treats it as an LDS write; completion is
 // waited for with explicit, counted vmcnt before the chunk's barrier)
 __device__ __forceinline__ void ldma16(const void* g, uint32_t lds) {
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(g) : "memory");
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(g) : "memory", "m0");
 }
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -164,7 +148,6 @@ __global__ __launch_bounds__(512, 1) void linear512_relu_kernel(int64_t M, const
     // chunk's row segment each; lane l: row kLRowsPerOp q + l / kLPieces,
     // the piece that lands in slot l % kLPieces, lswz)
     auto issue_chunk = [&](int t, int c, int slot) {
-        if (AVR_L512_DBG & 1) return;
         int rt, nh;
         tile_rc(t, rt, nh);
         const uint32_t base = lds0 + slot * kLSlot;
@@ -221,45 +204,39 @@ __global__ __launch_bounds__(512, 1) void linear512_relu_kernel(int64_t M, const
                     xfr[q] = *reinterpret_cast<const frag8*>(sb + r * (2 * kLKC) + lswz(r, pc) * 16);
                 }
             };
-            if constexpr (AVR_L512_PIPE) {
-                frag8 wfr[2][2], xfr[2][4];
-                read_frags(0, wfr[0], xfr[0]);
+            // k-step s + 1's fragments read during k-step s's MFMAs, in a
+            // ring of three: the reads of k-step s + 1 go into the registers
+            // of k-step s - 2, whose MFMAs issued a whole k-step earlier (the
+            // program order fixed by sched_barrier; the fragments of k-steps
+            // s - 1 and s used once more at the end of k-step s), so no read
+            // lands on a B register an MFMA may still wait to read (common.h)
+            frag8 wfr[3][2], xfr[3][4];
+            read_frags(0, wfr[0], xfr[0]);
 #pragma unroll
-                for (int s = 0; s < kLKS; ++s) {
-                    const int b = s & 1;
-                    if (s + 1 < kLKS) read_frags(s + 1, wfr[b ^ 1], xfr[b ^ 1]);
+            for (int s = 0; s < kLKS; ++s) {
+                const int b = s % 3;
+                if (s + 1 < kLKS) read_frags(s + 1, wfr[(s + 1) % 3], xfr[(s + 1) % 3]);
 #pragma unroll
-                    for (int a = 0; a < 2; ++a)
+                for (int a = 0; a < 2; ++a)
 #pragma unroll
-                        for (int q = 0; q < 4; ++q) acc[a][q] = mma<E>(wfr[b][a], xfr[b][q], acc[a][q]);
-                    // 8 MFMAs with the next k-step's 6 reads between them
-                    if (s + 1 < kLKS) {
+                    for (int q = 0; q < 4; ++q) acc[a][q] = mma<E>(wfr[b][a], xfr[b][q], acc[a][q]);
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                        for (int u = 0; u < 6; ++u) {
-                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                        }
-                        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int s = 0; s < kLKS; ++s) {
-                    frag8 wfr[2], xfr[4];
-                    read_frags(s, wfr, xfr);
-#pragma unroll
-                    for (int a = 0; a < 2; ++a)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) acc[a][q] = mma<E>(wfr[a], xfr[q], acc[a][q]);
+                for (int q = 0; q < 4; ++q) {
+                    keep_live(xfr[b][q]);
+                    if (s >= 1) keep_live(xfr[(s + 2) % 3][q]);
                 }
             }
+            mfma_queue_wait();
+#pragma unroll
+            for (int q = 0; q < 4; ++q) keep_live(xfr[(kLKS - 1) % 3][q]);
             // (scheduling fences: hipcc would otherwise sink the chunk's MFMAs
             // below the wait and the barrier)
             __builtin_amdgcn_sched_barrier(0);
             // chunk g + 1 landed: younger are the chunks issued after it
             // (kLAhead - 1 of them while the stream runs; none at its end)
             wait_vm_l(issued ? (kLAhead - 1) * kLOpsPerChunk : 0);
-            if (!(AVR_L512_DBG & 2)) lds_barrier();
+            lds_barrier();
             __builtin_amdgcn_sched_barrier(0);
         }
 
@@ -310,8 +287,7 @@ __global__ __launch_bounds__(512, 1) void linear512_relu_kernel(int64_t M, const
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] = keep_where_positive<E>(v[e], mk[u][e]);
                 }
-                if (!(AVR_L512_DBG & 4) || M < 0)
-                    __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_amdgcn_raw_buffer_store_b128(
                         v, yres, ((32 * q + row) * kLK + kLTileCols * nh + 64 * wc + 8 * ch) * 2, 0, 0);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -345,9 +321,11 @@ __global__ __launch_bounds__(256) void linear512_pack_kernel(const uint16_t* __r
 
 }  // namespace
 
+#ifdef AVR_SHAPE_PROBES
 extern "C" int avr_linear512_pack_w(const void* W, int32_t dtype, void* Wf, void* stream) {
     return avr_linear512_pack_w2(W, dtype, 0, Wf, stream);
 }
+#endif
 
 extern "C" int avr_linear512_pack_w2(const void* W, int32_t dtype, int32_t transpose, void* Wf, void* stream) {
     AVR_REQUIRE(W && Wf && (transpose == 0 || transpose == 1), "avr_linear512_pack_w: bad args");
@@ -372,9 +350,7 @@ int linear512_launch(int64_t M, const void* x, const void* Wf, int32_t dtype, co
     const int64_t ntiles = 16 * ((nrt + 7) / 8);
     AVR_REQUIRE(ntiles < (1ll << 31) && M * kLK * 2 < (1ll << 47), "avr_linear512_relu_fwd: too many rows");
     AVR_REQUIRE(128 * kLK * 2 < (1ll << 31), "avr_linear512_relu_fwd: tile too large");
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int cus = device_cus();
     // persistent: one workgroup per CU (160 KiB of LDS), a multiple of 16 so
     // that block b's tiles and block b + 8's are a row tile's two halves
     const int64_t g = std::min<int64_t>(ntiles, std::max(16, cus / 16 * 16));
@@ -386,18 +362,32 @@ int linear512_launch(int64_t M, const void* x, const void* Wf, int32_t dtype, co
         hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(512), kLLds, st, M, (const E*)x, (const frag8*)Wf, (E*)y,
                            (int)ntiles, (int)nrt, (const E*)mask);
     };
+#ifdef AVR_SHAPE_PROBES
+    if (!mask) {
+        if (dtype == AVR_DTYPE_F16)
+            go(__half{}, std::false_type{});
+        else
+            go(__hip_bfloat16{}, std::false_type{});
+        return check_launch("avr_linear512_relu_fwd");
+    }
+#endif
+    AVR_REQUIRE(mask != nullptr, "avr_linear512: mask required");
     if (dtype == AVR_DTYPE_F16)
-        mask ? go(__half{}, std::true_type{}) : go(__half{}, std::false_type{});
+        go(__half{}, std::true_type{});
     else
-        mask ? go(__hip_bfloat16{}, std::true_type{}) : go(__hip_bfloat16{}, std::false_type{});
-    return check_launch(mask ? "avr_linear512_mask_fwd" : "avr_linear512_relu_fwd");
+        go(__hip_bfloat16{}, std::true_type{});
+    return check_launch("avr_linear512_mask_fwd");
 }
 }  // namespace
 
+#ifdef AVR_SHAPE_PROBES
+// the inference layer relu(x W^T) (not faster than hipBLASLt's tuned
+// solution): shapes build only (tools/bench_linear512.py)
 extern "C" int avr_linear512_relu_fwd(int64_t M, const void* x, const void* Wf, int32_t dtype, void* y,
                                       void* stream) {
     return linear512_launch(M, x, Wf, dtype, nullptr, y, stream);
 }
+#endif
 
 extern "C" int avr_linear512_mask_fwd(int64_t M, const void* x, const void* Wf, int32_t dtype, const void* mask,
                                       void* y, void* stream) {

@@ -579,9 +579,7 @@ extern "C" int avr_narrow_mm(int64_t N, int32_t R, int32_t C, const void* X, con
                 "avr_narrow_mm: X, Bt 16-byte and Y, mask 8-byte aligned");
     const int nct = (C + 31) / 32;
     const int64_t ntiles = (N + kNarrowRows - 1) / kNarrowRows;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int cus = device_cus();
     const int64_t grid = std::min<int64_t>(ntiles, 2 * (int64_t)cus);
     hipStream_t st = as_stream(stream);
     // the staged form where Bt and the X tile fit two workgroups per CU

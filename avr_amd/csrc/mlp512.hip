@@ -69,7 +69,7 @@ namespace {
 // 32-bit lane offset: one VGPR for every piece)
 __device__ __forceinline__ void mlp_dma16(const void* sbase, uint32_t voff, uint32_t lds) {
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(lds), "v"(voff), "s"(sbase)
-                 : "memory");
+                 : "memory", "m0");
 }
 
 // workgroup barrier that waits for the LDS traffic only: the W staging
@@ -369,9 +369,7 @@ extern "C" int avr_mlp512x2_fwd(int64_t M, const void* x, const void* Wf, int32_
                 "avr_mlp512x2_fwd: x, Wf and y must be 16-byte aligned");
     const int64_t items = (M + kMRows - 1) / kMRows;
     AVR_REQUIRE(items < (1ll << 31) && M < (1ll << 40), "avr_mlp512x2_fwd: too many rows");
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int cus = device_cus();
     const int grid = (int)std::min<int64_t>(items, std::max(cus, 1));
     const size_t lds = 2 * (size_t)kMPair + (AVR_MLP_TSTORE ? 4 * 4096 : 0);
     hipStream_t st = as_stream(stream);

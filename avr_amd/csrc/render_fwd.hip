@@ -584,7 +584,8 @@ __global__ __launch_bounds__(kDftThreads) void dft_phase_fwd_kernel(
 #pragma unroll 8
         for (int kk = 0; kk < kKc; kk += 2) {
             const float a = As[lane & 31][kk + half];
-            const float2 c = tw[idx];
+            float2 c = tw[idx];
+            asm volatile("" : "+v"(c.x), "+v"(c.y));
             acc_re = __builtin_amdgcn_mfma_f32_32x32x2f32(a, c.x, acc_re, 0, 0, 0);
             acc_im = __builtin_amdgcn_mfma_f32_32x32x2f32(a, c.y, acc_im, 0, 0, 0);
             idx += inc;

@@ -258,6 +258,19 @@ struct Stager {
     }
 };
 
+// The layer's B operands stay in their registers until every MFMA of the
+// layer has issued and the queue wait has passed (common.h): the next
+// layer's fragments, weight reads and accumulators are not allocated onto
+// them while one of the layer's MFMAs may still wait to read them.
+template <int NT, int KS>
+__device__ __forceinline__ void hold_operands(const frag8 (&x)[NT][KS]) {
+    mfma_queue_wait();
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) keep_live(x[nt][ks]);
+}
+
 // acc[nt][ot] = W X^T for one layer: KS k-steps of input fragments, OT output
 // tiles, CO tiles per LDS chunk.
 template <typename E, int NT, int KS, int OT, int CO, class ST>
@@ -296,6 +309,7 @@ __device__ __forceinline__ void dense(ST& st, int lane,
         }
         st.finish_chunk();
     }
+    hold_operands(x);
 }
 
 // one accumulator tile -> 8 dwords of E: dword q holds registers 2q, 2q+1

@@ -21,13 +21,13 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 
 import numpy as np
 import torch
 import torch.nn as nn
 
 from . import _lib
+from .options import resolve
 from .wcache import cast_weight
 from ._lib import DTYPE_F16, DTYPE_F32
 
@@ -82,17 +82,17 @@ class _HashGridFn(torch.autograd.Function):
             g = g.float()
         st = torch.cuda.current_stream(x.device).cuda_stream
         N = x.size(0)
-        if os.environ.get("AVR_HASHGRID_BWD", "partitioned") == "atomic":
+        mode = enc.options.hashgrid_bwd
+        if mode == "atomic":
             gp = torch.zeros(enc.n_params, dtype=torch.float32, device=x.device)
             _lib.call("avr_hashgrid_bwd", N, enc.n_levels, x.data_ptr(), g.data_ptr(),
                       _code(g.dtype), enc._off.ctypes.data, enc._scale.ctypes.data,
                       enc._res.ctypes.data, gp.data_ptr(), st)
             return None, gp, None, None
         # partitioned (no global atomics), written rather than added: no
-        # clearing pass over the table (AVR_HASHGRID_BWD=partitioned_add: the
-        # += form into a cleared table, for A/B); workspace from the caching
-        # allocator
-        add = os.environ.get("AVR_HASHGRID_BWD") == "partitioned_add"
+        # clearing pass over the table ("partitioned_add": the += form into
+        # a cleared table, for A/B); workspace from the caching allocator
+        add = mode == "partitioned_add"
         gp = (torch.zeros if add else torch.empty)(enc.n_params, dtype=torch.float32, device=x.device)
         nbytes = ctypes.c_int64()
         _lib.call("avr_hashgrid_bwd_workspace", N, enc.n_levels, enc._off.ctypes.data, ctypes.byref(nbytes))
@@ -105,10 +105,12 @@ class _HashGridFn(torch.autograd.Function):
 
 
 class HashGridEncoding(nn.Module):
-    """tcnn.Encoding(n_input_dims=3, encoding_config, dtype) replacement."""
+    """tcnn.Encoding(n_input_dims=3, encoding_config, dtype) replacement;
+    `options` (avr_amd.KernelOptions) selects the backward's form."""
 
-    def __init__(self, n_input_dims, encoding_config, dtype=None, seed=None):
+    def __init__(self, n_input_dims, encoding_config, dtype=None, seed=None, options=None):
         super().__init__()
+        self.options = resolve(options)
         cfg = dict(encoding_config)
         if cfg.get("otype", "HashGrid") not in ("HashGrid", "Grid"):
             raise ValueError(f"unsupported encoding {cfg.get('otype')}")

@@ -15,19 +15,18 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+import os
+
 from . import sigma as _sigma
 from .concat import grouped_concat
 from .encoding import HashGridEncoding
+from .options import DEFAULT, KernelOptions, resolve
 from .wcache import cache_lookup, cache_store, capturing, cast_weight
 
-
-import os
-
 _WGRAD_ROWS = 4096  # rows per split of the weight-gradient GEMM
-# split only the large weights: every distinct batched-GEMM shape in a step
-# costs ~1 ms of host time in hipBLASLt's solution lookup once more than a
-# few alternate (tools/mm_probe.py --interleave)
-_WGRAD_MIN = int(os.environ.get("AVR_WGRAD_MIN", str(512 * 512)))
+# split only the large weights (KernelOptions.wgrad_min): every distinct
+# batched-GEMM shape in a step costs ~1 ms of host time in hipBLASLt's
+# solution lookup once more than a few alternate (tools/mm_probe.py --interleave)
 
 
 def _wgrad_hip(gy, x):
@@ -55,7 +54,7 @@ def _hip_wgrad_ok(gy, x):
             and gy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
 
 
-def _wgrad(gy, x):
+def _wgrad(gy, x, opts=DEFAULT):
     """dW = gy^T x for gy [N, out], x [N, in] with N >> out, in.
 
     A single GEMM with a K dimension of N = B*R*S (1e5..1e6) and a 512x512
@@ -76,7 +75,7 @@ def _wgrad(gy, x):
             return _wgrad_hip(gp, x)[:M].contiguous()
     N = gy.size(0)
     k = N // _WGRAD_ROWS
-    if k < 2 or gy.size(1) * x.size(1) < _WGRAD_MIN:
+    if k < 2 or gy.size(1) * x.size(1) < opts.wgrad_min:
         return (gy.t() @ x).float()
     m = k * _WGRAD_ROWS
     a = gy[:m].view(k, _WGRAD_ROWS, -1).transpose(1, 2)
@@ -93,10 +92,11 @@ class _Linear(torch.autograd.Function):
     the weight gradient uses the split-K GEMM above and is returned in fp32."""
 
     @staticmethod
-    def forward(ctx, x, w_master, dtype, cache=False):
+    def forward(ctx, x, w_master, dtype, cache=False, opts=DEFAULT):
         w = cast_weight(w_master, dtype, cache)
         ctx.save_for_backward(x, w)
-        return _mm_dgrad(x, w.t())  # (a g @ W-shaped GEMM: the tuned file's "NN" entries)
+        ctx.opts = opts
+        return _mm_dgrad(x, w.t(), opts)  # (a g @ W-shaped GEMM: the tuned file's "NN" entries)
 
     @staticmethod
     def backward(ctx, gy):
@@ -107,9 +107,9 @@ class _Linear(torch.autograd.Function):
             # one output (sigma decoder's last layer): the K = 1 GEMM is an
             # outer product; the broadcast multiply rounds the same exact
             # fp32 products once, at write speed (hipBLASLt's K=1 tile: 2 TB/s)
-            gx = gy * w if w.size(0) == 1 else _mm_dgrad(gy, w)
-        gw = _wgrad(gy, x) if ctx.needs_input_grad[1] else None
-        return gx, gw, None, None
+            gx = gy * w if w.size(0) == 1 else _mm_dgrad(gy, w, ctx.opts)
+        gw = _wgrad(gy, x, ctx.opts) if ctx.needs_input_grad[1] else None
+        return gx, gw, None, None, None
 
 
 class _LinearOut1(torch.autograd.Function):
@@ -157,12 +157,9 @@ class _LinearOut1(torch.autograd.Function):
         return (gx if ctx.needs_input_grad[0] else None), (gw if ctx.needs_input_grad[1] else None), None, None
 
 
-_OUT1 = os.environ.get("AVR_OUT1", "1") != "0"
-
-
-def _out1_ok(h, w_master, dtype):
+def _out1_ok(h, w_master, dtype, opts=DEFAULT):
     K = h.size(-1)
-    return (_OUT1 and h.is_cuda and torch.is_grad_enabled() and dtype in (torch.float16, torch.bfloat16)
+    return (opts.out1 and h.is_cuda and torch.is_grad_enabled() and dtype in (torch.float16, torch.bfloat16)
             and w_master.size(0) == 1 and h.dim() == 2 and 8 <= K <= 512 and K & (K - 1) == 0)
 
 
@@ -178,82 +175,6 @@ def _zero_bias(n, dtype, device):
     return z
 
 
-# Two consecutive width-512 hidden layers at inference in ONE launch
-# (csrc/mlp512.hip: the intermediate activation stays on chip, x read and y
-# written once).  AVR_MLP512X2=0 keeps the per-layer GEMMs.
-_MLP512X2 = os.environ.get("AVR_MLP512X2", "0") == "1"
-
-
-def _mlp512x2_ok(x, lin1, lin2, dtype):
-    return (_MLP512X2 and x.is_cuda and not torch.is_grad_enabled() and dtype in (torch.float16, torch.bfloat16)
-            and x.dim() == 2 and x.size(1) == 512 and tuple(lin1.weight.shape) == (512, 512)
-            and tuple(lin2.weight.shape) == (512, 512) and x.size(0) >= 1)
-
-
-def _mlp512x2(x, w1_master, w2_master, dtype):
-    """relu(relu(x W1^T) W2^T) for x [M, 512] on csrc/mlp512.hip.  The packed
-    weights are cached on W1's master weight, keyed by both weights' storage
-    and versions (bypassed while a HIP graph is captured, wcache.capturing)."""
-    import ctypes
-
-    from . import _lib
-
-    x = x.to(dtype).contiguous()
-    code = _lib.DTYPE_F16 if dtype == torch.float16 else _lib.DTYPE_BF16
-    st = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
-    key = (w1_master.data_ptr(), w1_master._version, w2_master.data_ptr(), w2_master._version, code)
-    use_cache = not capturing()
-    wf = cache_lookup(w1_master, "_avr_mlp512x2", key) if use_cache else None
-    if wf is None:
-        w1 = cast_weight(w1_master, dtype, use_cache).contiguous()
-        w2 = cast_weight(w2_master, dtype, use_cache).contiguous()
-        wf = torch.empty(2, 512, 512, dtype=dtype, device=x.device)
-        _lib.call("avr_mlp512x2_pack_w", ctypes.c_void_p(w1.data_ptr()), ctypes.c_void_p(w2.data_ptr()), code,
-                  ctypes.c_void_p(wf.data_ptr()), st)
-        if use_cache:
-            cache_store(w1_master, "_avr_mlp512x2", key, wf)
-    y = torch.empty_like(x)
-    _lib.call("avr_mlp512x2_fwd", x.size(0), ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(wf.data_ptr()), code,
-              ctypes.c_void_p(y.data_ptr()), st)
-    return y
-
-
-# One width-512 layer at inference on the hand-written GEMM (csrc/linear512.hip)
-# instead of hipBLASLt (AVR_LINEAR512=1).
-_LINEAR512 = os.environ.get("AVR_LINEAR512", "0") == "1"
-
-
-def _linear512_ok(x, lin, dtype):
-    return (_LINEAR512 and x.is_cuda and not torch.is_grad_enabled() and dtype in (torch.float16, torch.bfloat16)
-            and x.dim() == 2 and x.size(1) == 512 and tuple(lin.weight.shape) == (512, 512) and x.size(0) >= 1)
-
-
-def _linear512(x, w_master, dtype):
-    """relu(x W^T) for x [M, 512] on csrc/linear512.hip; the packed weight is
-    cached on the master weight, keyed by its storage and version (bypassed
-    while a HIP graph is captured, wcache.capturing)."""
-    import ctypes
-
-    from . import _lib
-
-    x = x.to(dtype).contiguous()
-    code = _lib.DTYPE_F16 if dtype == torch.float16 else _lib.DTYPE_BF16
-    st = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
-    key = (w_master.data_ptr(), w_master._version, code)
-    use_cache = not capturing()
-    wf = cache_lookup(w_master, "_avr_linear512", key) if use_cache else None
-    if wf is None:
-        w = cast_weight(w_master, dtype, use_cache).contiguous()
-        wf = torch.empty(512, 512, dtype=dtype, device=x.device)
-        _lib.call("avr_linear512_pack_w", ctypes.c_void_p(w.data_ptr()), code, ctypes.c_void_p(wf.data_ptr()), st)
-        if use_cache:
-            cache_store(w_master, "_avr_linear512", key, wf)
-    y = torch.empty_like(x)
-    _lib.call("avr_linear512_relu_fwd", x.size(0), ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(wf.data_ptr()),
-              code, ctypes.c_void_p(y.data_ptr()), st)
-    return y
-
-
 # hipBLASLt / rocBLAS solutions picked by PyTorch TunableOp over every
 # candidate on MI355X (tools/tune_gemms.sh; bit-identical output to the
 # default solution, which only changes tiling): the width-512 layers at
@@ -266,7 +187,7 @@ def _linear512(x, w_master, dtype):
 # the caller had it afterwards: every other GEMM of the process keeps the
 # default heuristic, nothing is tuned or recorded, and no results file is
 # written at exit (TunableOp writes one only while it is enabled).  Not used
-# when the process runs TunableOp itself, off with AVR_TUNABLEOP=0.
+# when the process runs TunableOp itself, off with KernelOptions(tunableop=False).
 _TUNED_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_gfx950.csv")
 _TUNED = [None]  # None: not loaded yet; then True (entries loaded) or False
 
@@ -336,7 +257,7 @@ def _enable_tuned_gemms(device):
     if _TUNED[0] is not None:
         return _TUNED[0]
     _TUNED[0] = False
-    if os.environ.get("AVR_TUNABLEOP", "1") == "0" or not _TUNED_SHAPES:
+    if not _TUNED_SHAPES:
         return False
     import torch.cuda.tunable as tun
 
@@ -349,22 +270,22 @@ def _enable_tuned_gemms(device):
     return _TUNED[0]
 
 
-def _tuned_gemm(x, w):
+def _tuned_gemm(x, w, opts=DEFAULT):
     """True when relu(x W^T) is one of the shipped tuned shapes and the
     results loaded: the caller then runs the GEMM inside `_tuned_window`."""
-    return (("relu", x.dtype, x.size(0), w.size(0), x.size(1)) in _TUNED_SHAPES and x.is_cuda
+    return (opts.tunableop and ("relu", x.dtype, x.size(0), w.size(0), x.size(1)) in _TUNED_SHAPES and x.is_cuda
             and _enable_tuned_gemms(x.device))
 
 
-def _tuned_dgrad(g, w):
+def _tuned_dgrad(g, w, opts=DEFAULT):
     """As `_tuned_gemm` for the data gradient g @ W (g [rows, out], W [out, in])."""
-    return (("dgrad", g.dtype, g.size(0), w.size(0), w.size(1)) in _TUNED_SHAPES and g.is_cuda
+    return (opts.tunableop and ("dgrad", g.dtype, g.size(0), w.size(0), w.size(1)) in _TUNED_SHAPES and g.is_cuda
             and _enable_tuned_gemms(g.device))
 
 
-def _mm_dgrad(g, w):
+def _mm_dgrad(g, w, opts=DEFAULT):
     """g @ W, inside the TunableOp window for the file's shapes."""
-    if _tuned_dgrad(g, w):
+    if _tuned_dgrad(g, w, opts):
         with _tuned_window():
             return g @ w
     return g @ w
@@ -372,15 +293,12 @@ def _mm_dgrad(g, w):
 
 # The data gradient of a width-512 ReLU layer whose input is the previous
 # layer's ReLU output, with that ReLU's backward fused into the GEMM's
-# epilogue (csrc/linear512.hip, `avr_linear512_mask_fwd`); AVR_FUSED_DGRAD=0
-# keeps hipBLASLt + threshold_backward.
-_FUSED_DGRAD = os.environ.get("AVR_FUSED_DGRAD", "1") != "0"
-
-
-def _dgrad512_ok(x, w_master, dtype):
+# epilogue (csrc/linear512.hip, `avr_linear512_mask_fwd`);
+# KernelOptions(fused_dgrad=False) keeps hipBLASLt + threshold_backward.
+def _dgrad512_ok(x, w_master, dtype, opts=DEFAULT):
     """x: the chain's input (device and grad mode); the layer's own input is
     512 wide when its weight is 512 x 512."""
-    return (_FUSED_DGRAD and x.is_cuda and torch.is_grad_enabled() and dtype in (torch.float16, torch.bfloat16)
+    return (opts.fused_dgrad and x.is_cuda and torch.is_grad_enabled() and dtype in (torch.float16, torch.bfloat16)
             and x.dim() == 2 and tuple(w_master.shape) == (512, 512))
 
 
@@ -391,6 +309,8 @@ def _dgrad512_masked(g, w, x):
 
     from . import _lib
 
+    if tuple(w.shape) != (512, 512) or g.dim() != 2 or g.size(1) != 512 or x.shape != g.shape:
+        raise ValueError("_dgrad512_masked: g, x [N, 512] and W [512, 512] required")
     code = _lib.DTYPE_F16 if w.dtype == torch.float16 else _lib.DTYPE_BF16
     st = ctypes.c_void_p(torch.cuda.current_stream(g.device).cuda_stream)
     w = w.contiguous()
@@ -411,17 +331,14 @@ def _dgrad512_masked(g, w, x):
 # is 80 wide (the RAF sigma encoder's first layer: 13.3 vs 17.9 us forward,
 # 14.4 vs 19.2 data gradient at 83,200 rows), slower at 128 / 256 (e.g.
 # 15.7 vs 14.0, and 32.6 vs 26.6 for the masked data gradient against
-# hipBLASLt + threshold_backward).  AVR_NARROW: "80" (default) those shapes
-# only, "1" every shape it takes, "0" none.
-_NARROW = os.environ.get("AVR_NARROW", "80")
-
-
-def _narrow_ok(x, R, C, dtype, in_backward=False):
+# hipBLASLt + threshold_backward).  KernelOptions.narrow: "80" (default)
+# those shapes only, "all" every shape it takes, "off" none.
+def _narrow_ok(x, R, C, dtype, opts=DEFAULT, in_backward=False):
     """Y[N, C] = act(X[N, R] Bt[C, R]^T) fits avr_narrow_mm (training only:
     grad mode on, or called from a backward)."""
-    if _NARROW == "0" or (_NARROW != "1" and 80 not in (R, C)):
+    if opts.narrow == "off" or (opts.narrow != "all" and 80 not in (R, C)):
         return False
-    return (x.is_cuda and (in_backward or torch.is_grad_enabled())
+    return (x.is_cuda and x.dim() == 2 and (in_backward or torch.is_grad_enabled())
             and dtype in (torch.float16, torch.bfloat16)
             and R in (80, 128, 256) and 68 <= C <= 256 and C % 4 == 0 and (R < 256 or C <= 128))
 
@@ -444,11 +361,10 @@ def _narrow(x, bt, act, mask=None):
     return y
 
 
-def _fuse_dgrad_ok(x, w_master, dtype):
+def _fuse_dgrad_ok(x, w_master, dtype, opts=DEFAULT):
     """The layer's data gradient can carry its input ReLU's backward: the
     width-512 kernel or the narrow one fits (x: the chain's input)."""
-    return _dgrad512_ok(x, w_master, dtype) or (
-        x.dim() == 2 and _narrow_ok(x, w_master.size(0), w_master.size(1), dtype))
+    return _dgrad512_ok(x, w_master, dtype, opts) or _narrow_ok(x, w_master.size(0), w_master.size(1), dtype, opts)
 
 
 class _LinearReLU(torch.autograd.Function):
@@ -467,18 +383,22 @@ class _LinearReLU(torch.autograd.Function):
     the same selection threshold_backward makes (y > 0 with y = the next
     layer's x), applied to the same rounded values.  `link` (the last layer
     of `MLP.hidden`): a one-element list the output's consumer sets when it
-    applies the mask itself (the fused head)."""
+    applies the mask itself (the fused head).  The data-gradient kernel is
+    chosen in the forward (ctx.dgrad: "narrow", "512" or "gemm") from the
+    shapes it was built for, so the backward never reaches a kernel whose
+    shape checks the forward did not make."""
 
     @staticmethod
-    def forward(ctx, x, w_master, dtype, cache=False, mask_gx=False, gy_masked=False, link=None):
+    def forward(ctx, x, w_master, dtype, cache=False, mask_gx=False, gy_masked=False, link=None, opts=DEFAULT):
         w = cast_weight(w_master, dtype, cache)
         # (grad mode is off inside forward: training is "an input needs grad")
-        if (x.is_cuda and any(ctx.needs_input_grad[:2]) and _narrow_ok(x, w.size(1), w.size(0), dtype, True)
-                and x.dtype == dtype and x.dim() == 2):
+        training = any(ctx.needs_input_grad[:2])
+        if (x.is_cuda and training and _narrow_ok(x, w.size(1), w.size(0), dtype, opts, True)
+                and x.dtype == dtype):
             y = _narrow(x, w, 1)
         elif x.is_cuda:
             bias = _zero_bias(w.size(0), dtype, x.device)
-            if _tuned_gemm(x, w):
+            if _tuned_gemm(x, w, opts):
                 with _tuned_window():
                     y = torch._addmm_activation(bias, x, w.t(), use_gelu=False)
             else:
@@ -486,7 +406,17 @@ class _LinearReLU(torch.autograd.Function):
         else:
             y = torch.relu(x @ w.t())
         ctx.save_for_backward(x, w, y)
-        ctx.mask_gx, ctx.gy_masked, ctx.link = mask_gx, gy_masked, link
+        ctx.gy_masked, ctx.link, ctx.opts = gy_masked, link, opts
+        # the data gradient g [N, out] @ W [out, in]: narrow kernel, the
+        # width-512 masked one (only with mask_gx, for a 512 x 512 weight and
+        # a 2-D 16-bit input), or the GEMM (+ threshold_backward if masked)
+        dg = "gemm"
+        if x.is_cuda and x.dtype == dtype and _narrow_ok(x, w.size(0), w.size(1), dtype, opts, True):
+            dg = "narrow"
+        elif (mask_gx and x.is_cuda and x.dim() == 2 and x.dtype == dtype and tuple(w.shape) == (512, 512)
+              and dtype in (torch.float16, torch.bfloat16) and opts.fused_dgrad):
+            dg = "512"
+        ctx.dgrad, ctx.mask_gx = dg, mask_gx
         return y
 
     @staticmethod
@@ -496,21 +426,26 @@ class _LinearReLU(torch.autograd.Function):
         g = gy.contiguous() if masked else torch.ops.aten.threshold_backward(gy, y, 0).contiguous()
         gx = None
         if ctx.needs_input_grad[0]:
-            narrow = _narrow_ok(g, w.size(0), w.size(1), w.dtype, True) and g.dtype == w.dtype
-            if ctx.mask_gx:
-                gx = _narrow(g, w.t(), 2, x) if narrow else _dgrad512_masked(g, w, x)
+            narrow = ctx.dgrad == "narrow" and g.dtype == w.dtype
+            if narrow:
+                gx = _narrow(g, w.t(), 2 if ctx.mask_gx else 0, x if ctx.mask_gx else None)
+            elif ctx.dgrad == "512" and g.dtype == w.dtype:
+                gx = _dgrad512_masked(g, w, x)
             else:
-                gx = _narrow(g, w.t(), 0) if narrow else _mm_dgrad(g, w)
-        gw = _wgrad(g, x) if ctx.needs_input_grad[1] else None
-        return gx, gw, None, None, None, None, None
+                gx = _mm_dgrad(g, w, ctx.opts)
+                if ctx.mask_gx:
+                    gx = torch.ops.aten.threshold_backward(gx, x, 0)
+        gw = _wgrad(g, x, ctx.opts) if ctx.needs_input_grad[1] else None
+        return gx, gw, None, None, None, None, None, None
 
 
 class MLP(nn.Module):
     """tcnn.Network(n_in, n_out, {n_neurons, n_hidden_layers, activation ReLU,
     output_activation None}) without biases."""
 
-    def __init__(self, n_in, n_out, cfg, dtype=torch.float32):
+    def __init__(self, n_in, n_out, cfg, dtype=torch.float32, options=None):
         super().__init__()
+        self.options = resolve(options)
         width = int(cfg["n_neurons"])
         depth = int(cfg["n_hidden_layers"])
         if cfg.get("activation", "ReLU") != "ReLU":
@@ -532,38 +467,29 @@ class MLP(nn.Module):
         x = x.to(self.dtype).contiguous()
         # layer i >= 1 takes layer i-1's ReLU output only: its data gradient
         # can carry that ReLU's backward (_LinearReLU's flags)
-        fuse = [i > 0 and _fuse_dgrad_ok(x, lin.weight, self.dtype) for i, lin in enumerate(hid)]
+        o = self.options
+        fuse = [i > 0 and _fuse_dgrad_ok(x, lin.weight, self.dtype, o) for i, lin in enumerate(hid)]
         for i, lin in enumerate(hid):
             x = _LinearReLU.apply(x, lin.weight, self.dtype, not torch.is_grad_enabled(), fuse[i],
-                                  i + 1 < len(hid) and fuse[i + 1], link if i + 1 == len(hid) else None)
+                                  i + 1 < len(hid) and fuse[i + 1], link if i + 1 == len(hid) else None, o)
         return x
 
     def hidden_from(self, x, start):
         """Hidden layers start .. n-2 (each followed by ReLU) on x, the
-        rectified output of layer start-1; at inference two 512 -> 512
-        layers at a time in one launch (`_mlp512x2`)."""
+        rectified output of layer start-1."""
         x = x.to(self.dtype).contiguous()
-        hid = list(self.layers[start:-1])
-        i = 0
-        while i < len(hid):
-            if i + 1 < len(hid) and _mlp512x2_ok(x, hid[i], hid[i + 1], self.dtype):
-                x = _mlp512x2(x, hid[i].weight, hid[i + 1].weight, self.dtype)
-                i += 2
-                continue
-            if _linear512_ok(x, hid[i], self.dtype):
-                x = _linear512(x, hid[i].weight, self.dtype)
-            else:
-                x = _LinearReLU.apply(x, hid[i].weight, self.dtype, not torch.is_grad_enabled())
-            i += 1
+        for lin in self.layers[start:-1]:
+            x = _LinearReLU.apply(x, lin.weight, self.dtype, not torch.is_grad_enabled(), False, False, None,
+                                  self.options)
         return x
 
     def last(self, h):
         """The bias-free output layer (output_activation None); a one-output
         layer in training on `_LinearOut1`."""
         w = self.layers[-1].weight
-        if _out1_ok(h, w, self.dtype):
+        if _out1_ok(h, w, self.dtype, self.options):
             return _LinearOut1.apply(h.to(self.dtype), w, self.dtype, False)
-        return _Linear.apply(h.contiguous(), w, self.dtype, not torch.is_grad_enabled())
+        return _Linear.apply(h.contiguous(), w, self.dtype, not torch.is_grad_enabled(), self.options)
 
     def forward(self, x, out_relu=False):
         """The network; `out_relu=True` returns relu(output) with the ReLU in
@@ -619,13 +545,12 @@ def _fused_sigma_ok(model, pts, layout, variant):
     kernel.  Training (autograd recording) keeps the per-layer path, whose
     saved activations the backward needs."""
     return (layout is not None and pts.is_cuda and not torch.is_grad_enabled()
-            and os.environ.get("AVR_FUSED_SIGMA", "1") != "0"
-            and _sigma.variant_of(model) == variant)
+            and model.options.fused_sigma and _sigma.variant_of(model) == variant)
 
 
-def _concat_ok(pts, layout):
+def _concat_ok(pts, layout, opts=DEFAULT):
     """Grouped concatenation on the HIP path (renderer layout, GPU tensors)."""
-    return layout is not None and pts.is_cuda and os.environ.get("AVR_GROUPED_CONCAT", "1") != "0"
+    return layout is not None and pts.is_cuda and opts.grouped_concat
 
 
 _HALF = torch.tensor(0.5)
@@ -705,19 +630,22 @@ def _cat_features(parts, layout):
 
 class AVRModel(nn.Module):
     """model.py:63-235 without channel embedding: pos/dir/tx hash grids,
-    sigma encoder (-> 128) and decoder (-> 1), signal network (-> T)."""
+    sigma encoder (-> 128) and decoder (-> 1), signal network (-> T).
+    `options`: the kernel selection (avr_amd.KernelOptions; defaults are the
+    shipped paths)."""
 
-    def __init__(self, cfg, mlp_dtype=torch.float32, enc_dtype=torch.float16):
+    def __init__(self, cfg, mlp_dtype=torch.float32, enc_dtype=torch.float16, options=None):
         super().__init__()
-        self._pos_encoding = HashGridEncoding(3, cfg["pos_encoding_sigma"], dtype=enc_dtype, seed=1)
-        self._dir_encoding = HashGridEncoding(3, cfg["dir_encoding_sig"], dtype=enc_dtype, seed=2)
-        self._tx_encoding = HashGridEncoding(3, cfg["tx_encoding_sig"], dtype=enc_dtype, seed=3)
+        o = self.options = resolve(options)
+        self._pos_encoding = HashGridEncoding(3, cfg["pos_encoding_sigma"], dtype=enc_dtype, seed=1, options=o)
+        self._dir_encoding = HashGridEncoding(3, cfg["dir_encoding_sig"], dtype=enc_dtype, seed=2, options=o)
+        self._tx_encoding = HashGridEncoding(3, cfg["tx_encoding_sig"], dtype=enc_dtype, seed=3, options=o)
         self.signal_output_dim = int(cfg["signal_output_dim"])
         self._model_encoder_sigma = MLP(self._pos_encoding.n_output_dims, 128,
-                                        cfg["sigma_encoder_network"], mlp_dtype)
-        self._model_decoder_sigma = MLP(128, 1, cfg["sigma_decoder_network"], mlp_dtype)
+                                        cfg["sigma_encoder_network"], mlp_dtype, o)
+        self._model_decoder_sigma = MLP(128, 1, cfg["sigma_decoder_network"], mlp_dtype, o)
         sig_in = 128 + self._dir_encoding.n_output_dims + self._tx_encoding.n_output_dims
-        self._model_signal = MLP(sig_in, self.signal_output_dim, cfg["signal_network"], mlp_dtype)
+        self._model_signal = MLP(sig_in, self.signal_output_dim, cfg["signal_network"], mlp_dtype, o)
         self._sigma_pack = _sigma.SigmaWeights()
 
     # AVRRender passes ray_layout=(B, R, S) to networks that declare this
@@ -740,7 +668,7 @@ class AVRModel(nn.Module):
         pos_enc = self._pos_encoding(_unit(pts.reshape(-1, 3)))
         sigma_feat = self._model_encoder_sigma(pos_enc)
         attn = self._model_decoder_sigma(F.relu(sigma_feat))
-        if _concat_ok(pts, L):
+        if _concat_ok(pts, L, self.options):
             B, R, S = L
             dir_e = self._dir_encoding(_unit(_per_ray(view.reshape(-1, 3), L)))
             tx_e = self._tx_encoding(_unit(_per_pose(tx.reshape(-1, 3), L)))
@@ -796,7 +724,7 @@ class AVRModel(nn.Module):
     def _signal_hidden(self, pts, view, tx, ch_idx, ray_layout):
         """(attn, h): h the signal network's last hidden activation."""
         if (ch_idx is None and _fused_sigma_ok(self, pts, ray_layout, _sigma.MESHRIR)
-                and os.environ.get("AVR_FUSED_H1", "1") != "0" and _sigma.h1_ok(self)):
+                and self.options.fused_h1 and _sigma.h1_ok(self)):
             attn, h1 = self._trunk_fused_h1(pts, view, tx, ray_layout)
             return attn, self._model_signal.hidden_from(h1, 1)
         attn, base = self._trunk(pts, view, tx, ch_idx, ray_layout)
@@ -822,11 +750,12 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
     """model.py:238-331: six hash grids (pos/tx for sigma and for signal,
     view and tx orientation), sigma encoder (-> 256) / decoder, signal MLP."""
 
-    def __init__(self, cfg, mlp_dtype=torch.float32, enc_dtype=torch.float32):
+    def __init__(self, cfg, mlp_dtype=torch.float32, enc_dtype=torch.float32, options=None):
         super().__init__()
+        o = self.options = resolve(options)
         self.leaky_relu = cfg["leaky_relu"]
         self.signal_output_dim = int(cfg["signal_output_dim"])
-        E = lambda key, seed: HashGridEncoding(3, cfg[key], dtype=enc_dtype, seed=seed)  # noqa: E731
+        E = lambda key, seed: HashGridEncoding(3, cfg[key], dtype=enc_dtype, seed=seed, options=o)  # noqa: E731
         self._pos_encoding = E("pos_encoding_sigma", 11)
         self._pos_signal_encoding = E("pos_encoding_sig", 12)
         self._tx_pos_encoding = E("tx_pos_encoding_sigma", 13)
@@ -834,11 +763,11 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
         self._dir_encoding = E("dir_encoding_sig", 15)
         self._tx_dir_encoding = E("tx_dir_encoding_sig", 16)
         n_in = self._pos_encoding.n_output_dims + self._tx_pos_encoding.n_output_dims
-        self._model_encoder_sigma = MLP(n_in, 256, cfg["sigma_encoder_network"], mlp_dtype)
-        self._model_decoder_sigma = MLP(256, 1, cfg["sigma_decoder_network"], mlp_dtype)
+        self._model_encoder_sigma = MLP(n_in, 256, cfg["sigma_encoder_network"], mlp_dtype, o)
+        self._model_decoder_sigma = MLP(256, 1, cfg["sigma_decoder_network"], mlp_dtype, o)
         n_sig = (256 + self._dir_encoding.n_output_dims + self._tx_dir_encoding.n_output_dims
                  + self._pos_signal_encoding.n_output_dims + self._tx_pos_signal_encoding.n_output_dims)
-        self._model_signal = MLP(n_sig, self.signal_output_dim, cfg["signal_network"], mlp_dtype)
+        self._model_signal = MLP(n_sig, self.signal_output_dim, cfg["signal_network"], mlp_dtype, o)
         self._sigma_pack = _sigma.SigmaWeights()
 
     accepts_ray_layout = True
@@ -870,7 +799,7 @@ class AVRModel_complex(nn.Module):  # noqa: N801  (reference name)
         view = _unit(view.reshape(-1, 3))
         tx = _unit(tx.reshape(-1, 3))
         tx_view = _unit(tx_view.reshape(-1, 3))
-        if _concat_ok(pts, L):
+        if _concat_ok(pts, L, self.options):
             return self._trunk_grouped(pts, view, tx, tx_view, L)
         pos_e = _grouped(self._pos_encoding, pts, L, "sample")
         txp_e = _grouped(self._tx_pos_encoding, tx, L, "pose")

@@ -20,7 +20,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 import threading
 
 import torch
@@ -28,6 +27,7 @@ import torch.nn as nn
 
 from . import _lib
 from ._lib import DTYPE_BF16, DTYPE_F16, DTYPE_F32, render_params
+from .options import tuning_env
 from .wcache import cache_lookup, cache_store, capturing, cast_weight
 
 
@@ -114,8 +114,8 @@ class Tables:
 
     def core_layout(self, p, B, sig_code):
         """(offsets[5], n_split, k_split) of avr_render_core_fwd's workspace."""
-        # tuning overrides read by the library (tools/tune.py) are part of the key
-        key = (p.n_rays, B, sig_code, os.environ.get("AVR_NSPLIT"), os.environ.get("AVR_KSPLIT"))
+        # tuning overrides read by the library (options.TUNING_ENV) are part of the key
+        key = (p.n_rays, B, sig_code) + tuning_env()
         v = self._layouts.get(key)
         if v is None:
             with _TABLE_LOCK:
@@ -166,11 +166,6 @@ def check_config(p, tables: Tables):
 # --------------------------------------------------------------------------
 # launch heuristics
 # --------------------------------------------------------------------------
-def _env_int(name):
-    v = os.environ.get(name)
-    return int(v) if v else None
-
-
 def reduce_splits(p, B, sig_code):
     """Ray splits of the reduction, decided by the library for this shape."""
     import ctypes
@@ -184,7 +179,8 @@ def pick_k_split(B, S, T):
     """t-slices of the DFT GEMM: about 256 workgroups. AVR_KSPLIT overrides."""
     F = T // 2 + 1
     nkc = math.ceil(T / 64)
-    forced = _env_int("AVR_KSPLIT")
+    forced = tuning_env()[1]
+    forced = int(forced) if forced else None
     if forced:
         return max(1, min(nkc, forced))
     base = math.ceil(F / 128) * math.ceil(S / 32) * B
@@ -330,12 +326,6 @@ def _packed_exact_weight(w_master, W, cache, pref, shape_key, nbytes, st):
     Wf = torch.empty(nbytes // 2, dtype=W.dtype, device=W.device)
     _lib.call("avr_head_pack_w_exact", pref, K, _ptr(W), code, _ptr(Wf), st)
     return cache_store(w_master, "_avr_exactpack", key, Wf) if cache else Wf
-
-
-# The fused head's backward applies the last hidden layer's ReLU mask when
-# that layer hands it over (AVR_HEAD_RELU=0: the layer keeps its own
-# threshold_backward; bitwise the same gradients)
-_HEAD_RELU = os.environ.get("AVR_HEAD_RELU", "1") != "0"
 
 
 class FusedHeadCore(torch.autograd.Function):
@@ -511,6 +501,10 @@ class AVRRender(nn.Module):
         # which sums the exact products (about 3e-4 relative off the
         # reference's rounded render at fp16).
         self.exact_head = bool(kwargs.get("exact_head", True))
+        # the fused head's backward applies the last hidden layer's ReLU mask
+        # when that layer hands it over (False: the layer keeps its own
+        # threshold_backward; bitwise the same gradients)
+        self.head_relu_link = bool(kwargs.get("head_relu_link", True))
         self._pcache = {}
         self._pcache_lock = threading.Lock()
         # jitter the sampling kernel reads at run time while a HIP graph is
@@ -764,7 +758,7 @@ class AVRRender(nn.Module):
             attn, h, weight, dtype = self.network_fn.forward_fused(*net_in, **kw)
             if self._head_supported(geom, h, weight, dtype):
                 # our own networks leave the link of h's ReLU (model.MLP.hidden)
-                link = getattr(self.network_fn, "_relu_link", None) if _HEAD_RELU else None
+                link = getattr(self.network_fn, "_relu_link", None) if self.head_relu_link else None
                 self.network_fn.__dict__.pop("_relu_link", None)
                 return self.render_from_hidden(attn, h, weight, dtype, geom, link)
             signal = self.network_fn.finish_signal(h)

@@ -336,17 +336,9 @@ int avr_linear_out1_fwd(int64_t N, int32_t K, const void* x, const void* w, int3
 int avr_linear_out1_workspace(int32_t K, int64_t* floats);
 int avr_linear_out1_bwd(int64_t N, int32_t K, const void* x, const void* w, const void* grad_y, int32_t dtype,
                         void* grad_x, float* workspace, float* grad_w, void* stream);
-/* One width-512 hidden layer at inference, y = relu(x W^T): x, y [M][512],
- * W [512][512] (out x in), 16-bit (AVR_DTYPE_F16 / AVR_DTYPE_BF16), fp32
- * accumulation, one rounding of the output (model.py:176-180, tcnn
- * CutlassMLP).  Replaces the hipBLASLt GEMM with ReLU epilogue the per-layer
- * path runs (torch._addmm_activation).  avr_linear512_pack_w lays W out in
- * MFMA fragment order into Wf (512 KiB, 16-byte aligned), once per weight
- * version; x, y 16-byte aligned. */
-int avr_linear512_pack_w(const void* W, int32_t dtype, void* Wf, void* stream);
-int avr_linear512_relu_fwd(int64_t M, const void* x, const void* Wf, int32_t dtype, void* y, void* stream);
-/* avr_linear512_pack_w with transpose = 1 packs W^T (for a data gradient,
- * g W = g (W^T)^T); transpose = 0 is avr_linear512_pack_w. */
+/* The packed weight of avr_linear512_mask_fwd: W [512][512] (16-bit,
+ * 16-byte aligned) in MFMA fragment order into Wf (512 KiB, 16-byte
+ * aligned); transpose = 1 packs W^T (for a data gradient, g W = g (W^T)^T). */
 int avr_linear512_pack_w2(const void* W, int32_t dtype, int32_t transpose, void* Wf, void* stream);
 /* The data gradient of a ReLU layer whose input x is itself a ReLU output
  * consumed only by this layer, with that ReLU's backward fused:
@@ -358,16 +350,19 @@ int avr_linear512_pack_w2(const void* W, int32_t dtype, int32_t transpose, void*
 int avr_linear512_mask_fwd(int64_t M, const void* x, const void* Wf, int32_t dtype, const void* mask, void* y,
                            void* stream);
 
-/* Two consecutive width-512 hidden layers of the signal network in one
- * launch (model.py:176-180, AVRModel's `_model_signal` layers 1 and 2 at
- * inference): y = relu(relu(x W1^T) W2^T), x / y [M][512], W1 / W2 [512][512]
- * (nn.Linear layout), all 16-bit (dtype fp16 / bf16); each layer fp32
- * accumulation over k in order and one rounding, the intermediate activation
- * kept on chip.  avr_mlp512x2_pack_w packs both weights into Wf (2 * 512 * 512
- * 16-bit values; once per weight update); x, W1, W2, Wf, y 16-byte aligned
- * (csrc/mlp512.hip). */
+#ifdef AVR_SHAPE_PROBES
+/* Experiments kept for tools/ (the shapes build, make -C avr_amd/csrc
+ * shapes), measured slower than the tuned hipBLASLt layers they would
+ * replace and not in libavr_hip.so:
+ * one width-512 ReLU layer at inference, y = relu(x W^T) (x, y [M][512], W
+ * packed by avr_linear512_pack_w = avr_linear512_pack_w2 with transpose 0),
+ * and two consecutive ones in one launch, y = relu(relu(x W1^T) W2^T)
+ * (csrc/mlp512.hip; avr_mlp512x2_pack_w packs both weights). */
+int avr_linear512_pack_w(const void* W, int32_t dtype, void* Wf, void* stream);
+int avr_linear512_relu_fwd(int64_t M, const void* x, const void* Wf, int32_t dtype, void* y, void* stream);
 int avr_mlp512x2_pack_w(const void* W1, const void* W2, int32_t dtype, void* Wf, void* stream);
 int avr_mlp512x2_fwd(int64_t M, const void* x, const void* Wf, int32_t dtype, void* y, void* stream);
+#endif
 int avr_linear_wgrad(int64_t N, int32_t M, int32_t K, const void* grad_y, const void* x,
                      float* workspace, int32_t splits, float* grad_w, void* stream);
 

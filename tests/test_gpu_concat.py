@@ -1,9 +1,12 @@
 """GPU: grouped feature concatenation (`csrc/concat.hip`) against the
 expand + cat it replaces (forward: exact; backward: group sums in fp32 up
 to summation order, deterministic), and inside the networks' training path
-(AVR_GROUPED_CONCAT=0 vs 1)."""
+(KernelOptions(grouped_concat=False) vs True)."""
 import pytest
 import torch
+
+from avr_amd.options import KernelOptions
+from avr_amd.options import apply as apply_options
 
 from avr_amd.concat import grouped_concat
 
@@ -68,8 +71,8 @@ def test_network_training_path_matches_expand_cat(cls, monkeypatch):
     view = torch.rand(B, R, 1, 3, device=DEV).expand(B, R, S, 3).reshape(B, R * S, 3) * 2 - 1
     tx = torch.rand(B, 1, 3, device=DEV).expand(B, R * S, 3).contiguous() * 2 - 1
     res = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("AVR_GROUPED_CONCAT", flag)
+    for flag in (False, True):
+        apply_options(m, KernelOptions(grouped_concat=flag))
         m.zero_grad()
         attn, sig = m(pts, view, tx, *extra, ray_layout=(B, R, S))
         (attn.float().sum() + sig.float().square().mean()).backward()

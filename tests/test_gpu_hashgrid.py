@@ -7,6 +7,8 @@ import numpy as np
 import pytest
 import torch
 
+from avr_amd.options import KernelOptions
+
 from oracle import hashgrid_oracle as hgo
 
 from avr_amd.encoding import HashGridEncoding, level_layout
@@ -53,9 +55,8 @@ BWD_IMPLS = ["partitioned", "atomic"]  # avr_hashgrid_bwd_partitioned (training'
 
 @pytest.mark.parametrize("impl", BWD_IMPLS)
 def test_backward_matches_restatement(impl, monkeypatch):
-    monkeypatch.setenv("AVR_HASHGRID_BWD", impl)
     cfg = dict(CFG, n_levels=8, log2_hashmap_size=14)
-    enc = HashGridEncoding(3, cfg, dtype=torch.float32, seed=6).to(DEV)
+    enc = HashGridEncoding(3, cfg, dtype=torch.float32, seed=6, options=KernelOptions(hashgrid_bwd=impl)).to(DEV)
     x = _points(2048, 1)
     xt = torch.from_numpy(x).to(DEV)
     out = enc(xt)
@@ -134,9 +135,8 @@ def test_backward_reference_size_tables(log2, gdtype, impl, monkeypatch):
     fp32 sums in any order: 1e-5 relative to the gradient's scale.  The
     first samples of 300 rays sit on one point (every ray of a pose starts at
     the listener): hundreds of adds into the same entries."""
-    monkeypatch.setenv("AVR_HASHGRID_BWD", impl)
     cfg = dict(CFG, log2_hashmap_size=log2)
-    enc = HashGridEncoding(3, cfg, dtype=gdtype, seed=9).to(DEV)
+    enc = HashGridEncoding(3, cfg, dtype=gdtype, seed=9, options=KernelOptions(hashgrid_bwd=impl)).to(DEV)
     x = np.concatenate([_ray_points(48, 256, 4), _points(8192, 5), _ray_points(300, 16, 7, step=2e-3)[:1].repeat(300, 0),
                         _points(37, 8)])
     xt = torch.from_numpy(x).to(DEV)

@@ -199,9 +199,8 @@ def test_head_takes_over_last_relu_backward(monkeypatch):
     hidden layer's ReLU mask (avr_head_bwd2 relu_mask) and the layer skips
     its threshold_backward.  The same selection on the same rounded values:
     every parameter gradient bitwise equal to the unlinked path
-    (AVR_HEAD_RELU=0), and the link was taken."""
+    (AVRRender(head_relu_link=False)), and the link was taken."""
     from avr_amd import model as M
-    from avr_amd import renderer
 
     w = WORKLOADS["c1_meshrir_plumbing"].replace(name="raf_small", **{k: v for k, v in WORKLOADS[
         "c3_raf_furnished_b4"].render.items() if k not in ("n_azi", "n_ele", "n_samples")})
@@ -218,7 +217,7 @@ def test_head_takes_over_last_relu_backward(monkeypatch):
     monkeypatch.setattr(M.MLP, "hidden", lambda self, x, link=None: (links.append(link), orig(self, x, link))[1])
     grads = []
     for on in (True, False):
-        monkeypatch.setattr(renderer, "_HEAD_RELU", on)
+        r.head_relu_link = on
         r.zero_grad(set_to_none=True)
         torch.manual_seed(5)
         out = r(ro, tx, dtx)

@@ -1,7 +1,7 @@
 """GPU: the fused sigma networks (`csrc/sigma.hip`) against the plain
 PyTorch statement of the unfused 16-bit path (`sigma.reference_fwd`, fp32
 GEMMs on bf16 / fp16 operands with outputs in that dtype), and inside the
-networks against the per-layer path (AVR_FUSED_SIGMA=0), in bf16 and in
+networks against the per-layer path (KernelOptions(fused_sigma=False)), in bf16 and in
 fp16 (tcnn's MLP precision, model.py:21-31).
 
 Tolerance: both sides round every activation to the MLP dtype; they differ
@@ -13,6 +13,9 @@ elements within 2 bf16 ulps."""
 import numpy as np
 import pytest
 import torch
+
+from avr_amd.options import KernelOptions
+from avr_amd.options import apply as apply_options
 
 from avr_amd import AVRRender, sigma
 from avr_amd.model import AVRModel, AVRModel_complex
@@ -117,9 +120,9 @@ def _net_pair(cls, dtype=torch.bfloat16):
 def test_network_fused_sigma_matches_per_layer(cls, monkeypatch, dtype):
     m, args, L = _net_pair(cls, dtype)
     with torch.no_grad():
-        monkeypatch.setenv("AVR_FUSED_SIGMA", "0")
+        apply_options(m, KernelOptions(fused_sigma=False))
         a0, h0, _, _ = m.forward_fused(*args, ray_layout=L)
-        monkeypatch.setenv("AVR_FUSED_SIGMA", "1")
+        apply_options(m, KernelOptions())
         a1, h1, _, _ = m.forward_fused(*args, ray_layout=L)
     torch.cuda.synchronize()
     assert h1.dtype == dtype
@@ -134,8 +137,8 @@ def test_render_with_fused_sigma_matches_per_layer(monkeypatch):
     ro = torch.rand(1, 3, device=DEV) * 2 - 1
     tx = torch.rand(1, 3, device=DEV) * 2 - 1
     outs = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("AVR_FUSED_SIGMA", flag)
+    for flag in (False, True):
+        apply_options(r, KernelOptions(fused_sigma=flag))
         torch.manual_seed(5)
         with torch.no_grad():
             outs.append(r(ro, tx))
@@ -184,10 +187,9 @@ def test_sigma_h1_kernel_matches_reference(N, S, dtype):
 def test_network_fused_h1_matches_per_layer(monkeypatch, dtype):
     m, args, L = _net_pair("AVRModel", dtype)
     with torch.no_grad():
-        monkeypatch.setenv("AVR_FUSED_SIGMA", "0")
+        apply_options(m, KernelOptions(fused_sigma=False))
         a0, h0, _, _ = m.forward_fused(*args, ray_layout=L)
-        monkeypatch.setenv("AVR_FUSED_SIGMA", "1")
-        monkeypatch.setenv("AVR_FUSED_H1", "1")
+        apply_options(m, KernelOptions(fused_sigma=True, fused_h1=True))
         a1, h1, _, _ = m.forward_fused(*args, ray_layout=L)
     torch.cuda.synchronize()
     _close(a1, a0, "attn")

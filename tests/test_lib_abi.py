@@ -16,6 +16,8 @@ HEADER = os.path.join(ROOT, "include", "avr_hip.h")
 def _declared():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    # the shapes build's experiments are not part of the product library
+    text = re.sub(r"#ifdef AVR_SHAPE_PROBES.*?#endif", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(avr_[a-z0-9_]+)\s*\(", text)))
 
 

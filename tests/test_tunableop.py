@@ -53,13 +53,18 @@ def test_tuned_shapes_parsed():
     assert not model._tuned_dgrad(x, w)
 
 
-def test_loader_respects_opt_out(monkeypatch):
-    """AVR_TUNABLEOP=0 returns before touching TunableOp or the device (on
-    this CPU-only container any such call would raise)."""
+def test_opt_out_never_touches_tunableop(monkeypatch):
+    """KernelOptions(tunableop=False) returns before touching TunableOp or the
+    device (on this CPU-only container any such call would raise)."""
+    from avr_amd.options import KernelOptions
+
     monkeypatch.setattr(model, "_TUNED", [None])
-    monkeypatch.setenv("AVR_TUNABLEOP", "0")
-    assert model._enable_tuned_gemms(torch.device("cpu")) is False
-    assert model._TUNED[0] is False
+    x = torch.empty(262144, 512, dtype=torch.float16)
+    w = torch.empty(512, 512, dtype=torch.float16)
+    off = KernelOptions(tunableop=False)
+    assert not model._tuned_gemm(x, w, off)
+    assert not model._tuned_dgrad(x, w, off)
+    assert model._TUNED[0] is None
 
 
 def _state():
@@ -75,8 +80,6 @@ def test_tuned_layer_bit_identical(dtype, rows):
     default hipBLASLt solution's output bit for bit (TunableOp off), with the
     tuned entry verifiably loaded, and TunableOp left as it was: config 2's
     262,144 rows and config 5's 2,097,152."""
-    if os.environ.get("AVR_TUNABLEOP", "1") == "0":
-        pytest.skip("AVR_TUNABLEOP=0: the shipped solution is switched off")
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(3)
     x = torch.relu(torch.randn(rows, 512, device=dev, generator=g)).to(dtype)
@@ -104,8 +107,6 @@ def test_tuned_dgrad_bit_identical(rows, out, inp):
     """The data gradient g @ W through `_mm_dgrad` with the shipped solution
     equals the default solution's output bit for bit, and TunableOp is left
     as it was (config-3 / -4 training shapes)."""
-    if os.environ.get("AVR_TUNABLEOP", "1") == "0":
-        pytest.skip("AVR_TUNABLEOP=0: the shipped solution is switched off")
     dev = torch.device("cuda", 0)
     gen = torch.Generator(device=dev).manual_seed(rows + out)
     g = torch.randn(rows, out, device=dev, generator=gen).to(torch.bfloat16)

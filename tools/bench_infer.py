@@ -21,6 +21,8 @@ sys.path.insert(0, ROOT)
 
 from avr_amd import AVRRender, spectrum_to_ir  # noqa: E402
 from avr_amd.model import AVRModel  # noqa: E402
+from avr_amd.options import KernelOptions  # noqa: E402
+from avr_amd.options import apply as apply_options  # noqa: E402
 from avr_amd.workloads import MESHRIR_MODEL, WORKLOADS  # noqa: E402
 
 
@@ -44,10 +46,10 @@ def main():
            "network": "AVRModel (avr_meshrir.yml model block, random init)"}
     outs = {}
     # (key, fused signal head, fused sigma networks)
-    for key, fused, fsig in (("unfused", False, "0"), ("fused_head_only", True, "0"), ("fused", True, "1")):
+    for key, fused, fsig in (("unfused", False, False), ("fused_head_only", True, False), ("fused", True, True)):
         if key not in args.variants.split(","):
             continue
-        os.environ["AVR_FUSED_SIGMA"] = fsig
+        apply_options(model, KernelOptions.from_env(KernelOptions(fused_sigma=fsig)))
         r = AVRRender(model, fused_head=fused, **w.render)
 
         def step():

@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 
 from avr_amd import AVRRender  # noqa: E402
 from avr_amd.model import AVRModel_complex  # noqa: E402
+from avr_amd.options import KernelOptions  # noqa: E402
 from avr_amd.training import TrainStep  # noqa: E402
 from avr_amd.workloads import RAF_MODEL, WORKLOADS  # noqa: E402
 
@@ -129,7 +130,7 @@ def main():
     # full training step
     mlp_dtype = torch.bfloat16 if args.mlp_dtype == "bf16" else torch.float32
     cfg = dict(RAF_MODEL, signal_output_dim=T)
-    model = AVRModel_complex(cfg, mlp_dtype=mlp_dtype).to(dev)
+    model = AVRModel_complex(cfg, mlp_dtype=mlp_dtype, options=KernelOptions.from_env()).to(dev)
     r = AVRRender(model, fused_head=not args.no_fused, **w.render).to(dev)
     # RAF training config (config_files/avr_raf_*.yml:24-40); the same Adam as
     # the reference's torch.optim.Adam, as one fused multi-tensor kernel

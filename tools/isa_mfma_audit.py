@@ -1,39 +1,48 @@
-"""Audit of MFMA operand hazards in the shipped kernels' compiled code
-(round-5 task 4).
+"""Audit of MFMA operand hazards in the compiled gfx950 code (DESIGN.md
+§14d, §15a).
 
-Compiles each HIP source of the library with -save-temps (the product
-flags) and scans the gfx950 assembly of every kernel, within basic blocks:
+Default: the product library as built.  The gfx950 code objects are taken
+out of `avr_amd/libavr_hip.so`'s `.hip_fatbin` (one clang offload bundle per
+translation unit), disassembled with llvm-objdump and scanned kernel by
+kernel, within basic blocks (split at branches and at branch targets):
 
-* WAR: after a `v_mfma_*`, any instruction within WINDOW wait states that
+* WAR: after a `v_mfma_*`, an instruction within WINDOW wait states that
   writes a VGPR of the MFMA's SrcA or SrcB (a VALU result, an LDS or
-  global load's return, another MFMA's D), with the number of wait states
-  between them (an instruction counts 1, `s_nop N` counts N + 1);
-* RAW: before a `v_mfma_*`, a VALU write of one of its SrcA/SrcB VGPRs
-  within WINDOW states, and the states between.
+  global load's return, another MFMA's D), with the wait states between
+  them (an instruction counts 1, `s_nop N` counts N + 1).  The kind
+  `WAR_after_mfma_B_behind_mfma` is the one that corrupted results on
+  MI355X (§14d: the MFMA issued right behind another MFMA, its B register
+  rewritten before the matrix pipe took it): the product must have none;
+* RAW: before a `v_mfma_*`, the nearest VALU write of one of its SrcA/SrcB
+  VGPRs within WINDOW states (the hardware needs one state, §14d);
+* M0: every LDS-DMA load (`global_load_lds_*`, `buffer_load_* ... lds`) and
+  every instruction naming m0 as a source must follow an m0 write in its
+  own basic block (the inline-asm DMA wrappers set m0 themselves; a compiler
+  value of m0 live across one of them would be clobbered).
 
-The hazard probe (tools/hazard_probe.hip) measures on the hardware which of
-these distances are safe; this script lists where the compiled code comes
-close.  Output: one JSON line per (source, kind, instruction class) with the
-minimum distance seen and an example.
+    python tools/isa_mfma_audit.py                 # product library, JSON lines
+    python tools/isa_mfma_audit.py --lib other.so
+    python tools/isa_mfma_audit.py --asm file.s    # hipcc -save-temps output
 
-    python tools/isa_mfma_audit.py [--window 8] [sources ...]
+tests/test_isa_audit.py runs `audit_library` in the CPU suite.
 """
 from __future__ import annotations
 
 import argparse
 import collections
-import glob
 import json
 import os
 import re
+import struct
 import subprocess
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CSRC = os.path.join(ROOT, "avr_amd", "csrc")
-FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-ffp-contract=off", "-fno-gpu-rdc",
-         "-Wno-unused-function", "-Wno-inline-asm", "-I" + os.path.join(ROOT, "include")]
+LIB = os.path.join(ROOT, "avr_amd", "libavr_hip.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
 REG = re.compile(r"\bv\[(\d+):(\d+)\]|\bv(\d+)\b")
+BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+BAD_KIND = "WAR_after_mfma_B_behind_mfma"
 
 
 def regs(tok):
@@ -46,11 +55,10 @@ def regs(tok):
     return out
 
 
-def split_ops(line):
-    ins = line.split(None, 1)
+def split_ops(text):
+    ins = text.split(None, 1)
     if len(ins) == 1:
         return ins[0], []
-    # operands separated by commas outside brackets
     ops, depth, cur = [], 0, ""
     for ch in ins[1]:
         if ch == "[":
@@ -76,18 +84,24 @@ def states(op, ops):
     return 1
 
 
+def is_lds_dma(op, ops):
+    return op.startswith("global_load_lds") or (
+        op.startswith("buffer_load") and any("lds" in o.split() for o in ops))
+
+
 def writes(op, ops):
     """VGPRs the instruction writes (its first operand for VALU / loads)."""
     if not ops:
         return set()
     if op.startswith(("v_", "ds_read", "global_load", "buffer_load", "flat_load", "scratch_load")) \
-            and not op.startswith(("v_cmp", "v_readlane", "v_readfirstlane")) and "_lds" not in op:
+            and not op.startswith(("v_cmp", "v_readlane", "v_readfirstlane", "v_cmpx")) \
+            and not is_lds_dma(op, ops):
         return regs(ops[0])
     return set()
 
 
 def klass(op):
-    if op.startswith("v_mfma"):
+    if op.startswith("v_mfma") or op.startswith("v_smfmac"):
         return "mfma"
     if op.startswith("v_"):
         return "valu"
@@ -98,22 +112,39 @@ def klass(op):
     return "other"
 
 
-def audit_asm(path, window):
-    findings = collections.defaultdict(lambda: {"min_states": 1 << 30, "count": 0, "example": None})
-    kernel = None
-    block = []
+def _m0_write(op, ops):
+    return bool(ops) and ops[0] == "m0"
 
-    def flush():
+
+def _m0_read(op, ops):
+    return is_lds_dma(op, ops) or any(o == "m0" for o in ops[1:])
+
+
+def audit_blocks(blocks, window=8):
+    """blocks: iterable of (kernel, [(op, ops, text), ...]).  Returns
+    {(kernel, kind, writer_class): {"min_states", "count", "example"}}."""
+    findings = collections.defaultdict(lambda: {"min_states": 1 << 30, "count": 0, "example": None})
+
+    def note(key, dist, example):
+        f = findings[key]
+        f["count"] += 1
+        if dist < f["min_states"]:
+            f["min_states"] = dist
+            f["example"] = example
+
+    for kernel, block in blocks:
+        m0_set = False
         for i, (op, ops, line) in enumerate(block):
-            if not op.startswith("v_mfma") or len(ops) < 4:
+            if _m0_read(op, ops) and not m0_set:
+                note((kernel, "M0_read_without_write_in_block", klass(op)), 0, [line])
+            if _m0_write(op, ops):
+                m0_set = True
+            if klass(op) != "mfma" or len(ops) < 4:
                 continue
+            note((kernel, "MFMA_count", "mfma"), 0, [line])
             srcab = regs(ops[1]) | regs(ops[2])
             srcb = regs(ops[2])
-            # the MFMA issued right behind another one (the matrix pipe busy:
-            # it may wait to start while later instructions issue)
-            behind = i > 0 and block[i - 1][0].startswith("v_mfma")
-            # WAR: later writers of SrcA/B (SrcB separately: the bf16x3 DFT's
-            # stale bins were B-operand lanes, §14d)
+            behind = i > 0 and klass(block[i - 1][0]) == "mfma"
             dist = 0
             for op2, ops2, line2 in block[i + 1:]:
                 if dist >= window:
@@ -123,83 +154,155 @@ def audit_asm(path, window):
                     kind = "WAR_after_mfma_B" if w & srcb else "WAR_after_mfma_A"
                     if behind and kind.endswith("B"):
                         kind += "_behind_mfma"
-                    key = (kernel, kind, klass(op2))
-                    f = findings[key]
-                    f["count"] += 1
-                    if dist < f["min_states"]:
-                        f["min_states"] = dist
-                        f["example"] = [line.strip(), line2.strip()]
+                    note((kernel, kind, klass(op2)), dist, [line, line2])
                 dist += states(op2, ops2)
-            # RAW: earlier VALU writers of SrcA/B
             dist = 0
             for op2, ops2, line2 in reversed(block[:i]):
                 if dist >= window:
                     break
                 if klass(op2) == "valu" and writes(op2, ops2) & srcab:
-                    key = (kernel, "RAW_before_mfma", "valu")
-                    f = findings[key]
-                    f["count"] += 1
-                    if dist < f["min_states"]:
-                        f["min_states"] = dist
-                        f["example"] = [line2.strip(), line.strip()]
+                    note((kernel, "RAW_before_mfma", "valu"), dist, [line2, line])
                     break
                 dist += states(op2, ops2)
-        block.clear()
+    return findings
 
-    for raw in open(path):
-        line = raw.split(";")[0].rstrip()
-        if not line.strip():
+
+# ---------------------------------------------------------------- objdump
+_FUNC = re.compile(r"^[0-9a-f]+ <(.+)>:$")
+_TARGET = re.compile(r"<(.+)\+0x([0-9a-f]+)>\s*$")
+_ADDR = re.compile(r"//\s*([0-9A-Fa-f]+):")
+
+
+def _objdump_blocks(code_object):
+    """Basic blocks of every function of a disassembled gfx950 code object."""
+    txt = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--mcpu=gfx950", "--no-show-raw-insn",
+                          code_object], check=True, capture_output=True, text=True).stdout
+    funcs = []  # (name, base, [(addr, op, ops, text, target)])
+    for raw in txt.splitlines():
+        m = _FUNC.match(raw.strip())
+        if m:
+            funcs.append((m.group(1), None, []))
             continue
-        s = line.strip()
+        if not raw.startswith("\t") or not funcs:
+            continue
+        body, _, comment = raw.strip().partition("//")
+        body = body.strip()
+        if not body:
+            continue
+        am = _ADDR.search(raw)
+        addr = int(am.group(1), 16) if am else None
+        tm = _TARGET.search(comment)
+        target = (tm.group(1), int(tm.group(2), 16)) if tm else None
+        op, ops = split_ops(body)
+        name, base, ins = funcs[-1]
+        if base is None and addr is not None:
+            funcs[-1] = (name, addr, ins)
+        ins.append((addr, op, ops, body, target))
+    for name, base, ins in funcs:
+        starts = {off for (_a, op, _o, _t, tgt) in ins if tgt and tgt[0] == name and op.startswith("s_") and
+                  ("branch" in op) for off in [tgt[1]]}
+        block = []
+        for addr, op, ops, text, tgt in ins:
+            if base is not None and addr is not None and (addr - base) in starts and block:
+                yield name, block
+                block = []
+            block.append((op, ops, text))
+            if op.startswith(("s_cbranch", "s_branch", "s_setpc", "s_endpgm", "s_swappc")):
+                yield name, block
+                block = []
+        if block:
+            yield name, block
+
+
+def code_objects(lib, outdir):
+    """gfx950 code objects of the library's offload bundles, written to
+    outdir; returns their paths."""
+    fat = os.path.join(outdir, "fatbin.bin")
+    subprocess.run([os.path.join(LLVM, "llvm-objcopy"), "--dump-section", f".hip_fatbin={fat}", lib,
+                    os.path.join(outdir, "stripped.so")], check=True, capture_output=True)
+    data = open(fat, "rb").read()
+    paths, pos = [], 0
+    while True:
+        i = data.find(BUNDLE_MAGIC, pos)
+        if i < 0:
+            break
+        (n,) = struct.unpack_from("<Q", data, i + 24)
+        o = i + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", data, o)
+            o += 24
+            triple = data[o:o + tlen].decode()
+            o += tlen
+            if triple.endswith("gfx950"):
+                p = os.path.join(outdir, f"co{len(paths)}.o")
+                with open(p, "wb") as f:
+                    f.write(data[i + off:i + off + size])
+                paths.append(p)
+        pos = i + len(BUNDLE_MAGIC)
+    return paths
+
+
+def audit_library(lib=LIB, window=8):
+    """Findings over every kernel of the library (see audit_blocks)."""
+    with tempfile.TemporaryDirectory(prefix="avr_isa_") as tmp:
+        found = {}
+        for co in code_objects(lib, tmp):
+            found.update(audit_blocks(_objdump_blocks(co), window))
+        return found
+
+
+def _asm_blocks(path):
+    kernel, block = None, []
+    for raw in open(path):
+        s = raw.split(";")[0].strip()
+        if not s:
+            continue
         if s.endswith(":") and not s.startswith("."):
-            flush()
+            if block:
+                yield kernel, block
+            block = []
             if not s.startswith(".L"):
                 kernel = s[:-1]
             continue
-        if s.startswith(".") or s.startswith(";"):
-            if s.startswith(".LBB") or s.startswith(".Lfunc_end"):
-                flush()
+        if s.startswith("."):
+            if (s.startswith(".LBB") or s.startswith(".Lfunc_end")) and block:
+                yield kernel, block
+                block = []
             continue
         op, ops = split_ops(s)
         block.append((op, ops, s))
         if op.startswith(("s_cbranch", "s_branch", "s_setpc", "s_endpgm")):
-            flush()
-    flush()
-    return findings
+            yield kernel, block
+            block = []
+    if block:
+        yield kernel, block
+
+
+def _demangle(names):
+    try:
+        out = subprocess.run([os.path.join(LLVM, "llvm-cxxfilt")], input="\n".join(names), capture_output=True,
+                             text=True, check=True).stdout.splitlines()
+        return dict(zip(names, out))
+    except (OSError, subprocess.CalledProcessError):
+        return {n: n for n in names}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("sources", nargs="*")
+    ap.add_argument("--lib", default=LIB)
     ap.add_argument("--window", type=int, default=8)
     ap.add_argument("--asm", nargs="*", default=[], help="audit these assembly files instead")
     a = ap.parse_args()
-    for path in a.asm:
-        for (kern, kind, cls), f in sorted(audit_asm(path, a.window).items()):
-            print(json.dumps({"asm": os.path.basename(path), "kernel": kern[:60], "kind": kind, "writer": cls,
-                              "pairs": f["count"], "min_wait_states": f["min_states"], "example": f["example"]}))
     if a.asm:
-        return
-    srcs = a.sources or sorted(os.path.basename(p) for p in glob.glob(os.path.join(CSRC, "*.hip")))
-    tmp = tempfile.mkdtemp(prefix="avr_isa_")
-    for src in srcs:
-        subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, "--save-temps", "-c", os.path.join(CSRC, src), "-o",
-                        os.path.join(tmp, src + ".o")], cwd=tmp, check=True, capture_output=True)
-        asm = glob.glob(os.path.join(tmp, os.path.splitext(src)[0] + "-hip-amdgcn-amd-amdhsa-gfx950.s"))
-        if not asm:
-            continue
-        found = audit_asm(asm[0], a.window)
-        per = collections.defaultdict(lambda: {"min_states": 1 << 30, "count": 0, "example": None, "kernels": 0})
-        for (kern, kind, cls), f in found.items():
-            g = per[(kind, cls)]
-            g["count"] += f["count"]
-            g["kernels"] += 1
-            if f["min_states"] < g["min_states"]:
-                g["min_states"], g["example"] = f["min_states"], f["example"]
-        for (kind, cls), g in sorted(per.items()):
-            print(json.dumps({"source": src, "kind": kind, "writer": cls, "pairs": g["count"],
-                              "kernels": g["kernels"], "min_wait_states": g["min_states"],
-                              "example": g["example"]}), flush=True)
+        found = {}
+        for path in a.asm:
+            found.update(audit_blocks(_asm_blocks(path), a.window))
+    else:
+        found = audit_library(a.lib, a.window)
+    names = _demangle(sorted({k[0] for k in found}))
+    for (kern, kind, cls), f in sorted(found.items()):
+        print(json.dumps({"kernel": names.get(kern, kern)[:90], "kind": kind, "writer": cls, "pairs": f["count"],
+                          "min_wait_states": f["min_states"], "example": f["example"]}))
 
 
 if __name__ == "__main__":

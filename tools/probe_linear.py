@@ -50,7 +50,9 @@ def main():
     PROBE.avr_linear_relu_fwd.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p,
                                           ctypes.c_void_p]
-    _lib.call("avr_linear_pack_w", N, K, w.data_ptr(), code, wf.data_ptr(), st)
+    PROBE.avr_linear_pack_w.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                        ctypes.c_void_p, ctypes.c_void_p]
+    assert PROBE.avr_linear_pack_w(N, K, w.data_ptr(), code, wf.data_ptr(), st) == 0
 
     def ours():
         assert PROBE.avr_linear_relu_fwd(M, N, K, x.data_ptr(), wf.data_ptr(), code, 1, y.data_ptr(), st) == 0
