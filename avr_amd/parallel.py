@@ -98,17 +98,25 @@ class RayShardedRender(nn.Module):
 
     Wraps an `avr_amd.AVRRender`; `network_fn` is called only on this rank's
     rays.  Returns the full [B, F, 2] spectrum on every rank.
+
+    `shard=(rank, world)` (one process, no collective): render only that
+    shard's rays and return its partial spectrum -- one rank's work of a
+    world-rank job, measured on a single GPU (bench.py --shard-of).
     """
 
-    def __init__(self, renderer, group=None):
+    def __init__(self, renderer, group=None, shard=None):
         super().__init__()
         self.renderer = renderer
         self.group = group
+        self.shard = shard
 
     def forward(self, rays_o, position_tx, direction_tx=None, ch_idx=None):
         r = self.renderer
-        world = dist.get_world_size(self.group) if dist.is_initialized() else 1
-        rank = dist.get_rank(self.group) if dist.is_initialized() else 0
+        if self.shard is not None:
+            rank, world = self.shard
+        else:
+            world = dist.get_world_size(self.group) if dist.is_initialized() else 1
+            rank = dist.get_rank(self.group) if dist.is_initialized() else 0
         R = int(r.n_azi) * int(r.n_ele) + 2
         r.ray_range = shard_range(R, rank, world)
         try:
@@ -121,7 +129,7 @@ class RayShardedRender(nn.Module):
             partial = r._render(rays_o, position_tx, direction_tx, ch_idx, None, u_azi=u)
         finally:
             r.ray_range = None
-        if world == 1:
+        if world == 1 or self.shard is not None:
             return partial
         return allreduce_spectrum(partial, self.group)
 

@@ -74,7 +74,7 @@ def _native_adam_ok(optimizer):
     return True
 
 
-def clip_sanitize_adam_(optimizer, max_norm=1.0):
+def clip_sanitize_adam_(optimizer, max_norm=1.0, events=None):
     """clip_and_sanitize_ + optimizer.step() of a torch.optim.Adam
     (avr_runner.py:190-200) as one HIP pass per parameter (`avr_adam_step`):
     p, g, m, v read once, p, m, v written once.
@@ -84,7 +84,8 @@ def clip_sanitize_adam_(optimizer, max_norm=1.0):
     load_state_dict(), checkpoints and the LR scheduler are unchanged.  The
     clipped, sanitised gradient is consumed inside the kernel and not written
     back to p.grad (the loop zeroes it before the next backward).  Returns the
-    total norm (a device tensor).
+    total norm (a device tensor).  `events`: an optional (begin, end) pair of
+    torch.cuda.Event recorded around the Adam launches (bench.py's roofline).
     """
     params = [p for g in optimizer.param_groups for p in g["params"] if p.grad is not None]
     if not params:
@@ -92,6 +93,8 @@ def clip_sanitize_adam_(optimizer, max_norm=1.0):
     dev = params[0].device
     total, coef = _clip_coef([p.grad for p in params], max_norm)
     st_ = _stream(dev)
+    if events is not None and events[0] is not None:
+        events[0].record()
     for group in optimizer.param_groups:
         b1, b2 = group["betas"]
         lr = float(group["lr"])
@@ -131,6 +134,8 @@ def clip_sanitize_adam_(optimizer, max_norm=1.0):
                       arr(ctypes.c_void_p, ms), arr(ctypes.c_void_p, vs), arr(ctypes.c_int64, ns),
                       arr(ctypes.c_float, ss), arr(ctypes.c_float, bs), float(b1), float(b2),
                       float(group["eps"]), float(group["weight_decay"]), coef.data_ptr(), st_)
+    if events is not None and events[1] is not None:
+        events[1].record()
     return total
 
 
@@ -151,6 +156,9 @@ class TrainStep:
             eta_min=float(train_cfg['eta_min']), last_epoch=-1)
         self.nan_check = nan_check
         self.current_iteration = 0
+        # instrumentation: a callable returning the (begin, end) events to
+        # record around this step's Adam launches, or None (bench.py)
+        self.adam_events = None
 
     def __call__(self, ori_sig, position_rx, position_tx, direction_tx=None, ch_idx=None):
         dev = next(self.renderer.parameters()).device
@@ -168,7 +176,8 @@ class TrainStep:
         self.optimizer.zero_grad(set_to_none=True)
         total.backward()
         if self.native_adam:
-            clip_sanitize_adam_(self.optimizer, max_norm=1)
+            clip_sanitize_adam_(self.optimizer, max_norm=1,
+                                events=self.adam_events() if self.adam_events is not None else None)
             # the Adam update ran natively: tell the LR scheduler that this
             # step's optimizer.step() happened (its order check reads the flag)
             self.optimizer._opt_called = True

@@ -150,6 +150,9 @@ def parse_args(argv=None):
                     help="pose mode: HIP streams the independent per-pose renders are issued on "
                          "round-robin, each with its own signal buffer (1 = strictly serial; "
                          "on MI355X 2, 3 and 4 streams measure the same within 1%%)")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="ray-shard mode on one GPU: render rank 0's shard of an N-rank job (its rays only, "
+                         "no collective): the per-rank time an N-GPU run would see")
     ap.add_argument("--mlp-dtype", default="bf16", choices=["bf16", "fp16", "fp32"],
                     help="ddp-train mode: MLP compute dtype")
     ap.add_argument("--oversubscribe", action="store_true",
@@ -338,6 +341,33 @@ def head_roofline(w, timer):
         "live_fraction": live / (rows * T) if rows else 0.0,
         "avg_launch_ms": k_ms,
         "measured": "HIP events around each head launch on its stream, the timed steps",
+    }
+
+
+def adam_roofline(events, n_params):
+    """Roofline object for the training step's optimizer pass (avr_adam_step:
+    clipped, sanitised Adam over every fp32 parameter; p, g, m, v read, p, m,
+    v written: 28 algorithmic bytes per parameter) from HIP events around its
+    launches."""
+    if not events:
+        return None
+    ts = [a.elapsed_time(b) for a, b in events]
+    k_ms = sum(ts) / len(ts)
+    alg = 28.0 * n_params
+    achieved = alg / (k_ms * 1e-3) / 1e9
+    return {
+        "kernel": "adam_kernel",
+        "bound": "hbm",
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": None,
+        "alg_bytes_per_launch": alg,
+        "params": n_params,
+        "avg_launch_ms": k_ms,
+        "measured": "HIP events around the optimizer's Adam launches (one per step), a phase of K steps "
+                    "before the timed region",
     }
 
 
@@ -660,7 +690,10 @@ def bench_ray_shard(args, w, world, rank, dev):
 
     B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
     dt = torch.float16 if w.signal_dtype == "float16" else torch.float32
-    r0, r1 = shard_range(R, rank, world)
+    shard_of = args.shard_of if args.shard_of > 1 else 0
+    if shard_of and world != 1:
+        raise SystemExit("--shard-of measures one rank's shard on a single GPU (--gpus 1)")
+    r0, r1 = shard_range(R, rank, shard_of or world)
     Rl = r1 - r0
     if args.network:
         # the reference network of config 5 (avr_simu.yml), the same random
@@ -682,7 +715,7 @@ def bench_ray_shard(args, w, world, rank, dev):
     renderer = AVRRender(net, **w.render).to(dev)
     timer = KernelTimer(args.steps)
     renderer.kernel_timer = timer
-    sharded = RayShardedRender(renderer)
+    sharded = RayShardedRender(renderer, shard=(0, shard_of) if shard_of else None)
     pose = [0]
 
     def step():
@@ -704,7 +737,10 @@ def bench_ray_shard(args, w, world, rank, dev):
     torch.cuda.synchronize()
     timer.enabled = False
     elapsed, t_issue = timed(lambda: run(args.steps), world, dev)
-    value = whole_job_rate(w.ray_samples, 1, args.steps, elapsed)  # one pose per step, all ranks
+    if shard_of:  # this shard's ray-samples per second (one rank's rate)
+        value = whole_job_rate(B * Rl * S, 1, args.steps, elapsed)
+    else:
+        value = whole_job_rate(w.ray_samples, 1, args.steps, elapsed)  # one pose per step, all ranks
     res = _base_result(args, w, world, value, elapsed, "f32" if dt == torch.float32 else "f16-storage/f32-math")
     # with the network the fused head replaces the ray reduction: the head's
     # own events (FusedHeadCore, rounding-exact 16-bit head)
@@ -718,7 +754,10 @@ def bench_ray_shard(args, w, world, rank, dev):
         "host_issue_ms_per_step": t_issue * 1e3 / args.steps,
         "config": {"workload": w.name, "mode": "ray-shard", "rays": R, "rays_per_rank": Rl, "samples": S,
                    "T": T, "freq_bins": w.F, "poses_per_step": B,
-                   "parallelism": f"rays x{world}, one RCCL all-reduce of the [B,F,2] spectrum per pose",
+                   "parallelism": (f"rank 0's shard of a {shard_of}-rank ray split on one GPU, no collective "
+                                   f"(the per-rank work of --gpus {shard_of}; value = this shard's ray-samples/s)"
+                                   if shard_of else
+                                   f"rays x{world}, one RCCL all-reduce of the [B,F,2] spectrum per pose"),
                    "network": "AVRModel (avr_simu.yml)" if args.network else "stub (outputs resident in HBM)"},
         "roofline": rf,
     })
@@ -763,9 +802,18 @@ def bench_ddp_train(args, w, world, rank, dev):
     torch.manual_seed(rank)
     run(args.warmup)
     torch.cuda.synchronize()
+    # roofline phase: HIP events around the optimizer's Adam launches (the
+    # step's largest single kernel, HBM-bound), then the timed region
+    pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    used = []
+    ts.adam_events = lambda: used.append(pool[len(used)]) or used[-1] if len(used) < len(pool) else None
+    run(args.steps)
+    torch.cuda.synchronize()
+    ts.adam_events = None
     elapsed, t_issue = timed(lambda: run(args.steps), world, dev)
     value = whole_job_rate(w.ray_samples, world, args.steps, elapsed)
     n_params = sum(p.numel() for p in r.parameters())
+    n_trained = sum(p.numel() for p in r.parameters() if p.requires_grad)
     res = _base_result(args, w, world, value, elapsed, args.mlp_dtype + " MLP / f32 render")
     res.update({
         "data": "synthetic poses and decaying-noise target IRs; random-init AVRModel_complex (RAF widths)",
@@ -775,7 +823,7 @@ def bench_ddp_train(args, w, world, rank, dev):
                    "model": "AVRModel_complex (6 hash grids, RAF MLP widths)",
                    "params": n_params, "grad_allreduce_bytes": 4 * n_params if world > 1 else 0,
                    "parallelism": f"dp{world} (DDP, RCCL bucketed gradient all-reduce)"},
-        "roofline": None,
+        "roofline": adam_roofline(used, n_trained),
     })
     return res
 
