@@ -272,17 +272,20 @@ __device__ __forceinline__ void hold_operands(const frag8 (&x)[NT][KS]) {
 }
 
 // acc[nt][ot] = W X^T for one layer: KS k-steps of input fragments, OT output
-// tiles, CO tiles per LDS chunk.
-template <typename E, int NT, int KS, int OT, int CO, class ST>
+// tiles, CO tiles per LDS chunk.  ZERO = false: acc holds the start values
+// (the h1 layer's bias) and the products are accumulated onto them.
+template <typename E, int NT, int KS, int OT, int CO, class ST, bool ZERO = true>
 __device__ __forceinline__ void dense(ST& st, int lane,
                                       const frag8 (&x)[NT][KS], f32x16 (&acc)[NT][OT]) {
     static_assert(OT % CO == 0 && CO * KS * kFrag <= kChunk, "chunk overflow");
+    if constexpr (ZERO) {
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
+        for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-        for (int ot = 0; ot < OT; ++ot)
+            for (int ot = 0; ot < OT; ++ot)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) acc[nt][ot][i] = 0.0f;
+                for (int i = 0; i < 16; ++i) acc[nt][ot][i] = 0.0f;
+    }
 #pragma unroll
     for (int c = 0; c < OT / CO; ++c) {
         const char* lds = st.buffer();
@@ -482,15 +485,13 @@ void sigma_meshrir_kernel(Args a) {
     if constexpr (!(DBG & 4)) copy_extras<E, NT>(a, n0, lane);
 }
 
-// signal layer 1 epilogue (variant 2): h1[n][128c + o] = bf16(relu(acc + bias[n / bias_div][128c + o])).
-// The MFMA result has the sample on the lane, so written straight out every
-// store instruction would touch 32 rows x 16 B; instead each pair of tiles
-// (32 samples x 64 columns, 4 KB) goes through a per-wave LDS area (16-byte
-// chunks XOR-swizzled by row: conflict-free) and leaves as 4 instructions
-// of 8 rows x 128 contiguous bytes (full cache lines).
-template <typename E, int NT, bool STORE = true, bool BIAS = true>
-__device__ __forceinline__ void store_h1(const Args& a, const f32x16 (&acc)[NT][4], int64_t n0, int lane, int c,
-                                         char* tr) {
+// the h1 layer's accumulators start at the bias: acc[nt][ot] register 4g + e
+// = bias[n / bias_div][128 c + 32 ot + 8 g + 4 h + e] of the lane's sample n
+// (the per-ray / per-pose columns' part of the layer, summed before the
+// per-sample products instead of after them: one fp32 sum order of the
+// same terms, and 16 fewer VALU adds per tile)
+template <int NT>
+__device__ __forceinline__ void bias_acc(const Args& a, f32x16 (&acc)[NT][4], int64_t n0, int lane, int c) {
     const int h = lane >> 5, r = lane & 31;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
@@ -498,17 +499,39 @@ __device__ __forceinline__ void store_h1(const Args& a, const f32x16 (&acc)[NT][
         const int64_t nl = n < a.N ? n : a.N - 1;
         const float* brow = a.bias + (int64_t)((uint32_t)nl / (uint32_t)a.bias_div) * 512 + 128 * c;
 #pragma unroll
+        for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 b = *reinterpret_cast<const f32x4*>(brow + 32 * ot + 8 * g + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[nt][ot][4 * g + e] = b[e];
+            }
+    }
+}
+
+// signal layer 1 epilogue (variant 2): h1[n][128c + o] = bf16(relu(acc)), acc
+// started at bias[n / bias_div][128c + o] (bias_acc).
+// The MFMA result has the sample on the lane, so written straight out every
+// store instruction would touch 32 rows x 16 B; instead each pair of tiles
+// (32 samples x 64 columns, 4 KB) goes through a per-wave LDS area (16-byte
+// chunks XOR-swizzled by row: conflict-free) and leaves as 4 instructions
+// of 8 rows x 128 contiguous bytes (full cache lines).
+template <typename E, int NT, bool STORE = true>
+__device__ __forceinline__ void store_h1(const Args& a, const f32x16 (&acc)[NT][4], int64_t n0, int lane, int c,
+                                         char* tr) {
+    const int h = lane >> 5, r = lane & 31;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
         for (int p = 0; p < 2; ++p) {
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int ot = 2 * p + j;
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    const f32x4 b = BIAS ? *reinterpret_cast<const f32x4*>(brow + 32 * ot + 8 * g + 4 * h)
-                                         : f32x4{0.f, 0.f, 0.f, 0.f};
                     const f32x16& v = acc[nt][ot];
-                    const uint32_t w0 = pack2<E>(relu(v[4 * g] + b[0]), relu(v[4 * g + 1] + b[1]));
-                    const uint32_t w1 = pack2<E>(relu(v[4 * g + 2] + b[2]), relu(v[4 * g + 3] + b[3]));
+                    const uint32_t w0 = pack2<E>(relu(v[4 * g]), relu(v[4 * g + 1]));
+                    const uint32_t w1 = pack2<E>(relu(v[4 * g + 2]), relu(v[4 * g + 3]));
                     const int ch = (4 * j + g) ^ (r & 7);  // 16-B chunk of the 128-B row
                     *reinterpret_cast<u32x2v*>(tr + r * 128 + ch * 16 + 8 * h) = u32x2v{w0, w1};
                 }
@@ -593,8 +616,9 @@ void sigma_meshrir_h1_kernel(Args a) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         f32x16 acc[NT][4];
-        dense<E, NT, 8, 4, 4>(st, lane, xs, acc);
-        store_h1<E, NT, !(DBG & 4), !(DBG & 8)>(a, acc, n0, lane, c, lds + 2 * kChunk + wave * 4096);
+        bias_acc<NT>(a, acc, n0, lane, c);
+        dense<E, NT, 8, 4, 4, decltype(st), false>(st, lane, xs, acc);
+        store_h1<E, NT, !(DBG & 4)>(a, acc, n0, lane, c, lds + 2 * kChunk + wave * 4096);
         if constexpr ((DBG & 64) != 0) st.issue_deferred();
     }
 }
@@ -767,7 +791,6 @@ int dispatch(const avr_sigma_desc* d, Args& a, bool h1, bool two, hipStream_t st
             if (d->tile_cfg == 17) return launch_meshrir_h1<E, 1, 4, 2, 2>(a, st);
             if (d->tile_cfg == 18) return launch_meshrir_h1<E, 1, 4, 2, 4>(a, st);
             if (d->tile_cfg == 19) return launch_meshrir_h1<E, 1, 4, 2, 7>(a, st);
-            if (d->tile_cfg == 20) return launch_meshrir_h1<E, 1, 4, 2, 8>(a, st);  // no bias loads
         }
 #endif
         if (d->tile_cfg == 8) return launch_meshrir_h1<E, 1, 4, 2>(a, st);  // register-staged weights

@@ -59,8 +59,24 @@ def test_argument_errors_are_reported_without_gpu(lib):
 
 
 def test_code_object_targets_gfx950(lib):
-    blob = open(_lib.LIB_PATH, "rb").read()
-    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in blob
+    """Every HIP translation unit's (compressed) offload bundle holds a gfx950
+    code object (unbundled for that target by clang-offload-bundler)."""
+    import sys
+    import tempfile
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_mfma_audit
+
+    if not os.path.exists(os.path.join(isa_mfma_audit.LLVM, "clang-offload-bundler")):
+        pytest.skip("needs ROCm's clang-offload-bundler")
+    hips = [f for f in os.listdir(os.path.join(ROOT, "avr_amd", "csrc")) if f.endswith(".hip")]
+    srcs = open(os.path.join(ROOT, "avr_amd", "csrc", "Makefile")).read().split("SRCS    :=")[1].split("\n")[0]
+    shipped = [f for f in hips if f in srcs.split()]
+    with tempfile.TemporaryDirectory() as tmp:
+        cos = isa_mfma_audit.code_objects(_lib.LIB_PATH, tmp)
+        assert len(cos) == len(shipped), (len(cos), shipped)
+        for co in cos:
+            assert open(co, "rb").read(4) == b"\x7fELF"
 
 
 def test_only_validated_knobs_read_the_environment():

@@ -1,5 +1,6 @@
-"""Interleaved timing of exact-head item shapes at config 2 (16-bit h,
-K = 512) with the shape-probe library (`make -C avr_amd/csrc shapes`,
+"""Interleaved timing of exact-head item shapes (16-bit h, K = 512; config 2
+by default, --workload for others, --shard-of N for one rank's ray shard)
+with the shape-probe library (`make -C avr_amd/csrc shapes`,
 csrc/probe.h): the kernel alone, HIP events around each launch of the full
 fused render, rounds interleaved so clock drift hits every shape alike.
 
@@ -39,10 +40,15 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--dtype", default="fp16")
+    ap.add_argument("--workload", default="c2_meshrir_1024x256x512")
+    ap.add_argument("--shard-of", type=int, default=1, help="render rank 0's ray shard of an N-rank split")
     args = ap.parse_args()
     dtype = torch.float16 if args.dtype == "fp16" else torch.bfloat16
-    w = WORKLOADS["c2_meshrir_1024x256x512"]
+    w = WORKLOADS[args.workload]
     B, R, S, T, K = w.batch, w.n_rays, w.n_samples, w.T, 512
+    from avr_amd.parallel import shard_range
+    r0, r1 = shard_range(R, 0, max(1, args.shard_of))
+    R = r1 - r0
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(19)
     ro = torch.rand(B, 3, device=dev, generator=g) * 4 - 2
@@ -51,6 +57,8 @@ def main():
     h = torch.relu(torch.randn(B, R * S, K, device=dev, generator=g)).to(dtype)
     W = torch.randn(T, K, device=dev, generator=g) / K ** 0.5
     r = AVRRender(None, **w.render)
+    if args.shard_of > 1:
+        r.ray_range = (r0, r1)
     torch.manual_seed(5)
     _, _, _, _, geom = r.sample(ro, tx)
     shapes = args.shapes.split(",")

@@ -215,17 +215,33 @@ def _objdump_blocks(code_object):
 
 
 def code_objects(lib, outdir):
-    """gfx950 code objects of the library's offload bundles, written to
-    outdir; returns their paths."""
+    """gfx950 code objects of the library's offload bundles (one per
+    translation unit, each 4096-byte aligned in .hip_fatbin; compressed
+    'CCOB' bundles, hipcc --offload-compress, are unpacked by
+    clang-offload-bundler), written to outdir; returns their paths."""
     fat = os.path.join(outdir, "fatbin.bin")
     subprocess.run([os.path.join(LLVM, "llvm-objcopy"), "--dump-section", f".hip_fatbin={fat}", lib,
                     os.path.join(outdir, "stripped.so")], check=True, capture_output=True)
     data = open(fat, "rb").read()
-    paths, pos = [], 0
-    while True:
-        i = data.find(BUNDLE_MAGIC, pos)
-        if i < 0:
-            break
+    starts = [i for i in range(0, len(data), 4096)
+              if data[i:i + 4] == b"CCOB" or data[i:i + len(BUNDLE_MAGIC)] == BUNDLE_MAGIC]
+    paths = []
+    for k, i in enumerate(starts):
+        end = starts[k + 1] if k + 1 < len(starts) else len(data)
+        out = os.path.join(outdir, f"co{len(paths)}.o")
+        if data[i:i + 4] == b"CCOB":
+            # header: magic, version (u16), method (u16), then the bundle's
+            # total size (u32 in version 2, u64 from version 3)
+            (ver,) = struct.unpack_from("<H", data, i + 4)
+            (total,) = struct.unpack_from("<Q" if ver >= 3 else "<I", data, i + 8)
+            blob = os.path.join(outdir, f"bundle{k}.bin")
+            with open(blob, "wb") as f:
+                f.write(data[i:min(end, i + total)])
+            subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--type=o", "--unbundle",
+                            f"--input={blob}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={out}"],
+                           check=True, capture_output=True)
+            paths.append(out)
+            continue
         (n,) = struct.unpack_from("<Q", data, i + 24)
         o = i + 32
         for _ in range(n):
@@ -234,11 +250,9 @@ def code_objects(lib, outdir):
             triple = data[o:o + tlen].decode()
             o += tlen
             if triple.endswith("gfx950"):
-                p = os.path.join(outdir, f"co{len(paths)}.o")
-                with open(p, "wb") as f:
+                with open(out, "wb") as f:
                     f.write(data[i + off:i + off + size])
-                paths.append(p)
-        pos = i + len(BUNDLE_MAGIC)
+                paths.append(out)
     return paths
 
 
