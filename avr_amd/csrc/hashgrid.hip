@@ -430,15 +430,20 @@ int launch_fwd_lm(dim3 grid, hipStream_t st, int64_t N, const float* x, const vo
 //               (kPartEntries consecutive entries of one level) in LDS;
 //   2. scan:    one wave per partition turns its per-chunk counts into
 //               offsets and a total;
-//   3. scatter: the same walk writes each contribution (entry within the
-//               partition, value pair) into its partition's segment of a
-//               workspace (key and value arrays; partition-contiguous,
-//               chunk-ordered segments, slot order within a chunk free);
-//   4. reduce:  one block per partition sums its contributions into a 64 KB
-//               LDS image of the partition (LDS float atomics) and adds the
-//               image to the gradient with plain vector loads/stores (the
-//               block owns those entries: no other writer).
-// The workspace holds N * L * 8 contributions at most (12 B each).
+//   3. scatter: the same walk writes each contribution into its partition's
+//               segment of a workspace (partition-contiguous, chunk-ordered
+//               segments, slot order within a chunk free) as ONE 4-byte
+//               record: the run it merges (first point, length <= 16) and
+//               the corner (run_record), not its key and values;
+//   4. reduce:  one wave per partition slice recomputes each record's key
+//               and value pair from the run's points and upstream gradients
+//               (the walk's own arithmetic, in its order: the same fp32
+//               values bit for bit), sums them into an LDS image of the
+//               partition and adds the image to the gradient with plain
+//               vector loads/stores (the wave owns those entries).
+// The workspace holds N * L * 8 records at most (4 B each; 12-byte (key, v0,
+// v1) records until round 6: a third of the scatter's stores and the
+// reduce's loads, for a re-read of x and the gradient that L2 serves).
 constexpr int kPartBits = 10;
 constexpr int kPartEntries = 1 << kPartBits;      // 1024 entries = 8 KB of fp32 pairs (one wave's image)
 constexpr int kBwdGroups = 32;                    // 8-lane groups per 256-thread block
@@ -446,6 +451,13 @@ constexpr int kBwdRun = 16;                       // consecutive points walked p
 constexpr int kChunkPts = kBwdGroups * kBwdRun;   // 512 points per block and level
 constexpr int kReduceWaves = 4;                   // reduce block: one partition slice per wave
 constexpr int kMaxScatterParts = 4096;            // partitions per level the count/scatter LDS holds
+
+// A contribution's record: its run's first point (25 bits), run length - 1
+// (4 bits: kBwdRun <= 16) and corner (3 bits)
+static_assert(kBwdRun <= 16, "run length field");
+__device__ __forceinline__ uint32_t run_record(int64_t first, int len, int k) {
+    return ((uint32_t)first << 7) | ((uint32_t)(len - 1) << 3) | (uint32_t)k;
+}
 
 struct BwdPlan {
     int pbase[kMaxLevels + 1];  // first partition of each level (prefix of ceil(size / kPartEntries))
@@ -457,7 +469,9 @@ struct BwdPlan {
 
 // The walk shared by the count and scatter passes: lane k of 8-lane group g
 // owns corner k of the group's kBwdRun consecutive points (both features);
-// emit(entry, v0, v1) is called for every merged contribution, in walk order.
+// emit(entry, v0, v1, run) is called for every merged contribution, in walk
+// order, with run = its record (run_record: points first .. first + len - 1
+// of the walk, corner k).
 template <typename Tg, class Emit>
 __device__ __forceinline__ void bwd_walk(int64_t N, int L, int l, const float* __restrict__ x,
                                          const Tg* __restrict__ gout, const LevelTable& lt, Emit&& emit) {
@@ -480,6 +494,7 @@ __device__ __forceinline__ void bwd_walk(int64_t N, int L, int l, const float* _
     }
     uint32_t pe = 0xffffffffu;
     float p0 = 0.0f, p1 = 0.0f;
+    int r0 = 0;  // first point of the pending run
 #pragma unroll
     for (int it = 0; it < kBwdRun; ++it) {
         const Corner c = locate(xi[it], scale);
@@ -501,13 +516,62 @@ __device__ __forceinline__ void bwd_walk(int64_t N, int L, int l, const float* _
             p0 += v0;
             p1 += v1;
         } else {
-            if (pe != 0xffffffffu && (p0 != 0.0f || p1 != 0.0f)) emit(pe, p0, p1);
+            if (pe != 0xffffffffu && (p0 != 0.0f || p1 != 0.0f)) emit(pe, p0, p1, run_record(first + r0, it - r0, k));
             pe = e;
             p0 = v0;
             p1 = v1;
+            r0 = it;
         }
     }
-    if (pe != 0xffffffffu && (p0 != 0.0f || p1 != 0.0f)) emit(pe, p0, p1);
+    if (pe != 0xffffffffu && (p0 != 0.0f || p1 != 0.0f)) emit(pe, p0, p1, run_record(first + r0, kBwdRun - r0, k));
+}
+
+// The reduce pass's side of a record: the key (entry within the partition)
+// and the value pair of the run, recomputed from the run's points and
+// upstream gradients with the walk's arithmetic in the walk's order.
+template <typename Tg>
+__device__ __forceinline__ void run_value(uint32_t rec, int64_t N, int L, int l, const float* __restrict__ x,
+                                          const Tg* __restrict__ gout, uint32_t size, uint32_t res, float scale,
+                                          uint32_t& key, float& s0, float& s1) {
+    const int64_t pt = rec >> 7;
+    const int len = (int)((rec >> 3) & 15) + 1, k = (int)(rec & 7);
+    uint32_t e = 0;
+    s0 = 0.0f;
+    s1 = 0.0f;
+    for (int m = 0; m < len; ++m) {
+        const int64_t i = pt + m;
+        const bool live = i < N;
+        const int64_t ic = live ? i : N - 1;
+        float xi[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) xi[d] = x[ic * 3 + d];
+        const int64_t gi = ic * (2 * L) + 2 * l;
+        const float g0 = live ? load_f(gout, gi) : 0.0f;
+        const float g1 = live ? load_f(gout, gi + 1) : 0.0f;
+        const Corner c = locate(xi, scale);
+        float wgt = 1.0f;
+        uint32_t gg[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            if (k & (1 << d)) {
+                wgt *= c.pos[d];
+                gg[d] = c.grid[d] + 1;
+            } else {
+                wgt *= 1.0f - c.pos[d];
+                gg[d] = c.grid[d];
+            }
+        }
+        e = grid_index(size, res, gg[0], gg[1], gg[2]);
+        const float v0 = wgt * g0, v1 = wgt * g1;
+        if (m == 0) {
+            s0 = v0;
+            s1 = v1;
+        } else {
+            s0 += v0;
+            s1 += v1;
+        }
+    }
+    key = e & (kPartEntries - 1);
 }
 
 template <typename Tg>
@@ -519,7 +583,8 @@ __global__ __launch_bounds__(256) void hg_bwd_count_kernel(int64_t N, int L, con
     const int P = plan.pbase[l + 1] - plan.pbase[l];
     for (int p = threadIdx.x; p < P; p += 256) cnt_l[p] = 0;
     __syncthreads();
-    bwd_walk(N, L, l, x, gout, lt, [&](uint32_t e, float, float) { atomicAdd(&cnt_l[e >> kPartBits], 1); });
+    bwd_walk(N, L, l, x, gout, lt,
+             [&](uint32_t e, float, float, uint32_t) { atomicAdd(&cnt_l[e >> kPartBits], 1); });
     __syncthreads();
     for (int p = threadIdx.x; p < P; p += 256)
         counts[(int64_t)(plan.pbase[l] + p) * plan.nchunks + blockIdx.x] = cnt_l[p];
@@ -623,7 +688,7 @@ __global__ __launch_bounds__(256) void hg_bwd_scatter_kernel(int64_t N, int L, c
                                                              const Tg* __restrict__ gout, LevelTable lt,
                                                              BwdPlan plan, const int* __restrict__ offs,
                                                              const int* __restrict__ part_start,
-                                                             uint3* __restrict__ contrib) {
+                                                             uint32_t* __restrict__ contrib) {
     extern __shared__ int scat_l[];  // base[P], slot[P]
     const int l = blockIdx.y;
     const int pb = plan.pbase[l];
@@ -635,11 +700,10 @@ __global__ __launch_bounds__(256) void hg_bwd_scatter_kernel(int64_t N, int L, c
         slot[q] = 0;
     }
     __syncthreads();
-    bwd_walk(N, L, l, x, gout, lt, [&](uint32_t e, float v0, float v1) {
+    bwd_walk(N, L, l, x, gout, lt, [&](uint32_t e, float, float, uint32_t rec) {
         const int part = (int)(e >> kPartBits);
         const int pos = base[part] + atomicAdd(&slot[part], 1);
-        // one 12-byte store per contribution: (key, v0, v1)
-        contrib[pos] = make_uint3(e & (kPartEntries - 1), __float_as_uint(v0), __float_as_uint(v1));
+        contrib[pos] = rec;  // one 4-byte store per contribution
     });
 }
 
@@ -668,12 +732,14 @@ __device__ __forceinline__ float wave_total(float x) {
 // the others are summed per key across the wave and added once per key.
 // Keys repeat within one wave-load only where many rays cross the same
 // cells (coarse levels), so the tag round alone is the rule.
-__global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L, LevelTable lt, BwdPlan plan,
-                                                                         int total_parts,
+template <typename Tg>
+__global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int64_t N, int L, const float* __restrict__ x,
+                                                                         const Tg* __restrict__ gout, LevelTable lt,
+                                                                         BwdPlan plan, int total_parts,
                                                                          const int* __restrict__ totals,
                                                                          const int* __restrict__ part_start,
                                                                          const int* __restrict__ slice_base,
-                                                                         const uint3* __restrict__ contrib,
+                                                                         const uint32_t* __restrict__ contrib,
                                                                          float* __restrict__ gparams, int overwrite) {
     __shared__ float2 img_all[kReduceWaves][kPartEntries];
     __shared__ uint8_t tag_all[kReduceWaves][kPartEntries];
@@ -708,16 +774,25 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int L,
     const int i0 = part_start[p] + (int)((int64_t)n * sl / ns);
     const int i1 = part_start[p] + (int)((int64_t)n * (sl + 1) / ns);
     for (int i = lane; i < ne; i += 64) img[i] = make_float2(0.f, 0.f);
+    const uint32_t size = (uint32_t)(lt.offset[l + 1] - lt.offset[l]);
+    const uint32_t res = lt.res[l];
+    const float scale = lt.scale[l];
     constexpr int U = 8;
     for (int i = i0; i < i1; i += 64 * U) {
-        uint32_t kk[U];
+        uint32_t kk[U], rc[U];
         float2 v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int j = i + 64 * u + lane;
-            const uint3 cv = contrib[j < i1 ? j : i0];
-            kk[u] = j < i1 ? cv.x : 0u;
-            v[u] = j < i1 ? make_float2(__uint_as_float(cv.y), __uint_as_float(cv.z)) : make_float2(0.f, 0.f);
+            rc[u] = contrib[j < i1 ? j : i0];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = i + 64 * u + lane;
+            float s0, s1;
+            run_value(rc[u], N, L, l, x, gout, size, res, scale, kk[u], s0, s1);
+            if (j >= i1) kk[u] = 0u;
+            v[u] = j < i1 ? make_float2(s0, s1) : make_float2(0.f, 0.f);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -846,9 +921,10 @@ int bwd_layout(int64_t N, int L, const int64_t* off, const int32_t* res, BwdLayo
     b.slice_base = o0;
     o0 += al((int64_t)(b.total_parts + 1) * 4);
     b.max_slices = b.total_parts + (int)(maxc / kDenseSlice) + 1;
-    b.scatter_ok = b.plan.max_parts <= kMaxScatterParts;
-    b.contrib = o0;  // (key, v0, v1) per contribution
-    o0 += al(maxc * 12);
+    // records hold the run's first point in 25 bits
+    b.scatter_ok = b.plan.max_parts <= kMaxScatterParts && N <= (int64_t(1) << 25);
+    b.contrib = o0;  // one 4-byte record per contribution (run_record)
+    o0 += al(maxc * 4);
     b.bytes = o0;
     // the workspace comes from the caller's allocator on every backward: past
     // this size the atomic kernel runs instead (no workspace, same += result)
@@ -1235,7 +1311,7 @@ int bwd_partitioned(int64_t N, int32_t n_levels, const float* x, const void* gra
     char* ws = static_cast<char*>(workspace);
     int* counts = reinterpret_cast<int*>(ws + b.counts);
     int* totals = reinterpret_cast<int*>(ws + b.totals);
-    uint3* contrib = reinterpret_cast<uint3*>(ws + b.contrib);
+    uint32_t* contrib = reinterpret_cast<uint32_t*>(ws + b.contrib);
     const dim3 grid((unsigned)b.plan.nchunks, (unsigned)L);
     const size_t lds_count = (size_t)b.plan.max_parts * 4, lds_scat = (size_t)b.plan.max_parts * 8;
     if (grad_dtype == AVR_DTYPE_F32)
@@ -1259,9 +1335,15 @@ int bwd_partitioned(int64_t N, int32_t n_levels, const float* x, const void* gra
     if (overwrite)
         hipLaunchKernelGGL(hg_bwd_zero_hot_kernel, dim3((unsigned)b.total_parts), dim3(256), 0, st, lt, b.plan,
                            b.total_parts, slice_base, grad_params);
-    hipLaunchKernelGGL(hg_bwd_reduce_kernel, dim3((unsigned)((b.max_slices + kReduceWaves - 1) / kReduceWaves)),
-                       dim3(64 * kReduceWaves), 0, st, L, lt, b.plan, b.total_parts, totals, part_start, slice_base,
-                       contrib, grad_params, (int)overwrite);
+    const dim3 rgrid((unsigned)((b.max_slices + kReduceWaves - 1) / kReduceWaves));
+    if (grad_dtype == AVR_DTYPE_F32)
+        hipLaunchKernelGGL(hg_bwd_reduce_kernel<float>, rgrid, dim3(64 * kReduceWaves), 0, st, N, L, x,
+                           (const float*)grad_out, lt, b.plan, b.total_parts, totals, part_start, slice_base,
+                           contrib, grad_params, (int)overwrite);
+    else
+        hipLaunchKernelGGL(hg_bwd_reduce_kernel<__half>, rgrid, dim3(64 * kReduceWaves), 0, st, N, L, x,
+                           (const __half*)grad_out, lt, b.plan, b.total_parts, totals, part_start, slice_base,
+                           contrib, grad_params, (int)overwrite);
     return check_launch("avr_hashgrid_bwd_partitioned");
 }
 }  // namespace
