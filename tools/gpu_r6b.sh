@@ -18,6 +18,10 @@ if [ "${TESTS:-}" != "" ]; then
   step tests 600 python -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread -W ignore
   tail -2 $OUT/tests.log
 fi
+step sigma 300 env AVR_AB_LIB=avr_amd/libavr_hip.so python tools/probe_sigma.py --variant 2 --dtype fp16 --cfgs 0,1,3,6,7,8,0
+cat $OUT/sigma.log | grep "^{"
+step sigma0 300 env AVR_AB_LIB=avr_amd/libavr_hip.so python tools/probe_sigma.py --variant 0 --dtype fp16 --cfgs 0,1,2,3,0
+cat $OUT/sigma0.log | grep "^{"
 step c5shard 500 rocprofv3 --kernel-trace --stats -d $OUT/c5shard -o run --output-format csv -- python bench.py --mode ray-shard --network --mlp-dtype fp16 --shard-of 8 --steps 10 --warmup 2 --no-cpu-baseline
 grep "^{" $OUT/c5shard.log | tail -1 > $OUT/c5shard.json
 step ddp 500 python bench.py --mode ddp-train --steps 20 --warmup 5
