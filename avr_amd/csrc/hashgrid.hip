@@ -467,6 +467,42 @@ struct BwdPlan {
     int hot_above[kMaxLevels];  // ... and kDenseSlice for partitions holding more than this (hot cells)
 };
 
+// One point's contribution to corner k (the walk's arithmetic): the entry
+// and the value pair w_k * g.
+__device__ __forceinline__ void corner_value(const float (&xi)[3], float g0, float g1, int k, float scale,
+                                             uint32_t size, uint32_t res, uint32_t& e, float& v0, float& v1) {
+    const Corner c = locate(xi, scale);
+    float wgt = 1.0f;
+    uint32_t gg[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        if (k & (1 << d)) {
+            wgt *= c.pos[d];
+            gg[d] = c.grid[d] + 1;
+        } else {
+            wgt *= 1.0f - c.pos[d];
+            gg[d] = c.grid[d];
+        }
+    }
+    e = grid_index(size, res, gg[0], gg[1], gg[2]);
+    v0 = wgt * g0;
+    v1 = wgt * g1;
+}
+
+// point i's coordinates and level-l gradient pair (zero past N; the walk's
+// clamped loads)
+template <typename Tg>
+__device__ __forceinline__ void point_inputs(int64_t i, int64_t N, int L, int l, const float* __restrict__ x,
+                                             const Tg* __restrict__ gout, float (&xi)[3], float& g0, float& g1) {
+    const bool live = i < N;
+    const int64_t ic = live ? i : N - 1;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) xi[d] = x[ic * 3 + d];
+    const int64_t gi = ic * (2 * L) + 2 * l;
+    g0 = live ? load_f(gout, gi) : 0.0f;
+    g1 = live ? load_f(gout, gi + 1) : 0.0f;
+}
+
 // The walk shared by the count and scatter passes: lane k of 8-lane group g
 // owns corner k of the group's kBwdRun consecutive points (both features);
 // emit(entry, v0, v1, run) is called for every merged contribution, in walk
@@ -497,21 +533,9 @@ __device__ __forceinline__ void bwd_walk(int64_t N, int L, int l, const float* _
     int r0 = 0;  // first point of the pending run
 #pragma unroll
     for (int it = 0; it < kBwdRun; ++it) {
-        const Corner c = locate(xi[it], scale);
-        float wgt = 1.0f;
-        uint32_t gg[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            if (k & (1 << d)) {
-                wgt *= c.pos[d];
-                gg[d] = c.grid[d] + 1;
-            } else {
-                wgt *= 1.0f - c.pos[d];
-                gg[d] = c.grid[d];
-            }
-        }
-        const uint32_t e = grid_index(size, res, gg[0], gg[1], gg[2]);
-        const float v0 = wgt * g0[it], v1 = wgt * g1[it];
+        uint32_t e;
+        float v0, v1;
+        corner_value(xi[it], g0[it], g1[it], k, scale, size, res, e, v0, v1);
         if (e == pe) {
             p0 += v0;
             p1 += v1;
@@ -524,54 +548,6 @@ __device__ __forceinline__ void bwd_walk(int64_t N, int L, int l, const float* _
         }
     }
     if (pe != 0xffffffffu && (p0 != 0.0f || p1 != 0.0f)) emit(pe, p0, p1, run_record(first + r0, kBwdRun - r0, k));
-}
-
-// The reduce pass's side of a record: the key (entry within the partition)
-// and the value pair of the run, recomputed from the run's points and
-// upstream gradients with the walk's arithmetic in the walk's order.
-template <typename Tg>
-__device__ __forceinline__ void run_value(uint32_t rec, int64_t N, int L, int l, const float* __restrict__ x,
-                                          const Tg* __restrict__ gout, uint32_t size, uint32_t res, float scale,
-                                          uint32_t& key, float& s0, float& s1) {
-    const int64_t pt = rec >> 7;
-    const int len = (int)((rec >> 3) & 15) + 1, k = (int)(rec & 7);
-    uint32_t e = 0;
-    s0 = 0.0f;
-    s1 = 0.0f;
-    for (int m = 0; m < len; ++m) {
-        const int64_t i = pt + m;
-        const bool live = i < N;
-        const int64_t ic = live ? i : N - 1;
-        float xi[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) xi[d] = x[ic * 3 + d];
-        const int64_t gi = ic * (2 * L) + 2 * l;
-        const float g0 = live ? load_f(gout, gi) : 0.0f;
-        const float g1 = live ? load_f(gout, gi + 1) : 0.0f;
-        const Corner c = locate(xi, scale);
-        float wgt = 1.0f;
-        uint32_t gg[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            if (k & (1 << d)) {
-                wgt *= c.pos[d];
-                gg[d] = c.grid[d] + 1;
-            } else {
-                wgt *= 1.0f - c.pos[d];
-                gg[d] = c.grid[d];
-            }
-        }
-        e = grid_index(size, res, gg[0], gg[1], gg[2]);
-        const float v0 = wgt * g0, v1 = wgt * g1;
-        if (m == 0) {
-            s0 = v0;
-            s1 = v1;
-        } else {
-            s0 += v0;
-            s1 += v1;
-        }
-    }
-    key = e & (kPartEntries - 1);
 }
 
 template <typename Tg>
@@ -786,12 +762,27 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int64_
             const int j = i + 64 * u + lane;
             rc[u] = contrib[j < i1 ? j : i0];
         }
+        // each record's run recomputed with the walk's arithmetic in the
+        // walk's order: the first points of all U records loaded together
+        // (most runs are one point long), then the rest of each run
+        float xs[U][3], ga[U], gb[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) point_inputs(rc[u] >> 7, N, L, l, x, gout, xs[u], ga[u], gb[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int j = i + 64 * u + lane;
+            const int k = (int)(rc[u] & 7), len = (int)((rc[u] >> 3) & 15) + 1;
+            uint32_t e;
             float s0, s1;
-            run_value(rc[u], N, L, l, x, gout, size, res, scale, kk[u], s0, s1);
-            if (j >= i1) kk[u] = 0u;
+            corner_value(xs[u], ga[u], gb[u], k, scale, size, res, e, s0, s1);
+            for (int m = 1; m < len; ++m) {
+                float xi[3], g0, g1, v0, v1;
+                point_inputs((int64_t)(rc[u] >> 7) + m, N, L, l, x, gout, xi, g0, g1);
+                corner_value(xi, g0, g1, k, scale, size, res, e, v0, v1);
+                s0 += v0;
+                s1 += v1;
+            }
+            const int j = i + 64 * u + lane;
+            kk[u] = j < i1 ? (e & (kPartEntries - 1)) : 0u;
             v[u] = j < i1 ? make_float2(s0, s1) : make_float2(0.f, 0.f);
         }
 #pragma unroll

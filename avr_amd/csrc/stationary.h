@@ -21,8 +21,12 @@ typedef uint32_t frag8_t __attribute__((ext_vector_type(4)));
 // One 16-byte-per-lane LDS-DMA load: lane i's 16 bytes at g land at LDS byte
 // address lds + 16 i (inline asm: the compiler does not treat the DMA as an
 // LDS write that later ds_reads wait for; completion is waited by vmcnt).
+// The rows are read once per launch (a work item's rows belong to it alone):
+// non-temporal (nt), so they stream past L2 instead of evicting what the
+// workgroups re-read from it (the exact head's W tiles, 4 MiB at config 5 =
+// one XCD's L2; MI355X_MICROARCH.md "nt-weights": once-read bytes).
 __device__ __forceinline__ void stat_dma16(const void* g, uint32_t lds) {
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds), "v"(g)
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt" ::"s"(lds), "v"(g)
                  : "memory", "m0");
 }
 
