@@ -430,20 +430,17 @@ int launch_fwd_lm(dim3 grid, hipStream_t st, int64_t N, const float* x, const vo
 //               (kPartEntries consecutive entries of one level) in LDS;
 //   2. scan:    one wave per partition turns its per-chunk counts into
 //               offsets and a total;
-//   3. scatter: the same walk writes each contribution into its partition's
-//               segment of a workspace (partition-contiguous, chunk-ordered
-//               segments, slot order within a chunk free) as ONE 4-byte
-//               record: the run it merges (first point, length <= 16) and
-//               the corner (run_record), not its key and values;
-//   4. reduce:  one wave per partition slice recomputes each record's key
-//               and value pair from the run's points and upstream gradients
-//               (the walk's own arithmetic, in its order: the same fp32
-//               values bit for bit), sums them into an LDS image of the
-//               partition and adds the image to the gradient with plain
-//               vector loads/stores (the wave owns those entries).
-// The workspace holds N * L * 8 records at most (4 B each; 12-byte (key, v0,
-// v1) records until round 6: a third of the scatter's stores and the
-// reduce's loads, for a re-read of x and the gradient that L2 serves).
+//   3. scatter: the same walk writes each contribution (entry within the
+//               partition, value pair) into its partition's segment of a
+//               workspace (partition-contiguous, chunk-ordered segments,
+//               slot order within a chunk free);
+//   4. reduce:  one wave per partition slice sums its contributions into
+//               an LDS image of the partition and adds the image to the
+//               gradient with plain vector loads/stores (the wave owns those
+//               entries).
+// The workspace holds N * L * 8 contributions at most (12 B each).  Both
+// walks read the upstream gradient level-major (glm, transposed by its own
+// pass first).
 constexpr int kPartBits = 10;
 constexpr int kPartEntries = 1 << kPartBits;      // 1024 entries = 8 KB of fp32 pairs (one wave's image)
 constexpr int kBwdGroups = 32;                    // 8-lane groups per 256-thread block
@@ -451,13 +448,6 @@ constexpr int kBwdRun = 16;                       // consecutive points walked p
 constexpr int kChunkPts = kBwdGroups * kBwdRun;   // 512 points per block and level
 constexpr int kReduceWaves = 4;                   // reduce block: one partition slice per wave
 constexpr int kMaxScatterParts = 4096;            // partitions per level the count/scatter LDS holds
-
-// A contribution's record: its run's first point (25 bits), run length - 1
-// (4 bits: kBwdRun <= 16) and corner (3 bits)
-static_assert(kBwdRun <= 16, "run length field");
-__device__ __forceinline__ uint32_t run_record(int64_t first, int len, int k) {
-    return ((uint32_t)first << 7) | ((uint32_t)(len - 1) << 3) | (uint32_t)k;
-}
 
 struct BwdPlan {
     int pbase[kMaxLevels + 1];  // first partition of each level (prefix of ceil(size / kPartEntries))
@@ -489,25 +479,46 @@ __device__ __forceinline__ void corner_value(const float (&xi)[3], float g0, flo
     v1 = wgt * g1;
 }
 
+// The count and scatter walks read the upstream gradient level-major, glm
+// [L][N][2] (hg_level_major_kernel): a block's 512 points of one level are
+// 4 KiB of consecutive pairs instead of one 8-byte pair in every 160-byte
+// row of grad_out [N][L][2] (a cache line per point and level, twice).
+__device__ __forceinline__ int64_t glm_index(int64_t i, int64_t N, int l) { return ((int64_t)l * N + i) * 2; }
+
 // point i's coordinates and level-l gradient pair (zero past N; the walk's
 // clamped loads)
 template <typename Tg>
 __device__ __forceinline__ void point_inputs(int64_t i, int64_t N, int L, int l, const float* __restrict__ x,
-                                             const Tg* __restrict__ gout, float (&xi)[3], float& g0, float& g1) {
+                                             const Tg* __restrict__ glm, float (&xi)[3], float& g0, float& g1) {
     const bool live = i < N;
     const int64_t ic = live ? i : N - 1;
 #pragma unroll
     for (int d = 0; d < 3; ++d) xi[d] = x[ic * 3 + d];
-    const int64_t gi = ic * (2 * L) + 2 * l;
-    g0 = live ? load_f(gout, gi) : 0.0f;
-    g1 = live ? load_f(gout, gi + 1) : 0.0f;
+    const int64_t gi = glm_index(ic, N, l);
+    g0 = live ? load_f(glm, gi) : 0.0f;
+    g1 = live ? load_f(glm, gi + 1) : 0.0f;
+}
+
+// grad_out [N][L][2] -> glm [L][N][2], 64 points per block through LDS
+template <typename Tg>
+__global__ __launch_bounds__(256) void hg_level_major_kernel(int64_t N, int L, const Tg* __restrict__ in,
+                                                             Tg* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) char lm_s[];
+    Tg* t = reinterpret_cast<Tg*>(lm_s);  // [64][2L]
+    const int64_t i0 = (int64_t)blockIdx.x * 64;
+    const int np = (int)min((int64_t)64, N - i0);
+    const int W = 2 * L;
+    for (int j = threadIdx.x; j < np * W; j += 256) t[j] = in[i0 * W + j];
+    __syncthreads();
+    for (int j = threadIdx.x; j < L * np * 2; j += 256) {
+        const int l = j / (np * 2), r = j - l * (np * 2);
+        out[((int64_t)l * N + i0) * 2 + r] = t[(r >> 1) * W + 2 * l + (r & 1)];
+    }
 }
 
 // The walk shared by the count and scatter passes: lane k of 8-lane group g
 // owns corner k of the group's kBwdRun consecutive points (both features);
-// emit(entry, v0, v1, run) is called for every merged contribution, in walk
-// order, with run = its record (run_record: points first .. first + len - 1
-// of the walk, corner k).
+// emit(entry, v0, v1) is called for every merged contribution, in walk order.
 template <typename Tg, class Emit>
 __device__ __forceinline__ void bwd_walk(int64_t N, int L, int l, const float* __restrict__ x,
                                          const Tg* __restrict__ gout, const LevelTable& lt, Emit&& emit) {
@@ -518,19 +529,9 @@ __device__ __forceinline__ void bwd_walk(int64_t N, int L, int l, const float* _
     const float scale = lt.scale[l];
     float xi[kBwdRun][3], g0[kBwdRun], g1[kBwdRun];
 #pragma unroll
-    for (int it = 0; it < kBwdRun; ++it) {
-        const int64_t i = first + it;
-        const bool live = i < N;
-        const int64_t ic = live ? i : N - 1;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) xi[it][d] = x[ic * 3 + d];
-        const int64_t gi = ic * (2 * L) + 2 * l;
-        g0[it] = live ? load_f(gout, gi) : 0.0f;
-        g1[it] = live ? load_f(gout, gi + 1) : 0.0f;
-    }
+    for (int it = 0; it < kBwdRun; ++it) point_inputs(first + it, N, L, l, x, gout, xi[it], g0[it], g1[it]);
     uint32_t pe = 0xffffffffu;
     float p0 = 0.0f, p1 = 0.0f;
-    int r0 = 0;  // first point of the pending run
 #pragma unroll
     for (int it = 0; it < kBwdRun; ++it) {
         uint32_t e;
@@ -540,14 +541,13 @@ __device__ __forceinline__ void bwd_walk(int64_t N, int L, int l, const float* _
             p0 += v0;
             p1 += v1;
         } else {
-            if (pe != 0xffffffffu && (p0 != 0.0f || p1 != 0.0f)) emit(pe, p0, p1, run_record(first + r0, it - r0, k));
+            if (pe != 0xffffffffu && (p0 != 0.0f || p1 != 0.0f)) emit(pe, p0, p1);
             pe = e;
             p0 = v0;
             p1 = v1;
-            r0 = it;
         }
     }
-    if (pe != 0xffffffffu && (p0 != 0.0f || p1 != 0.0f)) emit(pe, p0, p1, run_record(first + r0, kBwdRun - r0, k));
+    if (pe != 0xffffffffu && (p0 != 0.0f || p1 != 0.0f)) emit(pe, p0, p1);
 }
 
 template <typename Tg>
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(256) void hg_bwd_count_kernel(int64_t N, int L, con
     for (int p = threadIdx.x; p < P; p += 256) cnt_l[p] = 0;
     __syncthreads();
     bwd_walk(N, L, l, x, gout, lt,
-             [&](uint32_t e, float, float, uint32_t) { atomicAdd(&cnt_l[e >> kPartBits], 1); });
+             [&](uint32_t e, float, float) { atomicAdd(&cnt_l[e >> kPartBits], 1); });
     __syncthreads();
     for (int p = threadIdx.x; p < P; p += 256)
         counts[(int64_t)(plan.pbase[l] + p) * plan.nchunks + blockIdx.x] = cnt_l[p];
@@ -664,7 +664,7 @@ __global__ __launch_bounds__(256) void hg_bwd_scatter_kernel(int64_t N, int L, c
                                                              const Tg* __restrict__ gout, LevelTable lt,
                                                              BwdPlan plan, const int* __restrict__ offs,
                                                              const int* __restrict__ part_start,
-                                                             uint32_t* __restrict__ contrib) {
+                                                             uint3* __restrict__ contrib) {
     extern __shared__ int scat_l[];  // base[P], slot[P]
     const int l = blockIdx.y;
     const int pb = plan.pbase[l];
@@ -676,10 +676,11 @@ __global__ __launch_bounds__(256) void hg_bwd_scatter_kernel(int64_t N, int L, c
         slot[q] = 0;
     }
     __syncthreads();
-    bwd_walk(N, L, l, x, gout, lt, [&](uint32_t e, float, float, uint32_t rec) {
+    bwd_walk(N, L, l, x, gout, lt, [&](uint32_t e, float v0, float v1) {
         const int part = (int)(e >> kPartBits);
         const int pos = base[part] + atomicAdd(&slot[part], 1);
-        contrib[pos] = rec;  // one 4-byte store per contribution
+        // one 12-byte store per contribution: (key, v0, v1)
+        contrib[pos] = make_uint3(e & (kPartEntries - 1), __float_as_uint(v0), __float_as_uint(v1));
     });
 }
 
@@ -708,14 +709,11 @@ __device__ __forceinline__ float wave_total(float x) {
 // the others are summed per key across the wave and added once per key.
 // Keys repeat within one wave-load only where many rays cross the same
 // cells (coarse levels), so the tag round alone is the rule.
-template <typename Tg>
-__global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int64_t N, int L, const float* __restrict__ x,
-                                                                         const Tg* __restrict__ gout, LevelTable lt,
-                                                                         BwdPlan plan, int total_parts,
+__global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(LevelTable lt, BwdPlan plan, int total_parts,
                                                                          const int* __restrict__ totals,
                                                                          const int* __restrict__ part_start,
                                                                          const int* __restrict__ slice_base,
-                                                                         const uint32_t* __restrict__ contrib,
+                                                                         const uint3* __restrict__ contrib,
                                                                          float* __restrict__ gparams, int overwrite) {
     __shared__ float2 img_all[kReduceWaves][kPartEntries];
     __shared__ uint8_t tag_all[kReduceWaves][kPartEntries];
@@ -750,40 +748,16 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(int64_
     const int i0 = part_start[p] + (int)((int64_t)n * sl / ns);
     const int i1 = part_start[p] + (int)((int64_t)n * (sl + 1) / ns);
     for (int i = lane; i < ne; i += 64) img[i] = make_float2(0.f, 0.f);
-    const uint32_t size = (uint32_t)(lt.offset[l + 1] - lt.offset[l]);
-    const uint32_t res = lt.res[l];
-    const float scale = lt.scale[l];
     constexpr int U = 8;
     for (int i = i0; i < i1; i += 64 * U) {
-        uint32_t kk[U], rc[U];
+        uint32_t kk[U];
         float2 v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int j = i + 64 * u + lane;
-            rc[u] = contrib[j < i1 ? j : i0];
-        }
-        // each record's run recomputed with the walk's arithmetic in the
-        // walk's order: the first points of all U records loaded together
-        // (most runs are one point long), then the rest of each run
-        float xs[U][3], ga[U], gb[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) point_inputs(rc[u] >> 7, N, L, l, x, gout, xs[u], ga[u], gb[u]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int k = (int)(rc[u] & 7), len = (int)((rc[u] >> 3) & 15) + 1;
-            uint32_t e;
-            float s0, s1;
-            corner_value(xs[u], ga[u], gb[u], k, scale, size, res, e, s0, s1);
-            for (int m = 1; m < len; ++m) {
-                float xi[3], g0, g1, v0, v1;
-                point_inputs((int64_t)(rc[u] >> 7) + m, N, L, l, x, gout, xi, g0, g1);
-                corner_value(xi, g0, g1, k, scale, size, res, e, v0, v1);
-                s0 += v0;
-                s1 += v1;
-            }
-            const int j = i + 64 * u + lane;
-            kk[u] = j < i1 ? (e & (kPartEntries - 1)) : 0u;
-            v[u] = j < i1 ? make_float2(s0, s1) : make_float2(0.f, 0.f);
+            const uint3 cv = contrib[j < i1 ? j : i0];
+            kk[u] = j < i1 ? cv.x : 0u;
+            v[u] = j < i1 ? make_float2(__uint_as_float(cv.y), __uint_as_float(cv.z)) : make_float2(0.f, 0.f);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -867,7 +841,7 @@ constexpr int64_t kMaxBwdWorkspaceBytes = int64_t(1) << 31;  // 2 GiB (config 4:
 struct BwdLayout {
     BwdPlan plan;
     int total_parts;
-    int64_t counts, totals, part_start, slice_base, contrib, bytes;  // byte offsets in the workspace
+    int64_t counts, totals, part_start, slice_base, glm, contrib, bytes;  // byte offsets in the workspace
     int max_slices;  // reduce grid: total_parts + maxc / kDenseSlice bounds the slice count
     bool scatter_ok; // the largest level's partition table fits the count/scatter LDS
 };
@@ -912,10 +886,11 @@ int bwd_layout(int64_t N, int L, const int64_t* off, const int32_t* res, BwdLayo
     b.slice_base = o0;
     o0 += al((int64_t)(b.total_parts + 1) * 4);
     b.max_slices = b.total_parts + (int)(maxc / kDenseSlice) + 1;
-    // records hold the run's first point in 25 bits
-    b.scatter_ok = b.plan.max_parts <= kMaxScatterParts && N <= (int64_t(1) << 25);
-    b.contrib = o0;  // one 4-byte record per contribution (run_record)
-    o0 += al(maxc * 4);
+    b.scatter_ok = b.plan.max_parts <= kMaxScatterParts;
+    b.glm = o0;  // the upstream gradient level-major (fp32 or fp16: sized for fp32)
+    o0 += al(N * L * 2 * 4);
+    b.contrib = o0;  // (key, v0, v1) per contribution
+    o0 += al(maxc * 12);
     b.bytes = o0;
     // the workspace comes from the caller's allocator on every backward: past
     // this size the atomic kernel runs instead (no workspace, same += result)
@@ -1302,9 +1277,19 @@ int bwd_partitioned(int64_t N, int32_t n_levels, const float* x, const void* gra
     char* ws = static_cast<char*>(workspace);
     int* counts = reinterpret_cast<int*>(ws + b.counts);
     int* totals = reinterpret_cast<int*>(ws + b.totals);
-    uint32_t* contrib = reinterpret_cast<uint32_t*>(ws + b.contrib);
+    uint3* contrib = reinterpret_cast<uint3*>(ws + b.contrib);
     const dim3 grid((unsigned)b.plan.nchunks, (unsigned)L);
     const size_t lds_count = (size_t)b.plan.max_parts * 4, lds_scat = (size_t)b.plan.max_parts * 8;
+    // every pass below reads the gradient level-major
+    const dim3 tgrid((unsigned)((N + 63) / 64));
+    void* glm = ws + b.glm;
+    if (grad_dtype == AVR_DTYPE_F32)
+        hipLaunchKernelGGL(hg_level_major_kernel<float>, tgrid, dim3(256), 64 * 2 * L * 4, st, N, L,
+                           (const float*)grad_out, (float*)glm);
+    else
+        hipLaunchKernelGGL(hg_level_major_kernel<__half>, tgrid, dim3(256), 64 * 2 * L * 2, st, N, L,
+                           (const __half*)grad_out, (__half*)glm);
+    grad_out = glm;
     if (grad_dtype == AVR_DTYPE_F32)
         hipLaunchKernelGGL(hg_bwd_count_kernel<float>, grid, dim3(256), lds_count, st, N, L, x,
                            (const float*)grad_out, lt, b.plan, counts);
@@ -1326,15 +1311,9 @@ int bwd_partitioned(int64_t N, int32_t n_levels, const float* x, const void* gra
     if (overwrite)
         hipLaunchKernelGGL(hg_bwd_zero_hot_kernel, dim3((unsigned)b.total_parts), dim3(256), 0, st, lt, b.plan,
                            b.total_parts, slice_base, grad_params);
-    const dim3 rgrid((unsigned)((b.max_slices + kReduceWaves - 1) / kReduceWaves));
-    if (grad_dtype == AVR_DTYPE_F32)
-        hipLaunchKernelGGL(hg_bwd_reduce_kernel<float>, rgrid, dim3(64 * kReduceWaves), 0, st, N, L, x,
-                           (const float*)grad_out, lt, b.plan, b.total_parts, totals, part_start, slice_base,
-                           contrib, grad_params, (int)overwrite);
-    else
-        hipLaunchKernelGGL(hg_bwd_reduce_kernel<__half>, rgrid, dim3(64 * kReduceWaves), 0, st, N, L, x,
-                           (const __half*)grad_out, lt, b.plan, b.total_parts, totals, part_start, slice_base,
-                           contrib, grad_params, (int)overwrite);
+    hipLaunchKernelGGL(hg_bwd_reduce_kernel, dim3((unsigned)((b.max_slices + kReduceWaves - 1) / kReduceWaves)),
+                       dim3(64 * kReduceWaves), 0, st, lt, b.plan, b.total_parts, totals, part_start, slice_base,
+                       contrib, grad_params, (int)overwrite);
     return check_launch("avr_hashgrid_bwd_partitioned");
 }
 }  // namespace
