@@ -797,13 +797,16 @@ int dispatch(const avr_sigma_desc* d, Args& a, bool h1, bool two, hipStream_t st
         return launch_meshrir_h1<E, 1, 4, 2, 96>(a, st);  // LDS-DMA staging, h1 DMAs after the epilogue
     }
     const int cfg = d->tile_cfg;
-    // tile configs (tools/probe_sigma.py, MI355X at config 2): MeshRIR
-    // 0 = 64 samples per wave, 4 waves, 2 waves/SIMD (72 us); 1 = 32 per
-    // wave, 8 waves (80 us); 2 = 32 per wave, 4 waves at 2 waves/SIMD; 3 = 64 per wave, 4
-    // waves, 1 wave/SIMD.  RAF: 0 = 4 waves (120 us), 1 = 8 waves (137 us).
+    // tile configs (tools/probe_sigma.py, MI355X at config 2, fp16;
+    // profiles/r06_sigma_tilings.jsonl): MeshRIR 0 = 32 samples per wave, 4
+    // waves at 2 waves/SIMD (73.7 us, no scratch); 1 = 32 per wave, 8 waves
+    // (75.4 us); 2 = 64 per wave, 4 waves, 2 waves/SIMD (80.3 us: 68 bytes of
+    // scratch per lane once the layer's B operands are held, §15a; the default
+    // until round 5); 3 = 64 per wave, 4 waves, 1 wave/SIMD (92.7 us).
+    // RAF: 0 = 4 waves (120 us), 1 = 8 waves (137 us).
     if (two) return cfg == 1 ? launch_raf<E, 8, 1>(a, st) : launch_raf<E, 4, 2>(a, st);
     if (cfg == 1) return launch_meshrir<E, 1, 8, 1>(a, st);
-    if (cfg == 2) return launch_meshrir<E, 1, 4, 2>(a, st);
+    if (cfg == 2) return launch_meshrir<E, 2, 4, 2>(a, st);
     if (cfg == 3) return launch_meshrir<E, 2, 4, 1>(a, st);
 #if defined(AVR_PHASE_PROBES) || defined(AVR_SHAPE_PROBES)
     if constexpr (std::is_same<E, __bf16>::value) {  // timing experiments, garbage results
@@ -814,7 +817,7 @@ int dispatch(const avr_sigma_desc* d, Args& a, bool h1, bool two, hipStream_t st
         if (cfg == 20) return launch_meshrir<E, 1, 8, 1, 7>(a, st);
     }
 #endif
-    return launch_meshrir<E, 2, 4, 2>(a, st);
+    return launch_meshrir<E, 1, 4, 2>(a, st);
 }
 }  // namespace
 
