@@ -164,6 +164,8 @@ _SIGS = {
     "avr_das_fwd": (ctypes.c_int, [_c_i32] + [_vp] * 5 + [_c_f32] * 3 + [_vp, _vp, _c_i64, _vp]),
     "avr_das_bwd": (ctypes.c_int, [_c_i32] + [_vp] * 3 + [_c_f32] * 3 + [_vp, _vp, _c_i64, _vp, _vp]),
     "avr_scale_sanitize": (ctypes.c_int, [_c_i32, _vp, _vp, _vp, _vp]),
+    "avr_grad_clip_workspace": (ctypes.c_int, [_c_i32, _vp, _vp]),
+    "avr_grad_clip_coef": (ctypes.c_int, [_c_i32, _vp, _vp, ctypes.c_float, _vp, ctypes.c_int64, _vp, _vp, _vp]),
     "avr_adam_step": (ctypes.c_int, [_c_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double,
                                      ctypes.c_float, ctypes.c_float, _vp, _vp]),
     "avr_concat_fwd": (ctypes.c_int, [_c_i64, _c_i32, _vp, _vp, _c_i32, _vp]),

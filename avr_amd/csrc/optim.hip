@@ -5,8 +5,9 @@
 //   for p in params: p.grad[p.grad != p.grad] = 0           # NaN -> 0
 //                    p.grad[torch.isinf(p.grad)] = 0        # +-Inf -> 0
 //
-// The caller computes the clamped clip coefficient on the device (torch's
-// own foreach norm), so there is no host sync; this kernel applies
+// The clamped clip coefficient stays on the device (no host sync): torch's
+// own foreach norm (clip_and_sanitize_), or avr_grad_clip_coef below (the
+// fused Adam path); scale_sanitize_kernel applies
 // g = finite(g * coef) ? g * coef : 0 to every gradient tensor.  It replaces
 // clip_grad_norm_'s foreach multiply and the reference's 4-6 launches per
 // parameter tensor.
@@ -48,7 +49,115 @@ __global__ __launch_bounds__(256) void scale_sanitize_kernel(TensorTable tab,
     }
 }
 
+// ----------------------------------------------------------------------------
+// clip_grad_norm_'s total norm and coefficient in two launches (one read of
+// every gradient): blocks of the first write one partial sum of squares each
+// to a fixed slot, the second sums the slots in a fixed order, so the result
+// is the same on every run.  fp32 throughout, as torch's foreach norm; a NaN
+// or Inf gradient element makes the total NaN / Inf exactly as there.
+constexpr int kNormBlocks = 256;  // partial sums per tensor at most
+constexpr int kNormThreads = 256;
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    float t = 0.0f;
+    if (threadIdx.x == 0)
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+    return t;
+}
+
+struct NormTable {
+    const float* ptr[kMaxTensors];
+    int64_t n[kMaxTensors];
+    int64_t slot[kMaxTensors];  // first partial-sum slot of the tensor
+};
+
+__global__ __launch_bounds__(kNormThreads) void grad_sumsq_kernel(NormTable tab, float* __restrict__ part) {
+    __shared__ float red[kNormThreads / 64];
+    const int t = blockIdx.y;
+    const int64_t n = tab.n[t];
+    const float* __restrict__ g = tab.ptr[t];
+    const int64_t nb = (n + 4 * kNormThreads - 1) / (4 * kNormThreads) < kNormBlocks
+                           ? (n + 4 * kNormThreads - 1) / (4 * kNormThreads) : kNormBlocks;
+    if (blockIdx.x >= nb) return;  // (the grid is sized for the largest tensor)
+    const int64_t n4 = ((reinterpret_cast<uintptr_t>(g) & 15) == 0) ? n / 4 : 0;
+    const int64_t stride = nb * kNormThreads;
+    float acc = 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * kNormThreads + threadIdx.x; i < n4; i += stride) {
+        // (plain loads: the gradients stay in the caches for the Adam pass next)
+        const f32x4 v = reinterpret_cast<const f32x4*>(g)[i];
+        acc += v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    }
+    for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * kNormThreads + threadIdx.x; i < n; i += stride)
+        acc += g[i] * g[i];
+    const float s = block_sum(acc, red);
+    if (threadIdx.x == 0) part[tab.slot[t] + blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(1024) void clip_coef_kernel(const float* __restrict__ part, int64_t n_part, float max_norm,
+                                                         float* __restrict__ total, float* __restrict__ coef) {
+    __shared__ float red[16];
+    float acc = 0.0f;
+    for (int64_t i = threadIdx.x; i < n_part; i += blockDim.x) acc += part[i];
+    const float s = block_sum(acc, red);
+    if (threadIdx.x == 0) {
+        const float tn = sqrtf(s);
+        const float c = max_norm / (tn + 1e-6f);  // torch: max_norm / (total + 1e-6), clamped at 1
+        *total = tn;
+        *coef = c > 1.0f ? 1.0f : c;  // a NaN stays NaN (torch.clamp), so every gradient is zeroed
+    }
+}
+
+int64_t norm_blocks(int64_t n) {
+    const int64_t b = (n + 4 * kNormThreads - 1) / (4 * kNormThreads);
+    return b < kNormBlocks ? b : kNormBlocks;
+}
+
 }  // namespace
+
+extern "C" int avr_grad_clip_workspace(int32_t n_tensors, const int64_t* sizes, int64_t* bytes) {
+    AVR_REQUIRE(n_tensors >= 0 && bytes && (n_tensors == 0 || sizes), "avr_grad_clip_workspace: bad args");
+    int64_t slots = 1;
+    for (int i = 0; i < n_tensors; ++i) {
+        AVR_REQUIRE(sizes[i] >= 0, "avr_grad_clip_workspace: negative size");
+        slots += norm_blocks(sizes[i]);
+    }
+    *bytes = slots * (int64_t)sizeof(float);  // one partial sum of squares per block
+    return 0;
+}
+
+extern "C" int avr_grad_clip_coef(int32_t n_tensors, const float* const* ptrs, const int64_t* sizes, float max_norm,
+                                  void* workspace, int64_t workspace_bytes, float* total, float* coef,
+                                  void* stream) {
+    AVR_REQUIRE(n_tensors >= 0 && total && coef && workspace && (n_tensors == 0 || (ptrs && sizes)),
+                "avr_grad_clip_coef: bad args");
+    int64_t need = 0;
+    if (int e = avr_grad_clip_workspace(n_tensors, sizes, &need)) return e;
+    AVR_REQUIRE(workspace_bytes >= need, "avr_grad_clip_coef: workspace too small (avr_grad_clip_workspace)");
+    hipStream_t st = as_stream(stream);
+    float* part = static_cast<float*>(workspace);
+    int64_t n_part = 0;
+    for (int base = 0; base < n_tensors; base += kMaxTensors) {
+        NormTable tab{};
+        const int cnt = n_tensors - base < kMaxTensors ? n_tensors - base : kMaxTensors;
+        int64_t blocks = 1;
+        for (int i = 0; i < cnt; ++i) {
+            AVR_REQUIRE(ptrs[base + i] || sizes[base + i] == 0, "avr_grad_clip_coef: null tensor");
+            tab.ptr[i] = ptrs[base + i];
+            tab.n[i] = sizes[base + i];
+            tab.slot[i] = n_part;
+            n_part += norm_blocks(sizes[base + i]);
+            if (norm_blocks(sizes[base + i]) > blocks) blocks = norm_blocks(sizes[base + i]);
+        }
+        hipLaunchKernelGGL(grad_sumsq_kernel, dim3((unsigned)blocks, cnt), dim3(kNormThreads), 0, st, tab, part);
+        if (int e = check_launch("avr_grad_clip_coef")) return e;
+    }
+    hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1024), 0, st, part, n_part, max_norm, total, coef);
+    return check_launch("avr_grad_clip_coef");
+}
 
 extern "C" int avr_scale_sanitize(int32_t n_tensors, float* const* ptrs, const int64_t* sizes,
                                   const float* coef, void* stream) {

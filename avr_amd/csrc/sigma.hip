@@ -557,10 +557,14 @@ __device__ __forceinline__ void store_h1(const Args& a, const f32x16 (&acc)[NT][
 }
 
 // Variant 2 (AVRModel, sigma networks + the signal network's first layer):
-// as variant 0, then h1 = relu(W1[:, :128] sigma_feat + bias[ray]) with the
-// per-ray / per-pose columns of the layer (dir_enc, tx_enc) folded into
-// `bias` on the host, written as [N][512] bf16 in place of the
-// concatenated input.  12 chunks.
+// the sigma encoder, then h1 = relu(W1[:, :128] sigma_feat + bias[ray]) with
+// the per-ray / per-pose columns of the layer (dir_enc, tx_enc) folded into
+// `bias` on the host, written as [N][512] bf16 in place of the concatenated
+// input, then the decoder on relu(sigma_feat).  12 chunks, in that order
+// (sigma.py STREAM_ORDER): the h1 layer runs while bf16(sigma_feat) is the
+// only live activation, and the decoder's input is rectified from it in
+// place, so one copy of the features is held instead of two (32 VGPRs per
+// 32-sample tile).
 template <typename E, int NT, int WAVES, int OCC, int DBG = 0>
 __global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(OCC)))
 void sigma_meshrir_h1_kernel(Args a) {
@@ -569,6 +573,7 @@ void sigma_meshrir_h1_kernel(Args a) {
     const int64_t n0 = ((int64_t)blockIdx.x * WAVES + wave) * 32 * NT;
     Stager<WAVES, DBG & 99> st;
     st.start(a.wpack, lds, 12);
+    using ST = decltype(st);
 
     frag8 x0[NT][3];
     load_input<E, NT, 3>(a, n0, lane, x0);
@@ -584,8 +589,8 @@ void sigma_meshrir_h1_kernel(Args a) {
         dense<E, NT, 8, 4, 4>(st, lane, x, acc);
         to_frags<E, NT, 4>(acc, x);
     }
-    frag8 xs[NT][8];  // bf16(sigma_feat): the signal network's per-sample input
     {
+        // x <- bf16(sigma_feat) (linear): the signal network's per-sample input
         f32x16 acc[NT][4];
         dense<E, NT, 8, 4, 4>(st, lane, x, acc);
 #pragma unroll
@@ -594,10 +599,29 @@ void sigma_meshrir_h1_kernel(Args a) {
             for (int ot = 0; ot < 4; ++ot) {
                 uint32_t d[8];
                 pack_tile<E>(acc[nt][ot], d);
-                tile_frags(d, false, xs[nt][2 * ot], xs[nt][2 * ot + 1]);
-                tile_frags(d, true, x[nt][2 * ot], x[nt][2 * ot + 1]);
+                tile_frags(d, false, x[nt][2 * ot], x[nt][2 * ot + 1]);
             }
     }
+    // DBG & 64 (with the DMA stager): each h1 chunk's weight DMA is issued
+    // after the previous chunk's epilogue, whose bias loads would otherwise
+    // wait for it (vmcnt counts in order)
+    if constexpr ((DBG & 64) != 0) st.defer = true;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        f32x16 acc[NT][4];
+        bias_acc<NT>(a, acc, n0, lane, c);
+        dense<E, NT, 8, 4, 4, ST, false>(st, lane, x, acc);
+        store_h1<E, NT, !(DBG & 4)>(a, acc, n0, lane, c, lds + 2 * kChunk + wave * 4096);
+        if constexpr ((DBG & 64) != 0) st.issue_deferred();
+    }
+    st.defer = false;
+    // the decoder's input: relu(sigma_feat), rectified in the 16-bit format
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) x[nt][k][q] = relu16x2(x[nt][k][q]);
 #pragma unroll
     for (int l = 0; l < 3; ++l) {
         f32x16 acc[NT][4];
@@ -608,18 +632,6 @@ void sigma_meshrir_h1_kernel(Args a) {
         f32x16 acc[NT][1];
         dense<E, NT, 8, 1, 1>(st, lane, x, acc);
         store_attn<E, NT>(a, acc, n0, lane);
-    }
-    // DBG & 64 (with the DMA stager): each h1 chunk's weight DMA is issued
-    // after the previous chunk's epilogue, whose bias loads would otherwise
-    // wait for it (vmcnt counts in order)
-    if constexpr ((DBG & 64) != 0) st.defer = true;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        f32x16 acc[NT][4];
-        bias_acc<NT>(a, acc, n0, lane, c);
-        dense<E, NT, 8, 4, 4, decltype(st), false>(st, lane, xs, acc);
-        store_h1<E, NT, !(DBG & 4)>(a, acc, n0, lane, c, lds + 2 * kChunk + wave * 4096);
-        if constexpr ((DBG & 64) != 0) st.issue_deferred();
     }
 }
 

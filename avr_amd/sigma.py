@@ -39,6 +39,10 @@ SCHEDULE = {
           (128, 256, False, 2), (1, 128, False, 1)],
 }
 SCHEDULE[MESHRIR_H1] = SCHEDULE[MESHRIR] + [(512, 128, False, 4)]
+# the order the kernel streams the layers in, where it is not SCHEDULE's:
+# MESHRIR_H1 runs the signal layer (8) right after the encoder (0-3), then
+# the decoder (4-7) on the rectified features (csrc/sigma.hip)
+STREAM_ORDER = {MESHRIR_H1: [0, 1, 2, 3, 8, 4, 5, 6, 7]}
 
 
 class FeatSrc(ctypes.Structure):
@@ -101,7 +105,7 @@ def pack_layers(variant, weights, dtype=torch.bfloat16):
     sched = SCHEDULE[variant]
     if len(weights) != len(sched):
         raise ValueError(f"variant {variant} takes {len(sched)} layers, got {len(weights)}")
-    chunks = []
+    layers = []
     for w, (M, K, first, co) in zip(weights, sched):
         if tuple(w.shape) != (M, K):
             raise ValueError(f"layer shape {tuple(w.shape)} != {(M, K)}")
@@ -110,13 +114,16 @@ def pack_layers(variant, weights, dtype=torch.bfloat16):
         wp = torch.zeros(OT * 32 + 1, KS * 16 + 1, dtype=torch.float32, device=w.device)
         wp[:M, :K] = w.detach().float()
         frags = wp[oi, ki].to(dtype)  # [OT, KS, 64, 8]
+        chunks = []
         for c in range(OT // co):
             part = frags[c * co:(c + 1) * co].reshape(-1)
             pad = CHUNK // 2 - part.numel()
             if pad < 0:
                 raise AssertionError("chunk overflow")
             chunks.append(torch.cat([part, part.new_zeros(pad)]))
-    return torch.cat(chunks)
+        layers.append(chunks)
+    order = STREAM_ORDER.get(variant, range(len(layers)))
+    return torch.cat([c for i in order for c in layers[i]])
 
 
 def network_layers(mlp):

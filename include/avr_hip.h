@@ -562,6 +562,17 @@ int avr_das_bwd(int32_t n, const float* steer, const float* angles, const float*
  * launch per 32 tensors. */
 int avr_scale_sanitize(int32_t n_tensors, float* const* ptrs, const int64_t* sizes,
                        const float* coef, void* stream);
+/* clip_grad_norm_'s total 2-norm over n_tensors fp32 gradients (HOST arrays
+ * of device pointers and element counts) and its clamped coefficient
+ * min(max_norm / (total + 1e-6), 1), written to the DEVICE scalars total and
+ * coef without a host sync (the coef argument of avr_scale_sanitize /
+ * avr_adam_step).  One launch per 32 tensors + 1: partial sums of squares
+ * in fixed slots of `workspace` (avr_grad_clip_workspace bytes), summed in a
+ * fixed order (run to run identical; within fp32 rounding of torch's
+ * foreach norm).  A NaN / Inf element makes total NaN / Inf as in torch. */
+int avr_grad_clip_workspace(int32_t n_tensors, const int64_t* sizes, int64_t* bytes);
+int avr_grad_clip_coef(int32_t n_tensors, const float* const* ptrs, const int64_t* sizes, float max_norm,
+                       void* workspace, int64_t workspace_bytes, float* total, float* coef, void* stream);
 /* The same post-processing fused with torch.optim.Adam's update (amsgrad
  * off, L2 weight_decay; avr_runner.py:67-69, 190-200), one pass per element:
  *   g = finite(g*coef) ? g*coef : 0;  g += weight_decay * p;

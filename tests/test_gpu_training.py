@@ -244,3 +244,35 @@ def test_native_adam_many_tensors_and_empty():
         clip_sanitize_adam_(o_mine, max_norm=1)
     for a, b in zip(ref, mine):
         torch.testing.assert_close(b.detach(), a.detach(), rtol=2e-6, atol=2e-7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["plain", "small", "nan", "inf", "many", "empty"])
+def test_native_clip_coef_matches_torch_norm(case):
+    """avr_grad_clip_coef (the fused Adam path's clip coefficient) against
+    torch's foreach norm: equal within fp32 rounding, NaN / Inf propagated as
+    torch does, identical from run to run (fixed summation order)."""
+    from avr_amd.training import _clip_coef, _native_clip_coef
+    g = torch.Generator(device=DEV).manual_seed(11)
+    shapes = {"many": [(s,) for s in range(1, 70)] + [(1 << 20,)], "empty": [(0,), (5,)]}.get(
+        case, [(1 << 21,), (7,), (512, 512), (3, 1000), (1 << 18, 2)])
+    grads = [torch.randn(s, device=DEV, generator=g) * (1e-4 if case == "small" else 0.5) for s in shapes]
+    if case == "nan":
+        grads[2].view(-1)[12345] = float("nan")
+    if case == "inf":
+        grads[0].view(-1)[77] = -float("inf")
+    t_ref, c_ref = _clip_coef(grads, 1.0)
+    t0, c0 = _native_clip_coef(grads, 1.0, DEV)
+    t1, c1 = _native_clip_coef(grads, 1.0, DEV)
+    torch.cuda.synchronize()
+    bits = lambda t: t.view(torch.int32)  # noqa: E731  (NaN == NaN bit for bit)
+    assert torch.equal(bits(t0), bits(t1)) and torch.equal(bits(c0), bits(c1))
+    if case == "nan":
+        assert torch.isnan(t0) and torch.isnan(c0) and torch.isnan(c_ref)
+    elif case == "inf":
+        assert torch.isinf(t0) and float(c0) == 0.0 == float(c_ref)
+    else:
+        torch.testing.assert_close(t0, t_ref.float(), rtol=1e-5, atol=0)
+        torch.testing.assert_close(c0, c_ref.float(), rtol=1e-5, atol=0)
+        if case == "small":
+            assert float(c0) == 1.0

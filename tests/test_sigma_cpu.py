@@ -65,18 +65,20 @@ def run_model(variant, packed, inputs, extras, slope, bias=None, bias_div=1):
     h1_layer = 8 if variant == sigma.MESHRIR_H1 else -1
     xs = None
     h1 = torch.zeros(32, 512)
-    for li, (M, K, first, co) in enumerate(sched):
+    # the chunks in the kernel's stream order (MESHRIR_H1: the signal layer
+    # right after the encoder)
+    for li in sigma.STREAM_ORDER.get(variant, range(len(sched))):
+        M, K, first, co = sched[li]
         OT, KS = -(-M // 32), -(-K // 16)
-        if li == h1_layer:
-            x = xs
-        assert len(x) == KS
+        inp = xs if li == h1_layer else x
+        assert len(inp) == KS
         acc = [torch.zeros(64, 16) for _ in range(OT)]
         for c in range(OT // co):
             fr = chunks[ci][:co * KS * 512].view(co, KS, 64, 8)
             ci += 1
             for o in range(co):
                 for ks in range(KS):
-                    acc[c * co + o] = mfma(fr[o, ks], x[ks], acc[c * co + o])
+                    acc[c * co + o] = mfma(fr[o, ks], inp[ks], acc[c * co + o])
         if li == h1_layer:  # relu(acc + bias) -> h1
             for ot in range(OT):
                 for i in range(16):

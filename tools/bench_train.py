@@ -94,7 +94,12 @@ def main():
     ap.add_argument("--nan-check", action="store_true", help="reference's per-step isnan().item()")
     ap.add_argument("--sync-debug", action="store_true", help="report the torch ops of one step that "
                     "synchronise with the device (torch.cuda.set_sync_debug_mode), with their stacks")
+    ap.add_argument("--torch-norm", action="store_true", help="the fused Adam path's clip coefficient by "
+                    "torch's foreach norm (the round-5 form) instead of avr_grad_clip_coef")
     args = ap.parse_args()
+    if args.torch_norm:
+        from avr_amd import training as _tr
+        _tr._native_clip_coef = lambda grads, max_norm, dev: _tr._clip_coef(grads, max_norm)
     dev = torch.device("cuda", 0)
     w = WORKLOADS[args.workload]
     B, R, S, T = w.batch, w.n_rays, w.n_samples, w.T
