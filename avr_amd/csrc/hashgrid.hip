@@ -440,7 +440,7 @@ int launch_fwd_lm(dim3 grid, hipStream_t st, int64_t N, const float* x, const vo
 //               entries).
 // The workspace holds N * L * 8 contributions at most (12 B each).  Both
 // walks read the upstream gradient level-major (glm, transposed by its own
-// pass first; DESIGN.md §15f).
+// pass first; DESIGN.md §15e).
 constexpr int kPartBits = 10;
 constexpr int kPartEntries = 1 << kPartBits;      // 1024 entries = 8 KB of fp32 pairs (one wave's image)
 constexpr int kBwdGroups = 32;                    // 8-lane groups per 256-thread block
