@@ -1,5 +1,7 @@
 #!/bin/bash
-# Hash-grid backward reduce tiling A/B (partition size, waves per block),
+# Hash-grid backward reduce tiling A/B (partition size, waves per block;
+# variant libraries built by tools/build_ab.sh with -DAVR_HG_PART_BITS /
+# -DAVR_HG_REDUCE_WAVES overrides, removed once the A/B kept the defaults),
 # config-3 and config-4 training points, libraries interleaved in one process.
 set -u
 OUT=gpurun_out/${1:-hgab}
