@@ -433,7 +433,8 @@ int launch_fwd_lm(dim3 grid, hipStream_t st, int64_t N, const float* x, const vo
 //   3. scatter: the same walk writes each contribution (entry within the
 //               partition, value pair) into its partition's segment of a
 //               workspace (partition-contiguous, chunk-ordered segments,
-//               slot order within a chunk free);
+//               slot order within a chunk free), staged in LDS by partition
+//               so the stores are coalesced;
 //   4. reduce:  one wave per partition slice sums its contributions into
 //               an LDS image of the partition and adds the image to the
 //               gradient with plain vector loads/stores (the wave owns those
@@ -603,26 +604,51 @@ constexpr int kDenseSlice = 1024;
 constexpr int kTagRounds = 4;
 constexpr int kHashedSlice = 16384;
 
+// (the plan's level tables in LDS and each thread's totals loaded eight at a
+// time, independent of each other: read from the kernel argument with a
+// per-thread level index and one total per dependent step, this one-block
+// pass took ~12 us per grid)
 __global__ __launch_bounds__(1024) void hg_bwd_plan_kernel(int total_parts, BwdPlan plan,
                                                            const int* __restrict__ totals,
                                                            int* __restrict__ part_start,
                                                            int* __restrict__ slice_base) {
     __shared__ int ws_t[16], ws_s[16];
+    __shared__ int pbase_s[kMaxLevels + 1], hot_s[kMaxLevels], cap_s[kMaxLevels];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x <= kMaxLevels) pbase_s[threadIdx.x] = plan.pbase[threadIdx.x];
+    if (threadIdx.x < kMaxLevels) {
+        hot_s[threadIdx.x] = plan.hot_above[threadIdx.x];
+        cap_s[threadIdx.x] = plan.slice_cap[threadIdx.x];
+    }
+    __syncthreads();
     // thread t owns the `per` consecutive partitions from per * t: one
     // block-wide scan for all of them
     const int per = (total_parts + 1 + 1023) / 1024;
     const int q0 = threadIdx.x * per;
-    int l = 0;
+    int l0 = 0;
+    while (l0 < kMaxLevels && pbase_s[l0 + 1] <= q0) ++l0;
+    // the slices partition q's total t takes
+    auto slices = [&](int t, int l) {
+        const int cap = t > hot_s[l] ? kDenseSlice : cap_s[l];
+        return max(1, (t + cap - 1) / cap);
+    };
     int st = 0, ss = 0;  // this thread's sums
-    for (int j = 0; j < per; ++j) {
-        const int q = q0 + j;
-        if (q >= total_parts) break;
-        const int t = totals[q];
-        while (plan.pbase[l + 1] <= q) ++l;
-        const int cap = t > plan.hot_above[l] ? kDenseSlice : plan.slice_cap[l];
-        st += t;
-        ss += max(1, (t + cap - 1) / cap);
+    int l = l0;
+    for (int j0 = 0; j0 < per; j0 += 8) {
+        int tv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int q = q0 + j0 + u;
+            tv[u] = (j0 + u < per && q < total_parts) ? totals[q] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (tv[u] < 0) break;
+            const int q = q0 + j0 + u;
+            while (pbase_s[l + 1] <= q) ++l;
+            st += tv[u];
+            ss += slices(tv[u], l);
+        }
     }
     int it = st, is = ss;
 #pragma unroll
@@ -644,44 +670,109 @@ __global__ __launch_bounds__(1024) void hg_bwd_plan_kernel(int total_parts, BwdP
         ps += ws_s[w];
     }
     int rt = pt + it - st, rs = ps + is - ss;  // exclusive prefixes at q0
-    l = 0;
-    for (int j = 0; j < per; ++j) {
-        const int q = q0 + j;
-        if (q > total_parts) break;
-        part_start[q] = rt;
-        slice_base[q] = rs;
-        if (q == total_parts) break;
-        const int t = totals[q];
-        while (plan.pbase[l + 1] <= q) ++l;
-        const int cap = t > plan.hot_above[l] ? kDenseSlice : plan.slice_cap[l];
-        rt += t;
-        rs += max(1, (t + cap - 1) / cap);
+    l = l0;
+    for (int j0 = 0; j0 < per; j0 += 8) {
+        int tv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int q = q0 + j0 + u;
+            tv[u] = (j0 + u < per && q < total_parts) ? totals[q] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int q = q0 + j0 + u;
+            if (j0 + u >= per || q > total_parts) break;
+            part_start[q] = rt;
+            slice_base[q] = rs;
+            if (q == total_parts) break;
+            while (pbase_s[l + 1] <= q) ++l;
+            rt += tv[u];
+            rs += slices(tv[u], l);
+        }
     }
 }
+
+// The scatter walk stages the block's merged contributions in LDS, grouped
+// by partition at block-local offsets (the scan of its own counts), and then
+// copies them out in staged order: consecutive lanes store consecutive
+// records of one partition's segment.  Stored straight from the walk, each
+// lane's 12 bytes went to another partition's segment: one cache line per
+// lane and store instruction (issue-bound), and partly written lines
+// (written back as ~1.5x the record bytes).  The staged record carries its
+// partition in the key's upper bits.
+constexpr int kScatMaxRecs = 256 * kBwdRun;  // merged contributions of one block at most
+static_assert(((int64_t)kMaxScatterParts << kPartBits) <= (int64_t(1) << 32), "staged key: partition + entry in 32 bits");
+static_assert((3 * kScatMaxRecs + 3 * kMaxScatterParts + 1) * 4 + 16 <= 160 * 1024, "scatter LDS");
 
 template <typename Tg>
 __global__ __launch_bounds__(256) void hg_bwd_scatter_kernel(int64_t N, int L, const float* __restrict__ x,
                                                              const Tg* __restrict__ gout, LevelTable lt,
                                                              BwdPlan plan, const int* __restrict__ offs,
+                                                             const int* __restrict__ totals,
                                                              const int* __restrict__ part_start,
                                                              uint3* __restrict__ contrib) {
-    extern __shared__ int scat_l[];  // base[P], slot[P]
+    extern __shared__ __attribute__((aligned(16))) int scat_l[];  // stage[3 kScatMaxRecs], base[P], lofs[P + 1], slot[P]
+    __shared__ int wsum[4];
     const int l = blockIdx.y;
     const int pb = plan.pbase[l];
     const int P = plan.pbase[l + 1] - pb;
-    int* base = scat_l;
-    int* slot = scat_l + P;
-    for (int q = threadIdx.x; q < P; q += 256) {
-        base[q] = part_start[pb + q] + offs[(int64_t)(pb + q) * plan.nchunks + blockIdx.x];
+    uint32_t* stage = reinterpret_cast<uint32_t*>(scat_l);
+    int* base = scat_l + 3 * kScatMaxRecs;
+    int* lofs = base + P;
+    int* slot = lofs + P + 1;
+    const int chunk = blockIdx.x, nch = plan.nchunks;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // this chunk's count and global segment start per partition (the scan
+    // pass left exclusive offsets within each partition); E consecutive
+    // partitions per thread
+    const int E = (P + 255) / 256;
+    const int q0 = threadIdx.x * E;
+    int run = 0;
+    for (int j = 0; j < E; ++j) {
+        const int q = q0 + j;
+        if (q >= P) break;
+        const int64_t at = (int64_t)(pb + q) * nch + chunk;
+        const int o = offs[at];
+        const int c = (chunk + 1 < nch ? offs[at + 1] : totals[pb + q]) - o;
+        base[q] = part_start[pb + q] + o;
         slot[q] = 0;
+        lofs[q] = c;  // (the count, until the scan below)
+        run += c;
     }
+    int incl = run;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += u;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int acc = incl - run;
+    for (int w = 0; w < wave; ++w) acc += wsum[w];
+    for (int j = 0; j < E; ++j) {
+        const int q = q0 + j;
+        if (q >= P) break;
+        const int c = lofs[q];
+        lofs[q] = acc;
+        acc += c;
+    }
+    if (threadIdx.x == 0) lofs[P] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
     __syncthreads();
     bwd_walk(N, L, l, x, gout, lt, [&](uint32_t e, float v0, float v1) {
         const int part = (int)(e >> kPartBits);
-        const int pos = base[part] + atomicAdd(&slot[part], 1);
-        // one 12-byte store per contribution: (key, v0, v1)
-        contrib[pos] = make_uint3(e & (kPartEntries - 1), __float_as_uint(v0), __float_as_uint(v1));
+        const int lp = lofs[part] + atomicAdd(&slot[part], 1);
+        stage[3 * lp] = ((uint32_t)part << kPartBits) | (e & (kPartEntries - 1));
+        stage[3 * lp + 1] = __float_as_uint(v0);
+        stage[3 * lp + 2] = __float_as_uint(v1);
     });
+    __syncthreads();
+    const int total = lofs[P];
+    for (int r = threadIdx.x; r < total; r += 256) {
+        const uint32_t s0 = stage[3 * r], s1 = stage[3 * r + 1], s2 = stage[3 * r + 2];
+        const int q = (int)(s0 >> kPartBits);
+        // one 12-byte store per contribution: (key, v0, v1)
+        contrib[base[q] + (r - lofs[q])] = make_uint3(s0 & (kPartEntries - 1), s1, s2);
+    }
 }
 
 // Sum of x over the wave, uniform (DPP within rows of 16, then the four row
@@ -1279,7 +1370,8 @@ int bwd_partitioned(int64_t N, int32_t n_levels, const float* x, const void* gra
     int* totals = reinterpret_cast<int*>(ws + b.totals);
     uint3* contrib = reinterpret_cast<uint3*>(ws + b.contrib);
     const dim3 grid((unsigned)b.plan.nchunks, (unsigned)L);
-    const size_t lds_count = (size_t)b.plan.max_parts * 4, lds_scat = (size_t)b.plan.max_parts * 8;
+    const size_t lds_count = (size_t)b.plan.max_parts * 4;
+    const size_t lds_scat = (size_t)(3 * kScatMaxRecs + 3 * b.plan.max_parts + 1) * 4;
     // every pass below reads the gradient level-major
     const dim3 tgrid((unsigned)((N + 63) / 64));
     void* glm = ws + b.glm;
@@ -1304,10 +1396,10 @@ int bwd_partitioned(int64_t N, int32_t n_levels, const float* x, const void* gra
                        slice_base);
     if (grad_dtype == AVR_DTYPE_F32)
         hipLaunchKernelGGL(hg_bwd_scatter_kernel<float>, grid, dim3(256), lds_scat, st, N, L, x,
-                           (const float*)grad_out, lt, b.plan, counts, part_start, contrib);
+                           (const float*)grad_out, lt, b.plan, counts, totals, part_start, contrib);
     else
         hipLaunchKernelGGL(hg_bwd_scatter_kernel<__half>, grid, dim3(256), lds_scat, st, N, L, x,
-                           (const __half*)grad_out, lt, b.plan, counts, part_start, contrib);
+                           (const __half*)grad_out, lt, b.plan, counts, totals, part_start, contrib);
     if (overwrite)
         hipLaunchKernelGGL(hg_bwd_zero_hot_kernel, dim3((unsigned)b.total_parts), dim3(256), 0, st, lt, b.plan,
                            b.total_parts, slice_base, grad_params);
