@@ -16,7 +16,7 @@ step() {  # name, seconds, command...
 step tests 600 python -u -m pytest tests/test_gpu_hashgrid.py tests/test_gpu_training.py -m gpu -x -q --timeout 300 --timeout-method thread -W ignore
 tail -1 $OUT/tests.log
 for w in c3_raf_furnished_b4 c4_raf_empty_b4_per_gpu; do
-  step xb_$w 300 python tools/xbench_hgbwd.py old=tools/_lib/libab_hg_old.so,cur=avr_amd/libavr_hip.so --workload $w --rounds 6 --iters 10
+  step xb_$w 300 python tools/xbench_hgbwd.py old=tools/_lib/libab_hg_old.so,head=tools/_lib/libab_hg_head.so,cur=avr_amd/libavr_hip.so --workload $w --rounds 6 --iters 10
   grep "^{" $OUT/xb_$w.log
 done
 step train3 300 python tools/bench_train.py --workload c3_raf_furnished_b4 --steps 30
