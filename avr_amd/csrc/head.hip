@@ -1233,12 +1233,13 @@ extern "C" int avr_head_fwd(const avr_render_params* p, int32_t B, int32_t K, co
 
 // the block-sum form of dL/dh (head_bwd_h_blk) serves K % 8 == 0; its dL/dw
 // partials are per 128 features, the scan form's per feature group
-bool hb_blk_ok(int K) { return K % 8 == 0; }
-int hb_parts(const HeadShape& hs, int K) {
-    return hb_blk_ok(K) ? std::max(hs.n_kg, (K + kHbFeat - 1) / kHbFeat) : hs.n_kg;
+// (columns B * S are the grids' z dimension)
+bool hb_blk_ok(int B, int S, int K) { return K % 8 == 0 && (int64_t)B * S <= 65535; }
+int hb_parts(const HeadShape& hs, int B, int S, int K) {
+    return hb_blk_ok(B, S, K) ? std::max(hs.n_kg, (K + kHbFeat - 1) / kHbFeat) : hs.n_kg;
 }
 int64_t hb_sum_floats(int B, int S, int T, int K) {
-    return hb_blk_ok(K) ? (int64_t)B * S * (hb_nblk(T) + 2 * hb_nseg(T)) * K : 0;
+    return hb_blk_ok(B, S, K) ? (int64_t)B * S * (hb_nblk(T) + 2 * hb_nseg(T)) * K : 0;
 }
 
 extern "C" int avr_head_bwd_workspace(const avr_render_params* p, int32_t B, int32_t K, int32_t dtype,
@@ -1251,7 +1252,7 @@ extern "C" int avr_head_bwd_workspace(const avr_render_params* p, int32_t B, int
     dw_groups(hs, B, S, K, &n_sg, &s_per);
     // fp32 partials, then W packed in the backward's feature blocks (16-B
     // aligned), then the block sums of head_bwd_h_blk
-    *bytes = ((int64_t)hb_parts(hs, K) * B * R * S + (int64_t)B * n_sg * T * K) * 4 + 16 +
+    *bytes = ((int64_t)hb_parts(hs, B, S, K) * B * R * S + (int64_t)B * n_sg * T * K) * 4 + 16 +
              (int64_t)T * K * (elem_size(dtype)) + hb_sum_floats(B, S, T, K) * 4 + 16;
     return 0;
 }
@@ -1279,9 +1280,9 @@ extern "C" int avr_head_bwd2(const avr_render_params* p, int32_t B, int32_t K, c
     if (int e = head_shape(*p, B, R, K, elem_size(dtype), &hs)) return e;
     int n_sg, s_per;
     dw_groups(hs, B, S, K, &n_sg, &s_per);
-    const bool blk = hb_blk_ok(K);
+    const bool blk = hb_blk_ok(B, S, K);
     const int n_parts = blk ? (K + kHbFeat - 1) / kHbFeat : hs.n_kg;  // dL/dw partials written
-    const int64_t gw_elems = (int64_t)hb_parts(hs, K) * B * R * S;
+    const int64_t gw_elems = (int64_t)hb_parts(hs, B, S, K) * B * R * S;
     const int64_t gW_elems = (int64_t)B * n_sg * T * K;
     const int64_t es = elem_size(dtype);
     const int64_t sum_floats = hb_sum_floats(B, S, T, K);
