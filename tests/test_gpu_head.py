@@ -46,7 +46,16 @@ CASES = [
     # 16 keys per thread in registers (650 and 1024 rays above: 4)
     ("raf_e_rays", RAF, 48, 24, 16, 510, 64, 1),
     ("many_rays", MESHRIR, 64, 40, 8, 254, 64, 1),
+    # K % 8 != 0: the backward's scan form (csrc/head.hip head_bwd_h_kernel;
+    # every other case takes the block-sum form); no exact head
+    # for K % 16 != 0, so only the linear forms run it
+    ("k12_scan_bwd", SIMU, 8, 4, 24, 4094, 12, 1),  # (T > 2048: feature blocks of 4)
 ]
+
+
+def _skip_inexact(case, exact):
+    if exact and case[6] % 16:
+        pytest.skip("the exact head takes K % 16 == 0")
 
 
 def _operands(case, dtype):
@@ -101,6 +110,7 @@ def test_fused_head_matches_oracle(case, dtype, exact):
     forward and backward.  The backward of both forms differentiates the
     unrounded product, so for the exact form the gradients to attn differ
     from the rounded signal's by the 16-bit rounding (bar 3e-3 at bf16)."""
+    _skip_inexact(case, exact)
     name = case[0]
     ops = _operands(case, dtype)
     cfg, ro, tx, attn, h, W, go = ops
@@ -133,6 +143,7 @@ def test_fused_head_matches_oracle(case, dtype, exact):
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
 def test_fused_head_bitwise_reproducible(case, dtype, exact):
     """Two renders (forward + backward) of the same operands are identical."""
+    _skip_inexact(case, exact)
     ops = _operands(case, dtype)
     a = _fused(case, dtype, ops, exact)
     b = _fused(case, dtype, ops, exact)
@@ -146,6 +157,7 @@ def test_fused_head_matches_plain_render(case, dtype, exact):
     """The fused head against the plain (golden-pinned) render of the
     signal the unfused layer produces: the fp32 product, rounded to the
     16-bit dtype for the exact form."""
+    _skip_inexact(case, exact)
     name, base, n_azi, n_ele, S, T, K, B = case
     cfg, ro, tx, attn, h, W, go = _operands(case, dtype)
     r = AVRRender(None, exact_head=exact, **cfg)
