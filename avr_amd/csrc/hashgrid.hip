@@ -859,8 +859,17 @@ __global__ __launch_bounds__(64 * kReduceWaves) void hg_bwd_reduce_kernel(LevelT
                 // compiler barrier: the read-back must not be folded into the
                 // lane's own write (LDS keeps one wave's accesses in order)
                 asm volatile("" ::: "memory");
-                if (todo && tag[kk[u]] == (uint8_t)lane) {
-                    float2 a = img[kk[u]];
+                // the image entry is read with the tag (one wait, not two):
+                // only this round's winner for a key writes it, after the read
+                int tg = -1;
+                float2 a = make_float2(0.f, 0.f);
+                if (todo) {
+                    tg = tag[kk[u]];
+                    a = img[kk[u]];
+                }
+                // (keeps hipcc from sinking the image read into the branch)
+                asm volatile("" ::"v"(tg), "v"(a.x), "v"(a.y));
+                if (todo && tg == lane) {
                     a.x += v[u].x;
                     a.y += v[u].y;
                     img[kk[u]] = a;
