@@ -159,6 +159,7 @@ _SIGS = {
     "avr_criterion_window_len": (ctypes.c_int, []),
     "avr_criterion_workspace": (ctypes.c_int, [_c_i32, _c_i32, _vp]),
     "avr_criterion_fwd": (ctypes.c_int, [_c_i32, _c_i32] + [_vp] * 10 + [_c_i64, _vp]),
+    "avr_criterion_fwd2": (ctypes.c_int, [_c_i32, _c_i32] + [_vp] * 11 + [_c_i64, _vp]),
     "avr_criterion_bwd": (ctypes.c_int, [_c_i32, _c_i32] + [_vp] * 11 + [_c_i64, _vp, _vp]),
     "avr_das_workspace": (ctypes.c_int, [_vp]),
     "avr_das_fwd": (ctypes.c_int, [_c_i32] + [_vp] * 5 + [_c_f32] * 3 + [_vp, _vp, _c_i64, _vp]),

@@ -66,8 +66,9 @@ def _window_table(dev):
 
 class _CriterionFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, pred, ori, weights):
-        # pred, ori: [B, F, 2] fp32 contiguous device tensors
+    def forward(ctx, pred, ori, weights, with_total=False):
+        # pred, ori: [B, F, 2] fp32 contiguous device tensors; with_total: a
+        # last output, the eight losses' sum (avr_criterion_fwd2)
         B, F = pred.size(0), pred.size(1)
         n = 2 * (F - 1)
         dev = pred.device
@@ -78,17 +79,19 @@ class _CriterionFn(torch.autograd.Function):
         ws = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
         pred_time = torch.empty(B, n, dtype=torch.float32, device=dev)
         ori_time = torch.empty(B, n, dtype=torch.float32, device=dev)
-        losses = torch.empty(8, dtype=torch.float32, device=dev)
+        losses = torch.empty(9 if with_total else 8, dtype=torch.float32, device=dev)
         wts = (ctypes.c_float * 6)(*weights)
         with torch.cuda.device(dev):
-            _lib.call("avr_criterion_fwd", B, F, wts, _ptr(pred), _ptr(ori), _ptr(win),
+            _lib.call("avr_criterion_fwd2", B, F, wts, _ptr(pred), _ptr(ori), _ptr(win),
                       _ptr(tw512), _ptr(irtw), _ptr(pred_time), _ptr(ori_time), _ptr(losses),
-                      _ptr(ws), nbytes, _stream(dev))
+                      _ptr(losses[8:]) if with_total else None, _ptr(ws), nbytes, _stream(dev))
         ctx.save_for_backward(pred, ori, pred_time, ori_time, ws)
         ctx.weights = weights
         ctx.set_materialize_grads(False)
         ls = losses.unbind(0)
         ctx.mark_non_differentiable(ls[6], ls[7], ori_time)
+        if with_total:
+            return (*ls[:8], ori_time, pred_time, ls[8])
         return (*ls, ori_time, pred_time)
 
     @staticmethod
@@ -98,17 +101,24 @@ class _CriterionFn(torch.autograd.Function):
         dev = pred.device
         gl = grads[:6]
         g_pt = grads[9]
-        if all(g is None for g in gl) and g_pt is None:
-            return None, None, None
-        zero = None
-        parts = []
-        for g in gl:
-            if g is None:
-                if zero is None:
-                    zero = torch.zeros((), dtype=torch.float32, device=dev)
-                g = zero
-            parts.append(g.reshape(()).float())
-        g_losses = torch.stack(parts)
+        g_tot = grads[10] if len(grads) > 10 else None
+        if all(g is None for g in gl) and g_pt is None and g_tot is None:
+            return None, None, None, None
+        if all(g is None for g in gl) and g_tot is not None:
+            # d total / d loss_i = 1: each of the six losses gets total's grad
+            g_losses = g_tot.reshape(1).float().expand(6).contiguous()
+        else:
+            zero = None
+            parts = []
+            for g in gl:
+                if g is None:
+                    if zero is None:
+                        zero = torch.zeros((), dtype=torch.float32, device=dev)
+                    g = zero
+                parts.append(g.reshape(()).float())
+            g_losses = torch.stack(parts)
+            if g_tot is not None:
+                g_losses = g_losses + g_tot.reshape(()).float()
         if g_pt is not None:
             g_pt = g_pt.float().contiguous()
         grad_pred = torch.empty_like(pred)
@@ -119,7 +129,7 @@ class _CriterionFn(torch.autograd.Function):
                       _ptr(ori_time), _ptr(g_losses), _ptr(g_pt), _ptr(_window_table(dev)),
                       _ptr(_ir_twiddle(512, dev)), _ptr(_ir_twiddle(n, dev)), _ptr(ws),
                       ws.numel() * 4, _ptr(grad_pred), _stream(dev))
-        return grad_pred, None, None
+        return grad_pred, None, None, None
 
 
 _WS: dict = {}
@@ -176,6 +186,28 @@ class Criterion(nn.Module):
         if pred.shape != ori.shape:
             raise ValueError(f"pred_sig {tuple(pred.shape)} and ori_sig {tuple(ori.shape)} differ")
         out = _CriterionFn.apply(pred, ori, self._weights())
+        return self._with_das(out[:10])
+
+    def forward_total(self, pred_sig, ori_sig):
+        """(forward's ten outputs, total): total = the eight losses added left
+        to right (avr_runner.py:187), from the criterion's own kernel when the
+        DAS terms are off (seven torch adds otherwise)."""
+        if self.das_reg_loss_weight > 0 or self.das_ce_loss_weight > 0:
+            out = self.forward(pred_sig, ori_sig)
+            total = out[0]
+            for x in out[1:8]:
+                total = total + x
+            return out, total
+        if not pred_sig.is_cuda:
+            raise RuntimeError("avr_amd.Criterion needs HIP tensors (no CPU fallback)")
+        pred = _as_spectrum(pred_sig, "pred_sig")
+        ori = _as_spectrum(ori_sig, "ori_sig").detach()
+        if pred.shape != ori.shape:
+            raise ValueError(f"pred_sig {tuple(pred.shape)} and ori_sig {tuple(ori.shape)} differ")
+        out = _CriterionFn.apply(pred, ori, self._weights(), True)
+        return tuple(out[:10]), out[10]
+
+    def _with_das(self, out):
         spec, amp, angle, time, energy, mr, das_reg, das_ce, ori_time, pred_time = out
         if self.das_reg_loss_weight > 0 or self.das_ce_loss_weight > 0:
             from .das import das_losses

@@ -283,7 +283,8 @@ __global__ __launch_bounds__(kRedThreads) void crit_reduce_kernel(CritPlan P,
                                                                   const float* __restrict__ pt,
                                                                   const float* __restrict__ ot,
                                                                   CritWs W,
-                                                                  float* __restrict__ losses) {
+                                                                  float* __restrict__ losses,
+                                                                  float* __restrict__ total) {
     __shared__ float red[6][kRedThreads];
     __shared__ float qsum[4][3];
     const int tid = threadIdx.x;
@@ -386,16 +387,24 @@ __global__ __launch_bounds__(kRedThreads) void crit_reduce_kernel(CritPlan P,
         float esum_all = 0.f;
         for (int b = 0; b < B; ++b) esum_all += W.gtime[(int64_t)b * P.n];
         const float nbf = (float)B * (float)F;
-        losses[0] = (tot[0] / nbf + tot[1] / nbf) * P.w[0];
-        losses[1] = (tot[2] / nbf) * P.w[1];
-        losses[2] = (tot[3] / nbf + tot[4] / nbf) * P.w[2];
-        losses[3] = (tot[5] / ((float)B * (float)n)) * P.w[3];
-        losses[4] = (esum_all / ((float)B * (float)M)) * P.w[4];
+        float l[8];
+        l[0] = (tot[0] / nbf + tot[1] / nbf) * P.w[0];
+        l[1] = (tot[2] / nbf) * P.w[1];
+        l[2] = (tot[3] / nbf + tot[4] / nbf) * P.w[2];
+        l[3] = (tot[5] / ((float)B * (float)n)) * P.w[3];
+        l[4] = (esum_all / ((float)B * (float)M)) * P.w[4];
         float mr = 0.f;
         for (int q = 0; q < 4; ++q) mr += (qsum[q][0] + qsum[q][1]) + qsum[q][2];
-        losses[5] = (mr / 4.0f) * P.w[5];
-        losses[6] = 0.f;  // DAS terms (criterion.py:101-102), filled by the DAS kernels
-        losses[7] = 0.f;
+        l[5] = (mr / 4.0f) * P.w[5];
+        l[6] = 0.f;  // DAS terms (criterion.py:101-102), filled by the DAS kernels
+        l[7] = 0.f;
+        float t = l[0];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            losses[i] = l[i];
+            if (i > 0) t += l[i];  // left to right, as avr_runner.py:187 adds them
+        }
+        if (total) *total = t;
     }
 }
 
@@ -587,6 +596,14 @@ extern "C" int avr_criterion_fwd(int32_t B, int32_t F, const float* weights, con
                                  const float* ori, const float* wtab, const float* tw512,
                                  const float* irtw, float* pred_time, float* ori_time,
                                  float* losses, void* ws, int64_t ws_bytes, void* stream) {
+    return avr_criterion_fwd2(B, F, weights, pred, ori, wtab, tw512, irtw, pred_time, ori_time, losses, nullptr,
+                              ws, ws_bytes, stream);
+}
+
+extern "C" int avr_criterion_fwd2(int32_t B, int32_t F, const float* weights, const float* pred,
+                                  const float* ori, const float* wtab, const float* tw512,
+                                  const float* irtw, float* pred_time, float* ori_time,
+                                  float* losses, float* total, void* ws, int64_t ws_bytes, void* stream) {
     CritPlan P;
     if (int e = make_plan(B, F, weights, &P)) return e;
     AVR_REQUIRE(pred && ori && wtab && tw512 && irtw && pred_time && ori_time && losses && ws,
@@ -601,7 +618,7 @@ extern "C" int avr_criterion_fwd(int32_t B, int32_t F, const float* weights, con
     if (int e = check_launch("crit_stft_kernel")) return e;
     hipLaunchKernelGGL(crit_reduce_kernel, dim3(1), dim3(kRedThreads), 0, as_stream(stream), P,
                        reinterpret_cast<const float2*>(pred), reinterpret_cast<const float2*>(ori),
-                       pred_time, ori_time, W, losses);
+                       pred_time, ori_time, W, losses, total);
     return check_launch("crit_reduce_kernel");
 }
 

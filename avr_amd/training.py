@@ -187,12 +187,11 @@ class TrainStep:
             args.append(direction_tx.to(dev))
         kw = {} if ch_idx is None or int(ch_idx.reshape(-1)[0]) == -1 else {"ch_idx": ch_idx.to(dev)}
         out = self.renderer(*args, **kw)
-        losses = self.criterion(out, ori_sig.to(dev))
+        # total_loss = spec + ... + das_ce (avr_runner.py:187), summed in the
+        # criterion's reduce kernel
+        losses, total = self.criterion.forward_total(out, ori_sig.to(dev))
         if self.nan_check and torch.isnan(losses[4]).item():
             return None  # avr_runner.py:183-185: skip the step
-        total = losses[0]
-        for x in losses[1:8]:
-            total = total + x
         self.optimizer.zero_grad(set_to_none=True)
         total.backward()
         if self.native_adam:

@@ -533,6 +533,14 @@ int avr_criterion_fwd(int32_t B, int32_t F, const float* weights, const float* p
                       const float* ori, const float* wtab, const float* tw512, const float* irtw,
                       float* pred_time, float* ori_time, float* losses, void* workspace,
                       int64_t workspace_bytes, void* stream);
+/* As avr_criterion_fwd, and total[1] (DEVICE, may be NULL) = losses[0] +
+ * losses[1] + ... + losses[7] added left to right, the training loop's
+ * total_loss (avr_runner.py:187) in the same kernel (the reference sums the
+ * eight scalars with seven torch adds). */
+int avr_criterion_fwd2(int32_t B, int32_t F, const float* weights, const float* pred,
+                       const float* ori, const float* wtab, const float* tw512, const float* irtw,
+                       float* pred_time, float* ori_time, float* losses, float* total, void* workspace,
+                       int64_t workspace_bytes, void* stream);
 int avr_criterion_bwd(int32_t B, int32_t F, const float* weights, const float* pred,
                       const float* ori, const float* pred_time, const float* ori_time,
                       const float* grad_losses,

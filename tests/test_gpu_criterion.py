@@ -15,7 +15,7 @@ import pytest
 import torch
 
 from avr_amd.criterion import Criterion
-from criterion_cases import CASES, MESHRIR_W, RAF_W, RENDER, spectra as _spectra
+from criterion_cases import CASES, DAS_BOTH_W, MESHRIR_W, RAF_W, RENDER, spectra as _spectra
 from oracle import criterion_oracle as co
 
 pytestmark = pytest.mark.gpu
@@ -93,6 +93,31 @@ def test_criterion_pred_time_gradient_and_training_sum():
     total = out[0] + out[1] + out[2] + out[3] + out[4] + out[5] + out[6] + out[7]
     (total + (out[9] ** 2).sum()).backward()
     assert _rel(p.grad.cpu(), p_ref.grad) < 1e-3
+
+
+@pytest.mark.parametrize("das", [False, True])
+def test_criterion_forward_total_is_the_training_sum(das):
+    """forward_total's total (the reduce kernel's left-to-right sum, or the
+    torch adds when the DAS terms are on) is bit-identical to avr_runner.py:187's
+    seven adds of the eight losses, its losses to forward's, and the
+    gradient through it to the gradient through the adds."""
+    B, F = (8, 401) if das else (4, 801)
+    pred, ori = _spectra(B, F, 13)
+    crit = Criterion(DAS_BOTH_W if das else RAF_W, RENDER)
+    p1 = pred.to(DEV).requires_grad_(True)
+    out = crit(p1, ori.to(DEV))
+    ref = out[0]
+    for x in out[1:8]:
+        ref = ref + x
+    ref.backward()
+    p2 = pred.to(DEV).requires_grad_(True)
+    out2, total = crit.forward_total(p2, ori.to(DEV))
+    assert len(out2) == 10
+    for i in range(10):
+        assert torch.equal(out2[i], out[i]), i
+    assert torch.equal(total.view(torch.int32), ref.view(torch.int32))
+    total.backward()
+    assert torch.equal(p2.grad.view(torch.int32), p1.grad.view(torch.int32))
 
 
 def test_criterion_identical_spectra():

@@ -96,7 +96,19 @@ def main():
                     "synchronise with the device (torch.cuda.set_sync_debug_mode), with their stacks")
     ap.add_argument("--torch-norm", action="store_true", help="the fused Adam path's clip coefficient by "
                     "torch's foreach norm (the round-5 form) instead of avr_grad_clip_coef")
+    ap.add_argument("--torch-total", action="store_true", help="the loss total by seven torch adds "
+                    "(avr_runner.py:187 as written) instead of the criterion kernel's own sum")
     args = ap.parse_args()
+    if args.torch_total:
+        from avr_amd.criterion import Criterion
+
+        def _torch_total(self, pred_sig, ori_sig):
+            out = self.forward(pred_sig, ori_sig)
+            total = out[0]
+            for x in out[1:8]:
+                total = total + x
+            return out, total
+        Criterion.forward_total = _torch_total
     if args.torch_norm:
         from avr_amd import training as _tr
         _tr._native_clip_coef = lambda grads, max_norm, dev: _tr._clip_coef(grads, max_norm)
