@@ -1205,8 +1205,9 @@ __global__ __launch_bounds__(256) void ray_pose_bias_kernel(int B, int R, int S,
 // flight at once (one L2 round trip per grid instead of one per 8 k), and the
 // pose's tx term computed once for the workgroup's rays.  The same fma chains
 // (k ascending) and the same final sd + st as ray_pose_bias_kernel: the
-// results are equal bit for bit.
-constexpr int kBias2Rays = 8;
+// results are equal bit for bit.  4 rays per workgroup: 256 workgroups for
+// config 2's 1024 rays (15.6 us; 16.4-16.9 with 8 rays and 128 workgroups).
+constexpr int kBias2Rays = 4;
 #ifndef AVR_BIAS_V1  // (A/B: 1 keeps the round-4 kernel for every R)
 #define AVR_BIAS_V1 0
 #endif
